@@ -1,0 +1,111 @@
+// pybind11 bindings of the host-side native pieces (module: _host).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "contours.h"
+
+namespace py = pybind11;
+using namespace ssa;
+
+namespace {
+
+using U8 = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>;
+using I32 = py::array_t<int32_t, py::array::c_style | py::array::forcecast>;
+
+std::vector<Pt> to_pts(const I32& a) {
+  if (a.ndim() != 2 || a.shape(1) != 2) throw std::invalid_argument("points must be (N, 2) int32");
+  std::vector<Pt> p(a.shape(0));
+  auto r = a.unchecked<2>();
+  for (ssize_t i = 0; i < a.shape(0); ++i) p[i] = {r(i, 0), r(i, 1)};
+  return p;
+}
+
+py::array_t<int32_t> from_pts(const std::vector<Pt>& p) {
+  py::array_t<int32_t> a({(ssize_t)p.size(), (ssize_t)2});
+  auto w = a.mutable_unchecked<2>();
+  for (size_t i = 0; i < p.size(); ++i) {
+    w(i, 0) = p[i].x;
+    w(i, 1) = p[i].y;
+  }
+  return a;
+}
+
+py::list find_contours(const U8& mask) {
+  if (mask.ndim() != 2) throw std::invalid_argument("mask must be 2-D");
+  const int H = (int)mask.shape(0), W = (int)mask.shape(1);
+  std::vector<Contour> cs;
+  {
+    py::gil_scoped_release rel;
+    cs = find_contours_tree(mask.data(), H, W, W);
+  }
+  py::list out;
+  for (const Contour& c : cs) {
+    py::dict d;
+    d["points"] = from_pts(c.simple);
+    d["chain"] = from_pts(c.chain);
+    d["is_hole"] = c.is_hole;
+    d["parent"] = c.parent;
+    d["start"] = py::make_tuple(c.start.x, c.start.y);
+    out.append(d);
+  }
+  return out;
+}
+
+py::dict moments(const I32& pts) {
+  Moments m = contour_moments(to_pts(pts));
+  py::dict d;
+  d["m00"] = m.m00;
+  d["m10"] = m.m10;
+  d["m01"] = m.m01;
+  d["a00"] = m.a00;
+  d["a10"] = m.a10;
+  d["a01"] = m.a01;
+  return d;
+}
+
+py::array_t<uint8_t> fill(const I32& pts, int H, int W) {
+  py::array_t<uint8_t> out({(ssize_t)H, (ssize_t)W});
+  std::memset(out.mutable_data(), 0, (size_t)H * W);
+  fill_contour(to_pts(pts), H, W, out.mutable_data());
+  return out;
+}
+
+py::array_t<uint8_t> mask(const U8& labels, const I32& palette, int thr) {
+  if (labels.ndim() != 2) throw std::invalid_argument("labels must be 2-D");
+  if (palette.size() != 256 * 3) throw std::invalid_argument("palette must be (256, 3)");
+  const int h = (int)labels.shape(0), w = (int)labels.shape(1);
+  py::array_t<uint8_t> out({(ssize_t)h, (ssize_t)w});
+  palette_mask(labels.data(), h, w, w, palette.data(), thr, out.mutable_data());
+  return out;
+}
+
+py::list segments(const U8& labels, const I32& palette, double min_area) {
+  if (labels.ndim() != 2) throw std::invalid_argument("labels must be 2-D");
+  if (palette.size() != 256 * 3) throw std::invalid_argument("palette must be (256, 3)");
+  const int h = (int)labels.shape(0), w = (int)labels.shape(1);
+  std::vector<Segment> segs;
+  {
+    py::gil_scoped_release rel;
+    segs = segments_exact(labels.data(), h, w, w, palette.data(), min_area, 256);
+  }
+  py::list out;
+  for (const Segment& s : segs)
+    out.append(py::make_tuple(s.label, s.score, s.area, s.cx, s.cy, s.contour, s.is_hole));
+  return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_host, m) {
+  m.doc() = "Host-side exact contour analysis (Suzuki-Abe border following, OpenCV-equivalent).";
+  m.def("find_contours", &find_contours, py::arg("mask"),
+        "findContours(RETR_TREE, CHAIN_APPROX_SIMPLE) on a 0/nonzero uint8 mask.");
+  m.def("contour_area", [](const I32& p) { return contour_area(to_pts(p)); });
+  m.def("moments", &moments);
+  m.def("fill", &fill, py::arg("points"), py::arg("H"), py::arg("W"));
+  m.def("palette_mask", &mask, py::arg("labels"), py::arg("palette"), py::arg("thr") = 127);
+  m.def("segments", &segments, py::arg("labels"), py::arg("palette"), py::arg("min_area"),
+        "Reference post-processing of one cropped label map -> "
+        "[(label, score, area, cx, cy, contour_index, is_hole)] in contour order.");
+}

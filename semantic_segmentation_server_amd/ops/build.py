@@ -1,0 +1,119 @@
+"""In-tree build of the native extensions.
+
+Two pybind11 modules are produced next to this file:
+
+* ``_host``  — host C++ (g++): exact contour oracle, result ring, etc.
+* ``_hip``   — HIP kernels for gfx950 (hipcc ``--offload-arch=gfx950``) plus their
+  launch wrappers. No torch C++ headers are involved: tensors cross the boundary
+  as raw device pointers and the caller's HIP stream handle, so launches are
+  capturable by ``torch.cuda.CUDAGraph`` (hipGraph) and compile in seconds.
+
+Builds are skipped when a stamp of the sources + flags is unchanged. The
+``.so`` files are git-ignored but travel to the GPU box with the gpurun snapshot.
+"""
+from __future__ import annotations
+
+import glob
+import hashlib
+import os
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+CSRC = os.path.join(ROOT, "csrc")
+EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+ARCH = os.environ.get("SSA_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _pybind_includes():
+    import pybind11
+    return [sysconfig.get_paths()["include"], pybind11.get_include()]
+
+
+def _stamp(files, flags) -> str:
+    h = hashlib.sha256()
+    for f in sorted(files):
+        h.update(f.encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update(" ".join(flags).encode())
+    return h.hexdigest()
+
+
+def _up_to_date(out: str, stamp: str) -> bool:
+    sp = out + ".stamp"
+    return os.path.exists(out) and os.path.exists(sp) and open(sp).read().strip() == stamp
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed ({r.returncode}): {' '.join(cmd)}\n{r.stdout}")
+    return r.stdout
+
+
+def build_host(force: bool = False, verbose: bool = False) -> str:
+    srcs = sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp")))
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "host", "*.h")))
+    out = os.path.join(HERE, "_host" + EXT_SUFFIX)
+    flags = ["-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", "-Wall",
+             "-Wno-sign-compare"]
+    stamp = _stamp(srcs + hdrs, flags)
+    if not force and _up_to_date(out, stamp):
+        return out
+    inc = [f"-I{p}" for p in _pybind_includes() + [os.path.join(CSRC, "host")]]
+    cmd = [os.environ.get("CXX", "g++")] + flags + inc + srcs + ["-o", out + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    _run(cmd)
+    os.replace(out + ".tmp", out)
+    with open(out + ".stamp", "w") as f:
+        f.write(stamp)
+    return out
+
+
+def build_hip(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
+    hip_srcs = sorted(glob.glob(os.path.join(CSRC, "hip", "*.hip")))
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "hip", "*.h")))
+    binding = os.path.join(CSRC, "hip", "bindings.cpp")
+    out = os.path.join(HERE, "_hip" + EXT_SUFFIX)
+    cflags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fno-gpu-rdc",
+              "-Wno-unused-result", "-munsafe-fp-atomics"]
+    stamp = _stamp(hip_srcs + hdrs + [binding], cflags)
+    if not force and _up_to_date(out, stamp):
+        return out
+    bdir = os.path.join(ROOT, "build", "hip")
+    os.makedirs(bdir, exist_ok=True)
+    inc = [f"-I{p}" for p in _pybind_includes() + [os.path.join(CSRC, "hip")]]
+
+    def compile_one(src):
+        obj = os.path.join(bdir, os.path.basename(src) + ".o")
+        lang = ["-x", "hip"] if src.endswith(".hip") else []
+        cmd = [HIPCC] + cflags + inc + lang + ["-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        _run(cmd)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        objs = list(ex.map(compile_one, hip_srcs + [binding]))
+    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}"] + objs + ["-o", out + ".tmp"]
+    _run(cmd)
+    os.replace(out + ".tmp", out)
+    with open(out + ".stamp", "w") as f:
+        f.write(stamp)
+    return out
+
+
+def build_all(force: bool = False, verbose: bool = False):
+    return build_host(force, verbose), build_hip(force, verbose)
+
+
+if __name__ == "__main__":
+    force = "--force" in sys.argv
+    for p in build_all(force=force, verbose=True):
+        print(p)

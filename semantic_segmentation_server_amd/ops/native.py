@@ -1,0 +1,61 @@
+"""Loading of the in-tree native modules.
+
+``host()`` returns the host C++ module, building it on first use if the ``.so`` is
+missing (g++ is always present). ``hip()`` returns the HIP kernel module; it is
+built by ``__graft_entry__.build()`` / ``python -m semantic_segmentation_server_amd.ops.build``
+and, when a GPU is present, its absence is an error — there is no silent eager
+fallback on a GPU box (set ``SSA_ALLOW_TORCH_FALLBACK=1`` to opt into the torch
+reference path explicitly).
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import threading
+
+_lock = threading.Lock()
+_mods = {}
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+def _load(name: str, builder):
+    with _lock:
+        if name in _mods:
+            return _mods[name]
+        try:
+            mod = importlib.import_module(f"semantic_segmentation_server_amd.ops.{name}")
+        except ImportError:
+            if os.environ.get("SSA_NO_AUTOBUILD"):
+                raise
+            builder()
+            mod = importlib.import_module(f"semantic_segmentation_server_amd.ops.{name}")
+        _mods[name] = mod
+        return mod
+
+
+def host():
+    from .build import build_host
+    return _load("_host", build_host)
+
+
+def hip():
+    from .build import build_hip
+    try:
+        return _load("_hip", build_hip)
+    except Exception as e:  # pragma: no cover - exercised on broken installs
+        raise NativeUnavailable(f"HIP extension unavailable: {e}") from e
+
+
+def hip_available() -> bool:
+    try:
+        hip()
+        return True
+    except NativeUnavailable:
+        return False
+
+
+def torch_fallback_allowed() -> bool:
+    return os.environ.get("SSA_ALLOW_TORCH_FALLBACK", "0") == "1"

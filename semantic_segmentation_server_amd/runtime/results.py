@@ -1,0 +1,139 @@
+"""Bounded most-recent-first result buffers.
+
+Reference behaviour (``sem_seg_server.py:27-28,195,225-234``): one global
+``collections.deque`` used as a *stack*. The producer ``appendleft``s every
+accepted contour of a frame in contour order, and ``GetSegmentedObjects`` pops
+exactly ``num_detections`` entries from the left, padding with empty
+``SegmentedObject()`` when the stack runs dry. So the RPC returns the last
+contour of the newest frame first, and records of older frames stay buffered
+until popped. The reference deque is unbounded and relies on GIL atomicity.
+
+Here:
+* Records are plain tuples/ndarray rows of the dtype ``RECORD_DTYPE`` (label id
+  plus normalised score/area/centroid, frame id, stream id, capture time); proto
+  messages are only built inside the RPC for the few records popped.
+* The buffer is bounded (``maxlen``); when full, the *oldest* records are
+  dropped and counted (``drops``). ``maxlen=None`` reproduces the reference's
+  unbounded stack.
+* A lock makes a frame's batch push and an RPC's multi-pop atomic with respect
+  to each other (the reference could interleave them).
+* ``ResultHub`` keeps one buffer per stream (multi-stream config); the v1 RPC
+  reads stream 0 by default or a merged view.
+"""
+from __future__ import annotations
+
+import collections
+import threading
+from typing import Dict, Iterable, List, Optional, Sequence
+
+import numpy as np
+
+RECORD_DTYPE = np.dtype([
+    ("label", np.int32),
+    ("score", np.float32),
+    ("area", np.float32),
+    ("cx", np.float32),
+    ("cy", np.float32),
+    ("stream", np.int32),
+    ("frame", np.int64),
+    ("ts", np.float64),
+])
+
+
+def empty_records(n: int = 0) -> np.ndarray:
+    return np.zeros(n, dtype=RECORD_DTYPE)
+
+
+class ResultBuffer:
+    """Thread-safe bounded LIFO of segment records."""
+
+    def __init__(self, maxlen: Optional[int] = 4096):
+        self._dq: collections.deque = collections.deque(maxlen=maxlen)
+        self._lock = threading.Lock()
+        self.maxlen = maxlen
+        self.pushed = 0
+        self.popped = 0
+        self.drops = 0
+
+    def clear(self) -> None:
+        with self._lock:
+            self._dq.clear()
+
+    def push_frame(self, records: Iterable) -> None:
+        """Push one frame's records in contour order (newest ends up on top)."""
+        with self._lock:
+            for r in records:
+                if self.maxlen is not None and len(self._dq) == self.maxlen:
+                    self.drops += 1
+                self._dq.appendleft(r)
+                self.pushed += 1
+
+    def pop(self, n: int) -> List:
+        """Pop up to ``n`` most recent records (fewer if the buffer runs dry)."""
+        out = []
+        with self._lock:
+            for _ in range(n):
+                if not self._dq:
+                    break
+                out.append(self._dq.popleft())
+            self.popped += len(out)
+        return out
+
+    def peek(self, n: int) -> List:
+        with self._lock:
+            return [self._dq[i] for i in range(min(n, len(self._dq)))]
+
+    def __len__(self) -> int:
+        return len(self._dq)
+
+
+class ResultHub:
+    """One ``ResultBuffer`` per stream id."""
+
+    def __init__(self, num_streams: int = 1, maxlen: Optional[int] = 4096):
+        self.buffers: Dict[int, ResultBuffer] = {
+            s: ResultBuffer(maxlen) for s in range(num_streams)}
+        self.maxlen = maxlen
+        self._lock = threading.Lock()
+
+    def buffer(self, stream: int) -> ResultBuffer:
+        with self._lock:
+            buf = self.buffers.get(stream)
+            if buf is None:
+                buf = self.buffers[stream] = ResultBuffer(self.maxlen)
+            return buf
+
+    def push_records(self, recs: np.ndarray) -> None:
+        """Push a batch of records (any streams/frames), preserving order.
+
+        Records must be ordered by (frame, contour index) within each stream,
+        which is how the post-processing stage emits them.
+        """
+        if len(recs) == 0:
+            return
+        streams = recs["stream"]
+        for s in np.unique(streams):
+            sel = recs[streams == s]
+            self.buffer(int(s)).push_frame(sel)
+
+    @property
+    def depth(self) -> int:
+        return sum(len(b) for b in self.buffers.values())
+
+    @property
+    def drops(self) -> int:
+        return sum(b.drops for b in self.buffers.values())
+
+
+def record_to_proto(rec, labels: Dict[int, str], proto_mod) -> object:
+    from ..labels import label_name
+    return proto_mod.SegmentedObject(
+        label=label_name(labels, int(rec["label"])),
+        score=float(rec["score"]),
+        area=float(rec["area"]),
+        centroid=proto_mod.Centroid(cx=float(rec["cx"]), cy=float(rec["cy"])),
+    )
+
+
+def make_records(rows: Sequence[tuple]) -> np.ndarray:
+    return np.array([tuple(r) for r in rows], dtype=RECORD_DTYPE)

@@ -1,0 +1,185 @@
+"""Frame sources.
+
+Reference: a single ``cv2.VideoCapture(camera_idx)`` read in the producer loop
+(``sem_seg_server.py:144-148``) and probed once at startup for its native
+resolution (``:268-270``); end of stream stops the server. OpenCV is not available
+here, so:
+
+* ``SyntheticSource`` — deterministic BGR frames (moving coloured shapes plus
+  noise) at a given camera resolution; the benchmark source.
+* ``FileSource``     — replays ``.npy`` (N, H, W, 3) uint8 stacks or a directory
+  of images readable by Pillow.
+* ``V4L2Source``     — gated: only if ``cv2`` is importable (camera boxes).
+
+Every source yields ``Frame`` objects and exposes ``resolution`` (w, h). Sources
+are iterators; ``read_batch(n)`` returns a pinned host batch for the engine.
+"""
+from __future__ import annotations
+
+import glob
+import itertools
+import os
+import time
+from dataclasses import dataclass
+from typing import Iterator, List, Optional, Tuple
+
+import numpy as np
+
+
+@dataclass
+class Frame:
+    image: np.ndarray      # (H, W, 3) uint8 BGR
+    frame_id: int
+    stream: int
+    ts: float
+
+
+class FrameSource:
+    resolution: Tuple[int, int] = (0, 0)
+    stream: int = 0
+
+    def __iter__(self) -> Iterator[Frame]:
+        return self
+
+    def __next__(self) -> Frame:  # pragma: no cover
+        raise NotImplementedError
+
+    def read_batch(self, n: int) -> Tuple[np.ndarray, List[int], List[float]]:
+        frames = list(itertools.islice(self, n))
+        if not frames:
+            raise StopIteration
+        imgs = np.stack([f.image for f in frames])
+        return imgs, [f.frame_id for f in frames], [f.ts for f in frames]
+
+    def close(self) -> None:
+        pass
+
+
+class SyntheticSource(FrameSource):
+    """Deterministic synthetic camera.
+
+    Frames are generated from a small pool (``pool``) of pre-rendered images so
+    that producing a frame costs a copy, not a render — the source must not be the
+    bottleneck of a throughput benchmark.
+    """
+
+    def __init__(self, width: int = 640, height: int = 480, stream: int = 0, seed: int = 0,
+                 pool: int = 8, limit: Optional[int] = None, fps: Optional[float] = None):
+        self.resolution = (int(width), int(height))
+        self.stream = stream
+        self.limit = limit
+        self.fps = fps
+        rng = np.random.default_rng(seed + 7919 * stream)
+        self.pool = np.stack([self._render(rng, i) for i in range(max(1, pool))])
+        self._i = 0
+        self._t0 = time.time()
+
+    def _render(self, rng, i) -> np.ndarray:
+        w, h = self.resolution
+        yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+        img = np.zeros((h, w, 3), np.float32)
+        img += rng.uniform(0, 80, 3)
+        for _ in range(6):
+            cx, cy = rng.uniform(0, w), rng.uniform(0, h)
+            rx, ry = rng.uniform(w / 16, w / 3), rng.uniform(h / 16, h / 3)
+            m = ((xx - cx) / rx) ** 2 + ((yy - cy) / ry) ** 2 < 1
+            img[m] = rng.uniform(0, 255, 3)
+        img += rng.normal(0, 8, img.shape)
+        return np.clip(img, 0, 255).astype(np.uint8)
+
+    def __next__(self) -> Frame:
+        if self.limit is not None and self._i >= self.limit:
+            raise StopIteration
+        if self.fps:
+            target = self._t0 + self._i / self.fps
+            dt = target - time.time()
+            if dt > 0:
+                time.sleep(dt)
+        f = Frame(self.pool[self._i % len(self.pool)], self._i, self.stream, time.time())
+        self._i += 1
+        return f
+
+    def read_batch(self, n: int):
+        if self.limit is not None:
+            n = min(n, self.limit - self._i)
+            if n <= 0:
+                raise StopIteration
+        idx = (np.arange(self._i, self._i + n) % len(self.pool))
+        ids = list(range(self._i, self._i + n))
+        self._i += n
+        now = time.time()
+        return self.pool[idx], ids, [now] * n
+
+
+class FileSource(FrameSource):
+    def __init__(self, path: str, stream: int = 0, loop: bool = False):
+        self.stream = stream
+        self.loop = loop
+        if path.endswith(".npy"):
+            self.frames = np.load(path, mmap_mode="r", allow_pickle=False)
+        else:
+            from PIL import Image
+            files = sorted(glob.glob(os.path.join(path, "*")))
+            imgs = [np.asarray(Image.open(f).convert("RGB"))[..., ::-1] for f in files]
+            self.frames = np.stack(imgs)
+        if self.frames.ndim != 4 or self.frames.shape[-1] != 3:
+            raise ValueError("expected (N, H, W, 3) frames")
+        self.resolution = (int(self.frames.shape[2]), int(self.frames.shape[1]))
+        self._i = 0
+
+    def __next__(self) -> Frame:
+        if self._i >= len(self.frames):
+            if not self.loop:
+                raise StopIteration
+            self._i = 0
+        f = Frame(np.asarray(self.frames[self._i]), self._i, self.stream, time.time())
+        self._i += 1
+        return f
+
+
+class V4L2Source(FrameSource):  # pragma: no cover - needs a camera and cv2
+    def __init__(self, camera_idx: int, stream: int = 0):
+        import cv2  # gated: not installed in the build image
+        self.cap = cv2.VideoCapture(camera_idx)
+        self.stream = stream
+        self.resolution = (int(self.cap.get(cv2.CAP_PROP_FRAME_WIDTH)),
+                           int(self.cap.get(cv2.CAP_PROP_FRAME_HEIGHT)))
+        self._i = 0
+
+    def __next__(self) -> Frame:
+        ok, img = self.cap.read()
+        if not ok:
+            raise StopIteration
+        f = Frame(img, self._i, self.stream, time.time())
+        self._i += 1
+        return f
+
+    def close(self):
+        self.cap.release()
+
+
+def probe_resolution(kind: str, camera_idx: int = 1, width: int = 640, height: int = 480,
+                     path: Optional[str] = None) -> Tuple[int, int]:
+    """Native resolution of a source (reference probes the camera once, ``:268-270``)."""
+    if kind == "synthetic":
+        return (width, height)
+    if kind == "file":
+        return FileSource(path).resolution
+    if kind == "camera":
+        src = V4L2Source(camera_idx)
+        res = src.resolution
+        src.close()
+        return res
+    raise ValueError(kind)
+
+
+def make_source(kind: str, stream: int = 0, camera_idx: int = 1, width: int = 640,
+                height: int = 480, path: Optional[str] = None, limit: Optional[int] = None,
+                fps: Optional[float] = None, seed: int = 0) -> FrameSource:
+    if kind == "synthetic":
+        return SyntheticSource(width, height, stream, seed=seed, limit=limit, fps=fps)
+    if kind == "file":
+        return FileSource(path, stream, loop=limit is None)
+    if kind == "camera":
+        return V4L2Source(camera_idx + stream, stream)
+    raise ValueError(kind)
