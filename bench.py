@@ -1,0 +1,196 @@
+#!/usr/bin/env python3
+"""Headline benchmark: frames/sec (whole node) + p50 GetSegmentedObjects latency.
+
+Config (BASELINE.json): DeepLabv3-MobileNetV2, 513x513, PASCAL VOC (21 classes),
+bf16, synthetic 640x480 BGR camera frames, random-init weights. One process per
+GPU (torchrun); per-rank batch ``--batch`` (default 32) => weak scaling.
+
+One timed step, on every rank:
+  H2D of the rank's next frames (pinned, copy stream, overlapped) or the rank-0
+  upload + RCCL scatter (``--ingest scatter``)
+  -> hipGraph replay: letterbox/normalise + DeepLabv3 + upsample/argmax + mask +
+     CCL + contour statistics -> packed records
+  -> RCCL gather of records to rank 0 -> D2H -> push into the LIFO result hub.
+
+After the timed region, rank 0 serves the hub over gRPC on loopback and a client
+subprocess measures GetSegmentedObjects latency while all ranks keep stepping
+(the RPC is served under inference load, as in production).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+BASELINE_METRIC = "frames/sec (whole node) + p50 GetSegmentedObjects latency, 513x513 PASCAL VOC"
+
+
+def _client_proc(port: int, n: int, conn) -> None:
+    try:
+        from semantic_segmentation_server_amd.client import rpc_latency
+        conn.send(rpc_latency(f"127.0.0.1:{port}", n=n, warmup=min(200, n)))
+    except Exception as e:  # pragma: no cover
+        conn.send({"error": repr(e)})
+    conn.close()
+
+
+def main() -> int:
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
+    p.add_argument("--backend", choices=["hip", "torch"], default="hip")
+    p.add_argument("--arch", default="mnv2")
+    p.add_argument("--aspp", default="full")
+    p.add_argument("--input_size", type=int, default=513)
+    p.add_argument("--camera", default="640x480")
+    p.add_argument("--ingest", choices=["local", "scatter"], default="local")
+    p.add_argument("--contour_mode", choices=["fast", "exact", "none"], default="fast")
+    p.add_argument("--no-graph", dest="graph", action="store_false")
+    p.add_argument("--rpc", type=int, default=2000, help="GetSegmentedObjects calls to time (0: skip)")
+    p.add_argument("--dtype", default="bf16")
+    a = p.parse_args()
+
+    import numpy as np
+    import torch
+    from semantic_segmentation_server_amd import config as C
+    from semantic_segmentation_server_amd.parallel import dist as D
+    from semantic_segmentation_server_amd.parallel.dp import DataParallelPipeline
+    from semantic_segmentation_server_amd.runtime.engine import Engine
+    from semantic_segmentation_server_amd.runtime.results import ResultHub
+    from semantic_segmentation_server_amd.runtime.sources import SyntheticSource
+
+    ctx = D.init()
+    cam_w, cam_h = (int(v) for v in a.camera.split("x"))
+    cfg = C.Config(arch=a.arch, aspp=a.aspp, input_size=a.input_size, backend=a.backend,
+                   dtype=a.dtype, batch=a.batch, graph=a.graph, contour_mode=a.contour_mode,
+                   ingest=a.ingest, camera_width=cam_w, camera_height=cam_h,
+                   num_classes=21 if a.arch == "mnv2" else 19,
+                   dataset="pascal" if a.arch == "mnv2" else "cityscapes")
+    engine = Engine(cfg, ctx.device)
+    hub = ResultHub(ctx.world, maxlen=4096) if ctx.is_root else None
+    pipe = DataParallelPipeline(ctx, engine, cam_w, cam_h, a.batch, a.ingest, hub)
+
+    # synthetic camera frames, pinned; distinct per rank
+    src = SyntheticSource(cam_w, cam_h, stream=ctx.rank, seed=1, pool=max(2, min(a.batch, 8)))
+    nb = a.batch * (ctx.world if (a.ingest == "scatter" and ctx.is_root) else 1)
+    host_batches = []
+    for k in range(2):
+        frames, _, _ = src.read_batch(nb)
+        host_batches.append(torch.from_numpy(np.ascontiguousarray(frames)).pin_memory()
+                            if ctx.device.type == "cuda" else torch.from_numpy(frames.copy()))
+
+    verbose = os.environ.get("SSA_BENCH_VERBOSE", "0") == "1"
+
+    def run_steps(n: int, k0: int = 0) -> None:
+        for k in range(n):
+            pipe.prefetch(host_batches[(k0 + k) % 2])
+            pipe.step()
+            if verbose:
+                print(f"[rank {ctx.rank}] step {k0 + k} ok", file=sys.stderr, flush=True)
+
+    sync = (lambda: torch.cuda.synchronize(ctx.device)) if ctx.device.type == "cuda" else (lambda: None)
+    t_w0 = time.perf_counter()
+    run_steps(a.warmup)
+    sync()
+    warm_s = time.perf_counter() - t_w0
+    D.barrier(ctx)
+    sync()
+    t0 = time.perf_counter()
+    run_steps(a.steps, a.warmup)
+    sync()
+    D.barrier(ctx)
+    sync()
+    dt = time.perf_counter() - t0
+    dt = D.allreduce_max(ctx, dt)
+
+    frames_total = a.steps * a.batch * ctx.world
+    fps = frames_total / dt
+    records = pipe.records_out
+
+    rpc = None
+    if a.rpc > 0:
+        rpc = _rpc_under_load(ctx, pipe, hub, run_steps, a.rpc, D)
+
+    if ctx.is_root:
+        out = {
+            "metric": BASELINE_METRIC,
+            "value": round(fps, 2),
+            "unit": "frames/s",
+            "n_gpus": ctx.world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(dt / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": a.dtype,
+            "data": "synthetic 640x480 BGR frames, random-init weights",
+            "config": {
+                "model": "DeepLabv3-MobileNetV2" if a.arch == "mnv2" else "DeepLabv3-ResNet50",
+                "aspp": a.aspp,
+                "global_batch": a.batch * ctx.world,
+                "per_gpu_batch": a.batch,
+                "seq_len": a.input_size,
+                "input": f"{a.input_size}x{a.input_size}",
+                "camera": a.camera,
+                "classes": cfg.num_classes,
+                "parallelism": f"dp{ctx.world}",
+                "ingest": a.ingest,
+                "backend": a.backend,
+                "hipgraph": bool(a.graph and ctx.device.type == "cuda"),
+                "contour_mode": a.contour_mode,
+            },
+            "p50_get_segmented_objects_ms": rpc.get("p50_ms") if rpc else None,
+            "p99_get_segmented_objects_ms": rpc.get("p99_ms") if rpc else None,
+            "records_per_frame": round(records / max(1, pipe.frames_done), 4),
+            "warmup_s": round(warm_s, 2),
+        }
+        print(json.dumps(out), flush=True)
+    D.destroy(ctx)
+    return 0
+
+
+def _rpc_under_load(ctx, pipe, hub, run_steps, n_calls, D):
+    """Rank 0 serves the hub; a client subprocess times GetSegmentedObjects while
+    every rank keeps running pipeline steps. Returns the client's stats on rank 0."""
+    import torch
+    server = None
+    parent = None
+    proc = None
+    if ctx.is_root:
+        from semantic_segmentation_server_amd.api import service as S
+        from semantic_segmentation_server_amd.labels import load_labels
+        server, port = S.make_server(8, 0, "127.0.0.1")
+        S.add_v1_servicer(S.SemanticSegmentationServicer(hub, load_labels(), 3, pipe.cam), server)
+        server.start()
+        mpctx = mp.get_context("spawn")
+        parent, child = mpctx.Pipe()
+        proc = mpctx.Process(target=_client_proc, args=(port, n_calls, child), daemon=True)
+        proc.start()
+    k = 0
+    t_end = time.time() + 120
+    while True:
+        done = 1.0 if (ctx.is_root and (parent.poll() or time.time() > t_end)) else 0.0
+        if D.allreduce_max(ctx, done) > 0:
+            break
+        run_steps(1, k)
+        k += 1
+    res = None
+    if ctx.is_root:
+        res = parent.recv() if parent.poll(60) else {"error": "client timeout"}
+        proc.join(10)
+        server.stop(0)
+        res["load_steps"] = k
+    return res
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,87 @@
+// pybind11 bindings of the gfx950 kernels (module: _hip). Arguments are raw
+// device pointers (Python ints from tensor.data_ptr()) and a HIP stream handle
+// (torch.cuda.current_stream().cuda_stream), so every launch lands on the
+// caller's stream and is captured by an enclosing hipGraph capture. Shape checks
+// live in the Python wrappers (semantic_segmentation_server_amd/ops/hip_ops.py).
+#include <pybind11/pybind11.h>
+
+#include "kernels.h"
+
+namespace py = pybind11;
+using namespace ssa;
+
+namespace {
+template <class T>
+T* P(uintptr_t v) { return reinterpret_cast<T*>(v); }
+hipStream_t S(uintptr_t v) { return reinterpret_cast<hipStream_t>(v); }
+}  // namespace
+
+PYBIND11_MODULE(_hip, m) {
+  m.doc() = "gfx950 HIP kernels for DeepLabv3 inference and contour statistics";
+
+  m.def("conv_gemm",
+        [](uintptr_t in, uintptr_t w, uintptr_t bias, uintptr_t img_bias, uintptr_t res,
+           uintptr_t out, int B, int IH, int IW, int Cin, int OH, int OW, int Cout, int KH, int KW,
+           int stride, int dil, int ldo, int co_off, int ldr, int act, uintptr_t stream) {
+          ConvParams p;
+          p.in = P<const bf16>(in); p.w = P<const bf16>(w); p.bias = P<const float>(bias);
+          p.img_bias = P<const float>(img_bias); p.res = P<const bf16>(res); p.out = P<bf16>(out);
+          p.B = B; p.IH = IH; p.IW = IW; p.Cin = Cin; p.OH = OH; p.OW = OW; p.Cout = Cout;
+          p.KH = KH; p.KW = KW; p.stride = stride; p.dil = dil; p.ldo = ldo; p.co_off = co_off;
+          p.ldr = ldr; p.act = act;
+          conv_gemm(p, S(stream));
+        });
+
+  m.def("depthwise3x3",
+        [](uintptr_t in, uintptr_t w, uintptr_t bias, uintptr_t out, int B, int IH, int IW, int C,
+           int OH, int OW, int stride, int dil, int act, uintptr_t stream) {
+          depthwise3x3(P<const bf16>(in), P<const float>(w), P<const float>(bias), P<bf16>(out), B,
+                       IH, IW, C, OH, OW, stride, dil, act, S(stream));
+        });
+
+  m.def("stem_conv",
+        [](uintptr_t frames, uintptr_t lut_x, uintptr_t lut_y, uintptr_t w, uintptr_t bias,
+           uintptr_t out, int B, int Hc, int Wc, int H, int W, int OH, int OW, int Cout, int K,
+           int stride, int act, uintptr_t stream) {
+          stem_conv(P<const uint8_t>(frames), P<const int32_t>(lut_x), P<const int32_t>(lut_y),
+                    P<const float>(w), P<const float>(bias), P<bf16>(out), B, Hc, Wc, H, W, OH, OW,
+                    Cout, K, stride, act, S(stream));
+        });
+
+  m.def("maxpool3x3s2", [](uintptr_t in, uintptr_t out, int B, int IH, int IW, int C, int OH,
+                           int OW, uintptr_t stream) {
+    maxpool3x3s2(P<const bf16>(in), P<bf16>(out), B, IH, IW, C, OH, OW, S(stream));
+  });
+
+  m.def("global_avgpool", [](uintptr_t in, uintptr_t out, int B, int HW, int C, uintptr_t stream) {
+    global_avgpool(P<const bf16>(in), P<float>(out), B, HW, C, S(stream));
+  });
+
+  m.def("matvec", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t out, int B, int N, int K,
+                     int act, uintptr_t stream) {
+    matvec(P<const float>(x), P<const float>(w), P<const float>(bias), P<float>(out), B, N, K, act,
+           S(stream));
+  });
+
+  m.def("upsample_argmax", [](uintptr_t logits, uintptr_t labels, int B, int h, int w, int K,
+                              int ldk, int H, int W, uintptr_t stream) {
+    upsample_argmax(P<const bf16>(logits), P<uint8_t>(labels), B, h, w, K, ldk, H, W, S(stream));
+  });
+
+  m.def("post_workspace_bytes", &post_workspace_bytes);
+  m.def("postprocess",
+        [](uintptr_t labels, int B, int H, int W, int crop_h, int crop_w, uintptr_t palette,
+           int thr, double min_area, int num_bins, int K, uintptr_t ws, uintptr_t records,
+           uintptr_t stream) {
+          PostParams p;
+          p.labels = P<const uint8_t>(labels); p.B = B; p.H = H; p.W = W;
+          p.crop_h = crop_h; p.crop_w = crop_w; p.palette = P<const int32_t>(palette);
+          p.thr = thr; p.min_area = min_area; p.num_bins = num_bins; p.K = K;
+          p.ws = P<void>(ws); p.records = P<float>(records);
+          postprocess(p, S(stream));
+        });
+
+  m.attr("ACT_NONE") = (int)ACT_NONE;
+  m.attr("ACT_RELU") = (int)ACT_RELU;
+  m.attr("ACT_RELU6") = (int)ACT_RELU6;
+}

@@ -1,0 +1,70 @@
+// Host launch interfaces of the gfx950 kernels. Every launcher takes raw device
+// pointers plus the caller's stream, performs no allocation and no host sync, and
+// is therefore capturable into a hipGraph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+
+namespace ssa {
+
+struct ConvParams {
+  const bf16* in = nullptr;      // [B, IH, IW, Cin] NHWC
+  const bf16* w = nullptr;       // [Cout, KH, KW, Cin]
+  const float* bias = nullptr;   // [Cout]
+  const float* img_bias = nullptr;  // optional [B, Cout], added per image
+  const bf16* res = nullptr;     // optional residual [B, OH, OW, ldr]
+  bf16* out = nullptr;           // [B, OH, OW, ldo], written at channel offset co_off
+  int B = 0, IH = 0, IW = 0, Cin = 0, OH = 0, OW = 0, Cout = 0;
+  int KH = 1, KW = 1, stride = 1, dil = 1;
+  int ldo = 0, co_off = 0, ldr = 0, act = 0;
+};
+void conv_gemm(const ConvParams& p, hipStream_t s);
+
+// Depthwise KxK (K=3) conv, NHWC, pad = dil, bias + act. w: [9, C] fp32.
+void depthwise3x3(const bf16* in, const float* w, const float* bias, bf16* out, int B, int IH,
+                  int IW, int C, int OH, int OW, int stride, int dil, int act, hipStream_t s);
+
+// Fused letterbox preprocess + stem conv: uint8 BGR frames [B, Hc, Wc, 3] ->
+// model pixel (y, x) = frame[lut_y[y], lut_x[x]] (or 0 where a lut is -1), RGB,
+// x/127.5 - 1 -> KxK stride-s conv (pad K/2) 3 -> Cout, bias + act, NHWC bf16.
+// w: [K*K*3, Cout] fp32 (tap-major, then input channel).
+void stem_conv(const uint8_t* frames, const int32_t* lut_x, const int32_t* lut_y, const float* w,
+               const float* bias, bf16* out, int B, int Hc, int Wc, int H, int W, int OH, int OW,
+               int Cout, int K, int stride, int act, hipStream_t s);
+
+// 3x3 stride-2 pad-1 max pool, NHWC bf16 (ResNet stem).
+void maxpool3x3s2(const bf16* in, bf16* out, int B, int IH, int IW, int C, int OH, int OW,
+                  hipStream_t s);
+
+// Global average pool NHWC bf16 [B, H, W, C] -> fp32 [B, C].
+void global_avgpool(const bf16* in, float* out, int B, int HW, int C, hipStream_t s);
+
+// out[b, n] = act(sum_k W[n, k] * x[b, k] + bias[n]), fp32 everywhere (tiny).
+void matvec(const float* x, const float* w, const float* bias, float* out, int B, int N, int K,
+            int act, hipStream_t s);
+
+// Bilinear (align_corners=True) upsample of NHWC bf16 logits [B, h, w, ldk]
+// (first K channels valid) to H x W, then per-pixel argmax -> uint8 [B, H, W].
+void upsample_argmax(const bf16* logits, uint8_t* labels, int B, int h, int w, int K, int ldk,
+                     int H, int W, hipStream_t s);
+
+// ---- post-processing (postprocess.hip) -------------------------------------
+struct PostParams {
+  const uint8_t* labels = nullptr;  // [B, H, W] model-resolution label maps
+  int B = 0, H = 0, W = 0;          // model resolution (row stride W)
+  int crop_h = 0, crop_w = 0;       // letterboxed valid region
+  const int32_t* palette = nullptr; // [256, 3] RGB
+  int thr = 127;
+  double min_area = 0.0;            // pixels^2 (reference: ratio * H * W)
+  int num_bins = 32;                // histogram bins (class ids < num_bins)
+  int K = 64;                       // record slots per frame
+  // workspace (caller-allocated, sizes from post_workspace_bytes)
+  void* ws = nullptr;
+  float* records = nullptr;         // [B, 1 + 5K] packed output
+};
+size_t post_workspace_bytes(int B, int H, int W, int K, int num_bins);
+void postprocess(const PostParams& p, hipStream_t s);
+
+}  // namespace ssa

@@ -1,0 +1,318 @@
+// Memory-bound model kernels for gfx950: depthwise conv, fused preprocess+stem,
+// max pool, global average pool, small matvec, fused bilinear upsample + argmax.
+// All NHWC bf16 with 16-byte vector accesses along channels (8 bf16 per lane).
+#include "common.h"
+#include "kernels.h"
+
+namespace ssa {
+
+// ---------------------------------------------------------------- depthwise
+// One lane = one output pixel x 8 channels; a wave covers 64 channel groups of
+// consecutive pixels, so loads/stores are 16 B per lane and contiguous.
+__global__ __launch_bounds__(256) void dw3x3_kernel(const bf16* __restrict__ in,
+                                                    const float* __restrict__ w,
+                                                    const float* __restrict__ bias,
+                                                    bf16* __restrict__ out, int B, int IH, int IW,
+                                                    int C, int OH, int OW, int stride, int dil,
+                                                    int act) {
+  const int CG = C >> 3;
+  const long long total = (long long)B * OH * OW * CG;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int cg = (int)(t % CG);
+    long long pix = t / CG;
+    const int ox = (int)(pix % OW);
+    pix /= OW;
+    const int oy = (int)(pix % OH);
+    const int b = (int)(pix / OH);
+    const int c = cg * 8;
+    float acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = bias[c + q];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int iy = oy * stride + (ky - 1) * dil;
+      if (iy < 0 || iy >= IH) continue;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int ix = ox * stride + (kx - 1) * dil;
+        if (ix < 0 || ix >= IW) continue;
+        const bf16x8 v = ld8(in + (((long long)b * IH + iy) * IW + ix) * C + c);
+        const float4 w0 = *reinterpret_cast<const float4*>(w + (ky * 3 + kx) * C + c);
+        const float4 w1 = *reinterpret_cast<const float4*>(w + (ky * 3 + kx) * C + c + 4);
+        acc[0] += (float)v[0] * w0.x; acc[1] += (float)v[1] * w0.y;
+        acc[2] += (float)v[2] * w0.z; acc[3] += (float)v[3] * w0.w;
+        acc[4] += (float)v[4] * w1.x; acc[5] += (float)v[5] * w1.y;
+        acc[6] += (float)v[6] * w1.z; acc[7] += (float)v[7] * w1.w;
+      }
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = (bf16)apply_act(acc[q], act);
+    st8(out + t * 8, o);
+  }
+}
+
+void depthwise3x3(const bf16* in, const float* w, const float* bias, bf16* out, int B, int IH,
+                  int IW, int C, int OH, int OW, int stride, int dil, int act, hipStream_t s) {
+  if (C % 8) throw std::invalid_argument("depthwise3x3: C must be a multiple of 8");
+  const long long total = (long long)B * OH * OW * (C / 8);
+  const int grid = (int)std::min<long long>(cdiv(total, 256), 256LL * 32);
+  hipLaunchKernelGGL(dw3x3_kernel, dim3(grid), dim3(256), 0, s, in, w, bias, out, B, IH, IW, C,
+                     OH, OW, stride, dil, act);
+  check_launch("depthwise3x3");
+}
+
+// ---------------------------------------------------------------- stem
+// One lane = one output pixel x all Cout channels. The letterbox LUT turns the
+// uint8 camera frame into the normalised model input on the fly, so the
+// preprocessed 513x513x3 tensor is never materialised. Weights live in LDS.
+template <int COUT>
+__global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ frames,
+                                                   const int32_t* __restrict__ lut_x,
+                                                   const int32_t* __restrict__ lut_y,
+                                                   const float* __restrict__ w,
+                                                   const float* __restrict__ bias,
+                                                   bf16* __restrict__ out, int B, int Hc, int Wc,
+                                                   int H, int W, int OH, int OW, int K,
+                                                   int stride, int act) {
+  extern __shared__ __attribute__((aligned(16))) float sw[];  // [K*K*3][COUT] + bias
+  const int nw = K * K * 3 * COUT;
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) sw[i] = w[i];
+  for (int i = threadIdx.x; i < COUT; i += blockDim.x) sw[nw + i] = bias[i];
+  __syncthreads();
+  const long long total = (long long)B * OH * OW;
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int ox = (int)(t % OW);
+  const int oy = (int)((t / OW) % OH);
+  const int b = (int)(t / ((long long)OW * OH));
+  float acc[COUT];
+#pragma unroll
+  for (int n = 0; n < COUT; ++n) acc[n] = sw[nw + n];
+  const int pad = K / 2;
+  const uint8_t* fb = frames + (long long)b * Hc * Wc * 3;
+  for (int ky = 0; ky < K; ++ky) {
+    const int y = oy * stride + ky - pad;
+    if (y < 0 || y >= H) continue;  // conv zero padding (outside the model input)
+    const int sy = lut_y[y];
+    for (int kx = 0; kx < K; ++kx) {
+      const int x = ox * stride + kx - pad;
+      if (x < 0 || x >= W) continue;
+      const int sx = lut_x[x];
+      float rgb[3];
+      if (sy >= 0 && sx >= 0) {
+        const uint8_t* px = fb + ((long long)sy * Wc + sx) * 3;
+        rgb[0] = px[2] * (1.f / 127.5f) - 1.f;  // BGR -> RGB
+        rgb[1] = px[1] * (1.f / 127.5f) - 1.f;
+        rgb[2] = px[0] * (1.f / 127.5f) - 1.f;
+      } else {  // letterbox padding: uint8 zero -> -1
+        rgb[0] = rgb[1] = rgb[2] = -1.f;
+      }
+      const float* wt = sw + ((ky * K + kx) * 3) * COUT;
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int n = 0; n < COUT; ++n) acc[n] += rgb[c] * wt[c * COUT + n];
+    }
+  }
+  bf16* op = out + t * COUT;
+#pragma unroll
+  for (int n = 0; n < COUT; n += 8) {
+    bf16x8 o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = (bf16)apply_act(acc[n + q], act);
+    st8(op + n, o);
+  }
+}
+
+void stem_conv(const uint8_t* frames, const int32_t* lut_x, const int32_t* lut_y, const float* w,
+               const float* bias, bf16* out, int B, int Hc, int Wc, int H, int W, int OH, int OW,
+               int Cout, int K, int stride, int act, hipStream_t s) {
+  const long long total = (long long)B * OH * OW;
+  const size_t lds = (size_t)(K * K * 3 * Cout + Cout) * sizeof(float);
+  const int grid = cdiv(total, 256);
+#define STEM_CASE(C)                                                                          \
+  case C:                                                                                     \
+    hipLaunchKernelGGL(stem_kernel<C>, dim3(grid), dim3(256), lds, s, frames, lut_x, lut_y, w, \
+                       bias, out, B, Hc, Wc, H, W, OH, OW, K, stride, act);                  \
+    break;
+  switch (Cout) {
+    STEM_CASE(16)
+    STEM_CASE(24)
+    STEM_CASE(32)
+    STEM_CASE(48)
+    STEM_CASE(64)
+    default:
+      throw std::invalid_argument("stem_conv: unsupported Cout");
+  }
+#undef STEM_CASE
+  check_launch("stem_conv");
+}
+
+// ---------------------------------------------------------------- max pool
+__global__ void maxpool_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, int B, int IH,
+                               int IW, int C, int OH, int OW) {
+  const int CG = C >> 3;
+  const long long total = (long long)B * OH * OW * CG;
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int cg = (int)(t % CG);
+  long long pix = t / CG;
+  const int ox = (int)(pix % OW);
+  pix /= OW;
+  const int oy = (int)(pix % OH);
+  const int b = (int)(pix / OH);
+  float m[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) m[q] = -3.0e38f;
+  for (int ky = 0; ky < 3; ++ky) {
+    const int iy = oy * 2 + ky - 1;
+    if (iy < 0 || iy >= IH) continue;
+    for (int kx = 0; kx < 3; ++kx) {
+      const int ix = ox * 2 + kx - 1;
+      if (ix < 0 || ix >= IW) continue;
+      const bf16x8 v = ld8(in + (((long long)b * IH + iy) * IW + ix) * C + cg * 8);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) m[q] = fmaxf(m[q], (float)v[q]);
+    }
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) o[q] = (bf16)m[q];
+  st8(out + t * 8, o);
+}
+
+void maxpool3x3s2(const bf16* in, bf16* out, int B, int IH, int IW, int C, int OH, int OW,
+                  hipStream_t s) {
+  const long long total = (long long)B * OH * OW * (C / 8);
+  hipLaunchKernelGGL(maxpool_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, in, out, B, IH, IW,
+                     C, OH, OW);
+  check_launch("maxpool3x3s2");
+}
+
+// ---------------------------------------------------------------- GAP
+// grid (B, C/8/64 blocks): each lane owns 8 channels and strides over pixels;
+// the 4 waves of a block split the pixels and reduce through LDS.
+__global__ __launch_bounds__(256) void gap_kernel(const bf16* __restrict__ in,
+                                                  float* __restrict__ out, int HW, int C) {
+  const int b = blockIdx.x;
+  const int CG = C >> 3;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int cg = blockIdx.y * 64 + lane;
+  __shared__ float part[4][64][8];
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (cg < CG) {
+    const bf16* base = in + (long long)b * HW * C + cg * 8;
+    for (int p = wid; p < HW; p += 4) {
+      const bf16x8 v = ld8(base + (long long)p * C);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += (float)v[q];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) part[wid][lane][q] = acc[q];
+  __syncthreads();
+  if (wid == 0 && cg < CG) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float s = part[0][lane][q] + part[1][lane][q] + part[2][lane][q] + part[3][lane][q];
+      out[(long long)b * C + cg * 8 + q] = s / (float)HW;
+    }
+  }
+}
+
+void global_avgpool(const bf16* in, float* out, int B, int HW, int C, hipStream_t s) {
+  hipLaunchKernelGGL(gap_kernel, dim3(B, cdiv(C / 8, 64)), dim3(256), 0, s, in, out, HW, C);
+  check_launch("global_avgpool");
+}
+
+// ---------------------------------------------------------------- matvec
+// One wave per (b, n): lanes split K, shuffle-reduce across the 64-lane wave.
+__global__ __launch_bounds__(256) void matvec_kernel(const float* __restrict__ x,
+                                                     const float* __restrict__ w,
+                                                     const float* __restrict__ bias,
+                                                     float* __restrict__ out, int B, int N, int K,
+                                                     int act) {
+  const int lane = threadIdx.x & 63;
+  const long long item = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (item >= (long long)B * N) return;
+  const int b = (int)(item / N), n = (int)(item % N);
+  float s = 0.f;
+  for (int k = lane; k < K; k += 64) s += w[(long long)n * K + k] * x[(long long)b * K + k];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) out[item] = apply_act(s + (bias ? bias[n] : 0.f), act);
+}
+
+void matvec(const float* x, const float* w, const float* bias, float* out, int B, int N, int K,
+            int act, hipStream_t s) {
+  hipLaunchKernelGGL(matvec_kernel, dim3(cdiv((long long)B * N, 4)), dim3(256), 0, s, x, w, bias,
+                     out, B, N, K, act);
+  check_launch("matvec");
+}
+
+// ---------------------------------------------------------------- upsample + argmax
+// Logits of one frame (h x w x K, ~50 KB at 33x33x24 bf16) stay L1/L2 resident;
+// each lane produces 4 consecutive output pixels of a row and one 4-byte store.
+// Interpolation mirrors torch's upsample_bilinear2d(align_corners=True):
+// src = dst * (in - 1) / (out - 1) in fp32, lerp weights (1 - l, l).
+template <int KMAX>
+__global__ __launch_bounds__(256) void upsample_argmax_kernel(const bf16* __restrict__ logits,
+                                                              uint8_t* __restrict__ labels, int B,
+                                                              int h, int w, int K, int ldk, int H,
+                                                              int W) {
+  const int W4 = (W + 3) / 4;
+  const long long total = (long long)B * H * W4;
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int xq = (int)(t % W4);
+  const int Y = (int)((t / W4) % H);
+  const int b = (int)(t / ((long long)W4 * H));
+  const float sh = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
+  const float sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
+  const float fy = sh * (float)Y;
+  const int y0 = (int)fy;
+  const int yp = y0 < h - 1 ? 1 : 0;
+  const float ly1 = fy - (float)y0, ly0 = 1.f - ly1;
+  const bf16* L = logits + (long long)b * h * w * ldk;
+  uint32_t packed = 0;
+  for (int e = 0; e < 4; ++e) {
+    const int X = xq * 4 + e;
+    if (X >= W) break;
+    const float fx = sw * (float)X;
+    const int x0 = (int)fx;
+    const int xp = x0 < w - 1 ? 1 : 0;
+    const float lx1 = fx - (float)x0, lx0 = 1.f - lx1;
+    const bf16* p00 = L + ((long long)y0 * w + x0) * ldk;
+    const bf16* p01 = p00 + xp * ldk;
+    const bf16* p10 = p00 + (long long)yp * w * ldk;
+    const bf16* p11 = p10 + xp * ldk;
+    float best = -3.0e38f;
+    int arg = 0;
+#pragma unroll 4
+    for (int k = 0; k < K; ++k) {
+      const float v = ly0 * (lx0 * (float)p00[k] + lx1 * (float)p01[k]) +
+                      ly1 * (lx0 * (float)p10[k] + lx1 * (float)p11[k]);
+      if (v > best) { best = v; arg = k; }
+    }
+    packed |= (uint32_t)(arg & 0xff) << (8 * e);
+  }
+  uint8_t* op = labels + ((long long)b * H + Y) * W + xq * 4;
+  if (xq * 4 + 3 < W && ((((uintptr_t)op) & 3) == 0)) {
+    *reinterpret_cast<uint32_t*>(op) = packed;
+  } else {
+    for (int e = 0; e < 4 && xq * 4 + e < W; ++e) op[e] = (packed >> (8 * e)) & 0xff;
+  }
+}
+
+void upsample_argmax(const bf16* logits, uint8_t* labels, int B, int h, int w, int K, int ldk,
+                     int H, int W, hipStream_t s) {
+  if (K > 256) throw std::invalid_argument("upsample_argmax: K > 256");
+  const long long total = (long long)B * H * ((W + 3) / 4);
+  hipLaunchKernelGGL(upsample_argmax_kernel<256>, dim3(cdiv(total, 256)), dim3(256), 0, s, logits,
+                     labels, B, h, w, K, ldk, H, W);
+  check_launch("upsample_argmax");
+}
+
+}  // namespace ssa

@@ -1,0 +1,248 @@
+"""DeepLabv3 forward on the hand-written gfx950 kernels.
+
+The torch model (``models/deeplab.py``) is the weight source and the numerics
+reference; this module folds BatchNorm into every conv, packs the weights into
+the kernels' layouts once, and executes the network as a fixed list of kernel
+launches over static NHWC bf16 buffers (allocated per (batch, camera) on first
+use, outside any graph capture). The engine captures the whole list into one
+hipGraph.
+
+Layout decisions (MI355X-first, not a translation of the tflite graph):
+  * NHWC bf16 activations, fp32 accumulation; 1x1/3x3 dense convs are MFMA
+    implicit GEMMs (``conv_gemm``) with bias/activation/residual fused in the
+    epilogue; depthwise convs are vectorised VALU kernels (8 channels per lane).
+  * Letterbox preprocessing is fused into the stem conv: the uint8 camera frame
+    is read through the resize LUTs, so the 513x513x3 model input never exists.
+  * ASPP is concat-free: each branch writes its channel slice of one buffer; the
+    image-pooling branch (spatially constant) is folded through its slice of the
+    projection weights into a per-image bias of the projection GEMM.
+  * Logits are written with a padded channel stride (ld 24 for 21 classes) and
+    upsampled + argmax'ed in one kernel.
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from ..ops import hip_ops as K
+from ..ops.hip_ops import conv_out_hw
+from .deeplab import DeepLabV3
+from .layers import ConvBNAct
+from .mobilenetv2 import MobileNetV2Backbone
+from .resnet import ResNet50Backbone
+
+
+def _pack_dense(layer: ConvBNAct, dev) -> Tuple[torch.Tensor, torch.Tensor]:
+    w, b = layer.fold()
+    # [Cout, Cin, kh, kw] -> [Cout, kh, kw, Cin]
+    return (w.permute(0, 2, 3, 1).contiguous().to(dev, torch.bfloat16),
+            b.contiguous().to(dev, torch.float32))
+
+
+def _pack_dw(layer: ConvBNAct, dev) -> Tuple[torch.Tensor, torch.Tensor]:
+    w, b = layer.fold()  # [C, 1, 3, 3]
+    return (w.reshape(w.shape[0], 9).t().contiguous().to(dev, torch.float32),
+            b.contiguous().to(dev, torch.float32))
+
+
+def _pack_stem(layer: ConvBNAct, dev) -> Tuple[torch.Tensor, torch.Tensor]:
+    w, b = layer.fold()  # [Cout, 3, k, k] -> [k, k, 3, Cout]
+    return (w.permute(2, 3, 1, 0).reshape(-1, w.shape[0]).contiguous().to(dev, torch.float32),
+            b.contiguous().to(dev, torch.float32))
+
+
+class HipDeepLab:
+    def __init__(self, model: DeepLabV3, device: torch.device, cfg=None):
+        if device.type != "cuda":
+            raise RuntimeError("HipDeepLab needs a GPU")
+        self.device = device
+        self.model = model
+        self.H = self.W = int(cfg.input_size) if cfg is not None else 513
+        self.num_classes = model.num_classes
+        self.ldk = (self.num_classes + 7) // 8 * 8
+        dev = device
+        bb = model.backbone
+        self.kind = "mnv2" if isinstance(bb, MobileNetV2Backbone) else "resnet50"
+        self.stem = _pack_stem(bb.stem, dev) + (bb.stem.k, bb.stem.stride, bb.stem.act, bb.stem.cout)
+        self.blocks: List[dict] = []
+        if self.kind == "mnv2":
+            for blk in bb.blocks:
+                s = blk.spec
+                self.blocks.append(dict(
+                    spec=s,
+                    expand=_pack_dense(blk.expand, dev) if blk.expand is not None else None,
+                    dw=_pack_dw(blk.dw, dev),
+                    project=_pack_dense(blk.project, dev)))
+        else:
+            for blk in bb.blocks:
+                self.blocks.append(dict(
+                    blk=blk,
+                    conv1=_pack_dense(blk.conv1, dev), conv2=_pack_dense(blk.conv2, dev),
+                    conv3=_pack_dense(blk.conv3, dev),
+                    down=_pack_dense(blk.down, dev) if blk.down is not None else None))
+        aspp = model.aspp
+        self.aspp_c = aspp.cout
+        self.aspp_b0 = _pack_dense(aspp.b0, dev)
+        self.aspp_atrous = [(_pack_dense(b, dev), b.dilation) for b in aspp.atrous]
+        nb_sp = 1 + len(aspp.atrous)  # spatial branches
+        self.cat_c = nb_sp * aspp.cout
+        pw, pb = aspp.project.fold()  # [256, nb*256, 1, 1]
+        pw = pw[:, :, 0, 0]
+        self.proj_w = pw[:, : self.cat_c].contiguous().to(dev, torch.bfloat16)
+        self.proj_b = pb.to(dev, torch.float32)
+        self.has_pool = aspp.pool is not None
+        if self.has_pool:
+            qw, qb = aspp.pool.fold()
+            self.pool_w = qw[:, :, 0, 0].contiguous().to(dev, torch.float32)
+            self.pool_b = qb.to(dev, torch.float32)
+            self.proj_pool_w = pw[:, self.cat_c:].contiguous().to(dev, torch.float32)
+        lw, lb = model.logits.fold()
+        self.logit_w = lw[:, :, 0, 0].reshape(lw.shape[0], 1, 1, -1).contiguous().to(dev, torch.bfloat16)
+        self.logit_b = lb.to(dev, torch.float32)
+        self._plans: Dict[tuple, Tuple[List[Callable], Dict[str, torch.Tensor]]] = {}
+
+    # ------------------------------------------------------------------ plan
+    def _plan(self, B: int, Hc: int, Wc: int):
+        key = (B, Hc, Wc)
+        if key in self._plans:
+            return self._plans[key]
+        dev = self.device
+        bufs: Dict[str, torch.Tensor] = {}
+        ops: List[Callable] = []
+
+        def buf(name, *shape, dtype=torch.bfloat16):
+            t = torch.empty(shape, dtype=dtype, device=dev)
+            bufs[name] = t
+            return t
+
+        H, W = self.H, self.W
+        sw, sb, sk, ss, sact, sc = self.stem
+        OH, OW = conv_out_hw(H, W, sk, ss, 1)
+        x = buf("stem", B, OH, OW, sc)
+        bufs["_in_shape"] = torch.tensor([B, Hc, Wc])
+
+        def stem_op(frames, lx, ly, x=x, OH=OH, OW=OW):
+            K.stem_conv(frames, lx, ly, sw, sb, x, H=H, W=W, OH=OH, OW=OW, Cout=sc, k=sk,
+                        stride=ss, act=sact)
+        ops.append(stem_op)
+        h, w, c = OH, OW, sc
+        if self.kind == "resnet50":
+            PH, PW = conv_out_hw(h, w, 3, 2, 1)
+            y = buf("pool0", B, PH, PW, c)
+            ops.append(lambda *_, x=x, y=y, h=h, w=w, c=c, PH=PH, PW=PW:
+                       K.maxpool3x3s2(x, y, B=B, IH=h, IW=w, C=c, OH=PH, OW=PW))
+            x, h, w = y, PH, PW
+            for i, blk in enumerate(self.blocks):
+                x, h, w, c = self._resnet_block(ops, buf, i, blk, x, B, h, w, c)
+        else:
+            for i, blk in enumerate(self.blocks):
+                x, h, w, c = self._mnv2_block(ops, buf, i, blk, x, B, h, w, c)
+        # ---- ASPP
+        A = self.aspp_c
+        cat = buf("aspp_cat", B, h, w, self.cat_c)
+        b0w, b0b = self.aspp_b0
+        ops.append(lambda *_, x=x, h=h, w=w, c=c: K.conv_gemm(
+            x, b0w, b0b, cat, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w, Cout=A, k=1, ldo=self.cat_c,
+            co_off=0, act="relu"))
+        for j, ((aw, ab), rate) in enumerate(self.aspp_atrous):
+            ops.append(lambda *_, x=x, h=h, w=w, c=c, aw=aw, ab=ab, rate=rate, j=j: K.conv_gemm(
+                x, aw, ab, cat, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w, Cout=A, k=3, dil=rate,
+                ldo=self.cat_c, co_off=(j + 1) * A, act="relu"))
+        img_bias = None
+        if self.has_pool:
+            gap = buf("gap", B, c, dtype=torch.float32)
+            pooled = buf("pooled", B, A, dtype=torch.float32)
+            img_bias = buf("img_bias", B, A, dtype=torch.float32)
+            ops.append(lambda *_, x=x, h=h, w=w, c=c: K.global_avgpool(x, gap, B=B, HW=h * w, C=c))
+            ops.append(lambda *_, c=c: K.matvec(gap, self.pool_w, self.pool_b, pooled, B=B, N=A,
+                                                K=c, act="relu"))
+            ops.append(lambda *_: K.matvec(pooled, self.proj_pool_w, None, img_bias, B=B, N=A, K=A))
+        proj = buf("aspp_proj", B, h, w, A)
+        ops.append(lambda *_, h=h, w=w: K.conv_gemm(
+            cat, self.proj_w, self.proj_b, proj, B=B, IH=h, IW=w, Cin=self.cat_c, OH=h, OW=w,
+            Cout=A, k=1, act="relu", img_bias=img_bias))
+        logits = buf("logits", B, h, w, self.ldk)
+        ops.append(lambda *_, h=h, w=w: K.conv_gemm(
+            proj, self.logit_w, self.logit_b, logits, B=B, IH=h, IW=w, Cin=A, OH=h, OW=w,
+            Cout=self.num_classes, k=1, ldo=self.ldk, act=None))
+        labels = buf("labels", B, H, W, dtype=torch.uint8)
+        ops.append(lambda *_, h=h, w=w: K.upsample_argmax(
+            logits, labels, B=B, h=h, w=w, K=self.num_classes, ldk=self.ldk, H=H, W=W))
+        self._plans[key] = (ops, bufs)
+        return self._plans[key]
+
+    def _mnv2_block(self, ops, buf, i, blk, x, B, h, w, c):
+        s = blk["spec"]
+        hid = s.hidden
+        inp = x
+        if blk["expand"] is not None:
+            ew, eb = blk["expand"]
+            e = buf(f"b{i}_exp", B, h, w, hid)
+            ops.append(lambda *_, x=x, e=e, h=h, w=w, c=c: K.conv_gemm(
+                x, ew, eb, e, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w, Cout=hid, k=1, act="relu6"))
+            x = e
+        OH, OW = conv_out_hw(h, w, 3, s.stride, s.dilation)
+        dw_w, dw_b = blk["dw"]
+        d = buf(f"b{i}_dw", B, OH, OW, hid)
+        ops.append(lambda *_, x=x, d=d, h=h, w=w, OH=OH, OW=OW: K.depthwise3x3(
+            x, dw_w, dw_b, d, B=B, IH=h, IW=w, C=hid, OH=OH, OW=OW, stride=s.stride,
+            dil=s.dilation, act="relu6"))
+        pw_, pb_ = blk["project"]
+        out = buf(f"b{i}_out", B, OH, OW, s.cout)
+        res = inp if s.residual else None
+        ops.append(lambda *_, d=d, out=out, OH=OH, OW=OW, res=res: K.conv_gemm(
+            d, pw_, pb_, out, B=B, IH=OH, IW=OW, Cin=hid, OH=OH, OW=OW, Cout=s.cout, k=1,
+            act=None, res=res))
+        return out, OH, OW, s.cout
+
+    def _resnet_block(self, ops, buf, i, blk, x, B, h, w, c):
+        m = blk["blk"]
+        width = m.conv1.cout
+        cout = m.conv3.cout
+        w1, b1 = blk["conv1"]
+        t1 = buf(f"r{i}_c1", B, h, w, width)
+        ops.append(lambda *_, x=x, t1=t1, h=h, w=w, c=c: K.conv_gemm(
+            x, w1, b1, t1, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w, Cout=width, k=1, act="relu"))
+        OH, OW = conv_out_hw(h, w, 3, m.stride, m.dilation)
+        w2, b2 = blk["conv2"]
+        t2 = buf(f"r{i}_c2", B, OH, OW, width)
+        ops.append(lambda *_, t1=t1, t2=t2, h=h, w=w, OH=OH, OW=OW: K.conv_gemm(
+            t1, w2, b2, t2, B=B, IH=h, IW=w, Cin=width, OH=OH, OW=OW, Cout=width, k=3,
+            stride=m.stride, dil=m.dilation, act="relu"))
+        if blk["down"] is not None:
+            wd, bd = blk["down"]
+            idt = buf(f"r{i}_down", B, OH, OW, cout)
+            ops.append(lambda *_, x=x, idt=idt, h=h, w=w, c=c, OH=OH, OW=OW: K.conv_gemm(
+                x, wd, bd, idt, B=B, IH=h, IW=w, Cin=c, OH=OH, OW=OW, Cout=cout, k=1,
+                stride=m.stride, act=None))
+        else:
+            idt = x
+        w3, b3 = blk["conv3"]
+        out = buf(f"r{i}_out", B, OH, OW, cout)
+        ops.append(lambda *_, t2=t2, out=out, idt=idt, OH=OH, OW=OW: K.conv_gemm(
+            t2, w3, b3, out, B=B, IH=OH, IW=OW, Cin=width, OH=OH, OW=OW, Cout=cout, k=1,
+            act="relu", res=idt))
+        return out, OH, OW, cout
+
+    # ------------------------------------------------------------------ run
+    def segment(self, frames: torch.Tensor, lut_x: torch.Tensor, lut_y: torch.Tensor) -> torch.Tensor:
+        """frames: (B, Hc, Wc, 3) uint8 BGR on device -> (B, H, W) uint8 labels (static buffer)."""
+        B, Hc, Wc, _ = frames.shape
+        if lut_x.numel() != self.W or lut_y.numel() != self.H:
+            raise ValueError("letterbox LUTs do not match the model input size")
+        ops, bufs = self._plan(B, Hc, Wc)
+        frames = frames.contiguous()
+        for op in ops:
+            op(frames, lut_x, lut_y)
+        return bufs["labels"]
+
+    def logits(self, frames, lut_x, lut_y) -> torch.Tensor:
+        """Run and return the NHWC logits buffer (tests)."""
+        self.segment(frames, lut_x, lut_y)
+        B, Hc, Wc, _ = frames.shape
+        return self._plans[(B, Hc, Wc)][1]["logits"][..., : self.num_classes]
+
+    def buffers(self, B: int, Hc: int, Wc: int) -> Dict[str, torch.Tensor]:
+        return self._plan(B, Hc, Wc)[1]

@@ -1,0 +1,171 @@
+"""Checked torch-tensor wrappers around the gfx950 kernels in ``_hip``.
+
+Every wrapper validates dtype/contiguity/shape on the host (an out-of-bounds
+kernel can reset the whole GPU node, so shapes are checked before launch), then
+launches on ``torch.cuda.current_stream()`` — inside a ``torch.cuda.graph``
+capture that is the capture stream, so the launches are recorded into the graph.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import os
+
+import torch
+
+from .native import hip as _hip_mod
+
+ACT = {None: 0, "none": 0, "relu": 1, "relu6": 2}
+
+
+_DEBUG_SYNC = os.environ.get("SSA_DEBUG_SYNC", "0") == "1"
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _dbg(name: str, **shapes) -> None:
+    """SSA_DEBUG_SYNC=1: synchronise after every launch and name the failing kernel."""
+    if not _DEBUG_SYNC or torch.cuda.is_current_stream_capturing():
+        return
+    try:
+        torch.cuda.synchronize()
+    except Exception as e:
+        raise RuntimeError(f"kernel {name} failed with {shapes}: {e}") from e
+
+
+def _ptr(t: Optional[torch.Tensor]) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _chk(t: torch.Tensor, dtype, name: str, numel: Optional[int] = None) -> None:
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: must be a CUDA tensor")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if numel is not None and t.numel() < numel:
+        raise ValueError(f"{name}: has {t.numel()} elements, kernel needs {numel}")
+
+
+def conv_out_hw(IH: int, IW: int, k: int, stride: int, dil: int):
+    pad = dil * (k // 2)
+    OH = (IH + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    OW = (IW + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    return OH, OW
+
+
+def conv_gemm(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out: torch.Tensor, *,
+              B: int, IH: int, IW: int, Cin: int, OH: int, OW: int, Cout: int, k: int = 1,
+              stride: int = 1, dil: int = 1, ldo: Optional[int] = None, co_off: int = 0,
+              act=None, res: Optional[torch.Tensor] = None, ldr: Optional[int] = None,
+              img_bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """NHWC implicit-GEMM conv. x: [B,IH,IW,Cin] bf16; w: [Cout,k,k,Cin] bf16;
+    out: [B,OH,OW,ldo] bf16 written at channel offset co_off."""
+    ldo = Cout if ldo is None else ldo
+    ldr = Cout if ldr is None else ldr
+    if Cin % 8:
+        raise ValueError("conv_gemm: Cin must be a multiple of 8")
+    if co_off + Cout > ldo:
+        raise ValueError("conv_gemm: co_off + Cout > ldo")
+    _chk(x, torch.bfloat16, "x", B * IH * IW * Cin)
+    _chk(w, torch.bfloat16, "w", Cout * k * k * Cin)
+    _chk(bias, torch.float32, "bias", Cout)
+    _chk(out, torch.bfloat16, "out", B * OH * OW * ldo)
+    if res is not None:
+        _chk(res, torch.bfloat16, "res", B * OH * OW * ldr)
+    if img_bias is not None:
+        _chk(img_bias, torch.float32, "img_bias", B * Cout)
+    _hip_mod().conv_gemm(_ptr(x), _ptr(w), _ptr(bias), _ptr(img_bias), _ptr(res), _ptr(out), B, IH,
+                         IW, Cin, OH, OW, Cout, k, k, stride, dil, ldo, co_off, ldr, ACT[act],
+                         _stream())
+    _dbg('conv_gemm')
+    return out
+
+
+def depthwise3x3(x, w, bias, out, *, B, IH, IW, C, OH, OW, stride=1, dil=1, act="relu6"):
+    """x: [B,IH,IW,C] bf16; w: [9, C] fp32; out: [B,OH,OW,C] bf16."""
+    _chk(x, torch.bfloat16, "x", B * IH * IW * C)
+    _chk(w, torch.float32, "w", 9 * C)
+    _chk(bias, torch.float32, "bias", C)
+    _chk(out, torch.bfloat16, "out", B * OH * OW * C)
+    if C % 8:
+        raise ValueError("depthwise3x3: C must be a multiple of 8")
+    _hip_mod().depthwise3x3(_ptr(x), _ptr(w), _ptr(bias), _ptr(out), B, IH, IW, C, OH, OW, stride,
+                            dil, ACT[act], _stream())
+    _dbg('depthwise3x3')
+    return out
+
+
+def stem_conv(frames, lut_x, lut_y, w, bias, out, *, H, W, OH, OW, Cout, k, stride, act):
+    """frames: [B,Hc,Wc,3] uint8 BGR; luts int32 [W]/[H]; w: [k*k*3, Cout] fp32."""
+    B, Hc, Wc, C3 = frames.shape
+    if C3 != 3:
+        raise ValueError("frames must be (B, H, W, 3)")
+    _chk(frames, torch.uint8, "frames")
+    _chk(lut_x, torch.int32, "lut_x", W)
+    _chk(lut_y, torch.int32, "lut_y", H)
+    _chk(w, torch.float32, "w", k * k * 3 * Cout)
+    _chk(bias, torch.float32, "bias", Cout)
+    _chk(out, torch.bfloat16, "out", B * OH * OW * Cout)
+    _hip_mod().stem_conv(_ptr(frames), _ptr(lut_x), _ptr(lut_y), _ptr(w), _ptr(bias), _ptr(out), B,
+                         Hc, Wc, H, W, OH, OW, Cout, k, stride, ACT[act], _stream())
+    _dbg('stem_conv')
+    return out
+
+
+def maxpool3x3s2(x, out, *, B, IH, IW, C, OH, OW):
+    _chk(x, torch.bfloat16, "x", B * IH * IW * C)
+    _chk(out, torch.bfloat16, "out", B * OH * OW * C)
+    _hip_mod().maxpool3x3s2(_ptr(x), _ptr(out), B, IH, IW, C, OH, OW, _stream())
+    _dbg('maxpool3x3s2')
+    return out
+
+
+def global_avgpool(x, out, *, B, HW, C):
+    _chk(x, torch.bfloat16, "x", B * HW * C)
+    _chk(out, torch.float32, "out", B * C)
+    _hip_mod().global_avgpool(_ptr(x), _ptr(out), B, HW, C, _stream())
+    _dbg('global_avgpool')
+    return out
+
+
+def matvec(x, w, bias, out, *, B, N, K, act=None):
+    _chk(x, torch.float32, "x", B * K)
+    _chk(w, torch.float32, "w", N * K)
+    if bias is not None:
+        _chk(bias, torch.float32, "bias", N)
+    _chk(out, torch.float32, "out", B * N)
+    _hip_mod().matvec(_ptr(x), _ptr(w), _ptr(bias), _ptr(out), B, N, K, ACT[act], _stream())
+    _dbg('matvec')
+    return out
+
+
+def upsample_argmax(logits, labels, *, B, h, w, K, ldk, H, W):
+    _chk(logits, torch.bfloat16, "logits", B * h * w * ldk)
+    _chk(labels, torch.uint8, "labels", B * H * W)
+    if K > ldk:
+        raise ValueError("K > ldk")
+    _hip_mod().upsample_argmax(_ptr(logits), _ptr(labels), B, h, w, K, ldk, H, W, _stream())
+    _dbg('upsample_argmax')
+    return labels
+
+
+def post_workspace_bytes(B, H, W, K, bins) -> int:
+    return int(_hip_mod().post_workspace_bytes(B, H, W, K, bins))
+
+
+def postprocess(labels, palette, ws, records, *, B, H, W, crop_h, crop_w, min_area, K, bins,
+                thr=127):
+    _chk(labels, torch.uint8, "labels", B * H * W)
+    _chk(palette, torch.int32, "palette", 256 * 3)
+    _chk(ws, torch.uint8, "ws", post_workspace_bytes(B, H, W, K, bins))
+    _chk(records, torch.float32, "records", B * (1 + 5 * K))
+    if not (0 < crop_h <= H and 0 < crop_w <= W):
+        raise ValueError("bad crop")
+    _hip_mod().postprocess(_ptr(labels), B, H, W, crop_h, crop_w, _ptr(palette), thr,
+                           float(min_area), bins, K, _ptr(ws), _ptr(records), _stream())
+    _dbg('postprocess')
+    return records

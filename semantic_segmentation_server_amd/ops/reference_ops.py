@@ -59,8 +59,8 @@ def preprocess(frames_bgr: torch.Tensor, lut_x, lut_y, out_dtype=torch.float32,
     ``x / 127.5 - 1`` (padding therefore becomes -1).
     """
     dev = frames_bgr.device
-    lx = torch.as_tensor(np.array(lut_x), device=dev, dtype=torch.long)
-    ly = torch.as_tensor(np.array(lut_y), device=dev, dtype=torch.long)
+    lx = lut_x.long() if torch.is_tensor(lut_x) else torch.as_tensor(np.array(lut_x), device=dev, dtype=torch.long)
+    ly = lut_y.long() if torch.is_tensor(lut_y) else torch.as_tensor(np.array(lut_y), device=dev, dtype=torch.long)
     vx, vy = lx >= 0, ly >= 0
     g = frames_bgr[:, ly.clamp(min=0)][:, :, lx.clamp(min=0)]          # N,H,W,3
     g = g * (vy[None, :, None, None] & vx[None, None, :, None])

@@ -1,0 +1,88 @@
+"""Process-group plumbing.
+
+One process per GPU; ``torch.distributed`` with backend ``"nccl"``, which binds
+RCCL on ROCm (xGMI between the GPUs of a node), or ``"gloo"`` on CPU for tests.
+Rendezvous comes from the torchrun environment (RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR / MASTER_PORT); MASTER_ADDR defaults to 127.0.0.1.
+
+The reference has no distributed code at all (single Edge TPU, batch 1).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: Optional[str] = None
+
+    @property
+    def is_root(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def initialized(self) -> bool:
+        return self.backend is not None
+
+
+def init(backend: Optional[str] = None, timeout_s: float = 300.0) -> DistContext:
+    """Initialise from env. Single process (no WORLD_SIZE) -> no process group."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    use_cuda = torch.cuda.is_available() and backend != "gloo"
+    if use_cuda:
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    if world == 1:
+        return DistContext(0, 1, 0, device, None)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    backend = backend or ("nccl" if use_cuda else "gloo")
+    kw = {}
+    if backend == "nccl":
+        kw["device_id"] = device
+    dist.init_process_group(backend, rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return DistContext(rank, world, local, device, backend)
+
+
+def barrier(ctx: DistContext) -> None:
+    if ctx.initialized:
+        if ctx.backend == "nccl":
+            dist.barrier(device_ids=[ctx.device.index])
+        else:
+            dist.barrier()
+
+
+def allreduce_max(ctx: DistContext, v: float) -> float:
+    if not ctx.initialized:
+        return v
+    t = torch.tensor([v], dtype=torch.float64, device=ctx.device if ctx.backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def allreduce_sum(ctx: DistContext, v: float) -> float:
+    if not ctx.initialized:
+        return v
+    t = torch.tensor([v], dtype=torch.float64, device=ctx.device if ctx.backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def destroy(ctx: DistContext) -> None:
+    if ctx.initialized and dist.is_initialized():
+        dist.destroy_process_group()

@@ -1,0 +1,225 @@
+"""Per-device inference engine.
+
+Replaces the reference's ``BasicEngine`` (``sem_seg_server.py:18,139,162,264``) plus
+the per-frame host post-processing (``:164-192``). One ``Engine`` owns one device:
+
+    uint8 BGR camera frames (B, Hc, Wc, 3)
+      -> letterbox/normalise (+ stem conv, fused on the HIP path)
+      -> DeepLabv3 backbone + ASPP + logits
+      -> bilinear upsample + argmax -> (B, H, W) uint8 labels
+      -> contour statistics -> compact per-frame records
+
+Backends:
+  * ``hip``   — hand-written gfx950 kernels (``models/hip_model.py``,
+                ``postprocess/device.py``); the whole step is captured once into a
+                hipGraph (``torch.cuda.CUDAGraph``) with static buffers and replayed.
+  * ``torch`` — stock PyTorch-ROCm ops (the "framework floor" baseline and the
+                CPU path of config 1); also graph-capturable on GPU.
+
+Post-processing (``contour_mode``):
+  * ``fast``  — device CCL + quad-decomposition statistics on the HIP backend,
+                numpy/scipy component statistics on CPU (same math);
+  * ``exact`` — host C++ Suzuki-Abe tracer on the label maps (oracle).
+"""
+from __future__ import annotations
+
+import logging
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..config import Config
+from ..labels import colormap_for, load_labels
+from ..models.deeplab import build_model
+from ..ops import reference_ops as R
+from ..postprocess import reference as PR
+from .results import RECORD_DTYPE
+
+log = logging.getLogger(__name__)
+
+DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32, "int8": torch.bfloat16}
+
+
+def _per_frame(streams, n: int) -> List[int]:
+    if isinstance(streams, (int, np.integer)):
+        return [int(streams)] * n
+    return [int(s) for s in streams]
+
+
+def resolve_device(spec: str = "auto") -> torch.device:
+    if spec == "auto":
+        return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
+            else torch.device("cpu")
+    return torch.device(spec)
+
+
+class Engine:
+    def __init__(self, cfg: Config, device: Optional[torch.device] = None,
+                 model: Optional[torch.nn.Module] = None):
+        self.cfg = cfg
+        self.device = device or resolve_device(cfg.device)
+        self.is_cuda = self.device.type == "cuda"
+        self.H = self.W = int(cfg.input_size)
+        self.min_area = cfg.min_area
+        self.palette = np.ascontiguousarray(colormap_for(cfg.dataset), np.int32)
+        self.model = model if model is not None else build_model(
+            cfg.arch, cfg.num_classes, cfg.width_mult, cfg.output_stride, cfg.aspp, cfg.seed)
+        if cfg.model:
+            self._load_weights(cfg.model)
+        self.model.eval()
+        self.backend = cfg.backend if self.is_cuda else "torch"
+        if self.backend == "hip" and not self.is_cuda:
+            raise RuntimeError("hip backend requires a GPU device")
+        self.dtype = DTYPES[cfg.dtype] if self.is_cuda else torch.float32
+        self.cam: Optional[Tuple[int, int]] = None
+        self._graph = None
+        self._static: Dict[str, torch.Tensor] = {}
+        self._hip_model = None
+        self._hip_post = None
+        if self.backend == "torch":
+            self.model = self.model.to(self.device, self.dtype)
+            if self.is_cuda:
+                self.model = self.model.to(memory_format=torch.channels_last)
+        else:
+            from ..models.hip_model import HipDeepLab
+            self._hip_model = HipDeepLab(self.model, self.device, cfg)
+        self.stream = torch.cuda.Stream(self.device) if self.is_cuda else None
+
+    # ------------------------------------------------------------------ setup
+    def _load_weights(self, path: str) -> None:
+        if path.endswith(".safetensors"):
+            from safetensors.torch import load_file
+            sd = load_file(path)
+        else:
+            sd = torch.load(path, map_location="cpu", weights_only=True)
+        missing, unexpected = self.model.load_state_dict(sd, strict=False)
+        log.info("loaded %s (missing=%d unexpected=%d)", path, len(missing), len(unexpected))
+
+    def set_camera(self, cam_w: int, cam_h: int) -> None:
+        if self.cam == (cam_w, cam_h):
+            return
+        self.cam = (int(cam_w), int(cam_h))
+        lx, ly, rw, rh, cw, ch = R.letterbox_luts(cam_w, cam_h, self.W, self.H,
+                                                  self.cfg.keep_aspect_ratio)
+        self.crop_w, self.crop_h = cw, ch
+        self.lut_x = torch.tensor(lx, device=self.device, dtype=torch.int32)
+        self.lut_y = torch.tensor(ly, device=self.device, dtype=torch.int32)
+        self._graph = None
+
+    # -------------------------------------------------------------- inference
+    def _infer_eager(self, frames: torch.Tensor) -> torch.Tensor:
+        if self.backend == "hip":
+            return self._hip_model.segment(frames, self.lut_x, self.lut_y)
+        x = R.preprocess(frames, self.lut_x, self.lut_y,
+                         out_dtype=self.dtype, channels_last=self.is_cuda)
+        with torch.no_grad():
+            logits = self.model(x)
+        return R.upsample_argmax(logits, self.H, self.W)
+
+    def _device_post(self, labels: torch.Tensor):
+        if self._hip_post is None:
+            from ..postprocess.device import DevicePostprocess
+            self._hip_post = DevicePostprocess(self.device, self.H, self.W, self.palette,
+                                               self.cfg.max_segments)
+        return self._hip_post.run(labels, self.crop_w, self.crop_h, self.min_area)
+
+    def _use_device_post(self) -> bool:
+        return self.is_cuda and self.cfg.contour_mode == "fast"
+
+    def _step_device(self, frames: torch.Tensor):
+        labels = self._infer_eager(frames)
+        post = self._device_post(labels) if self._use_device_post() else None
+        return labels, post
+
+    def _capture(self, B: int) -> None:
+        Hc, Wc = self.cam[1], self.cam[0]
+        st = self._static
+        st["frames"] = torch.zeros((B, Hc, Wc, 3), dtype=torch.uint8, device=self.device)
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(2):  # warm up allocator / lazy init outside capture
+                self._step_device(st["frames"])
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            labels, post = self._step_device(st["frames"])
+        st["labels"] = labels
+        st["post"] = post
+        self._graph = g
+        self._graph_B = B
+
+    def run_device(self, frames: torch.Tensor):
+        """frames: (B, Hc, Wc, 3) uint8 on this device -> (labels, device post outputs).
+
+        With ``cfg.graph`` the step is captured on first use per (B, camera) and
+        replayed; outputs then live in static buffers overwritten by the next call.
+        """
+        B = frames.shape[0]
+        if self.cfg.graph and self.is_cuda:
+            if self._graph is None or self._graph_B != B:
+                self._capture(B)
+            self._static["frames"].copy_(frames, non_blocking=True)
+            self._graph.replay()
+            return self._static["labels"], self._static["post"]
+        return self._step_device(frames)
+
+    # ------------------------------------------------------------ post/host
+    def records_from_labels(self, labels: torch.Tensor, frame_ids: Sequence[int],
+                            ts: Sequence[float], streams) -> np.ndarray:
+        """Host post-processing of label maps (exact tracer, or CPU component path)."""
+        if self.cfg.contour_mode == "none":  # ablation: inference only
+            return np.zeros(0, RECORD_DTYPE)
+        lab = labels.cpu().numpy() if labels.device.type != "cpu" else labels.numpy()
+        streams = _per_frame(streams, lab.shape[0])
+        out = []
+        for i in range(lab.shape[0]):
+            out.append(PR.frame_records(lab[i], self.crop_w, self.crop_h, self.cfg.min_area_ratio,
+                                        self.palette, streams[i], frame_ids[i], ts[i])
+                       if self.cfg.contour_mode == "exact" or not self._has_scipy()
+                       else self._component_records(lab[i], streams[i], frame_ids[i], ts[i]))
+        return np.concatenate(out) if out else np.zeros(0, RECORD_DTYPE)
+
+    @staticmethod
+    def _has_scipy() -> bool:
+        try:
+            import scipy.ndimage  # noqa: F401
+            return True
+        except Exception:
+            return False
+
+    def _component_records(self, lab: np.ndarray, stream: int, fid: int, ts: float) -> np.ndarray:
+        from ..postprocess.components import component_segments
+        segs = component_segments(lab[: self.crop_h, : self.crop_w], self.min_area, self.palette)
+        out = np.zeros(len(segs), RECORD_DTYPE)
+        H, W = self.H, self.W
+        for i, (l, sc, area, cx, cy, _, _) in enumerate(segs):
+            out[i] = (l, sc, min(1.0, area / (W * H)), min(1.0, cx / W), min(1.0, cy / H),
+                      stream, fid, ts)
+        return out
+
+    def step(self, frames_host: np.ndarray, frame_ids: Sequence[int], ts: Sequence[float],
+             streams=0) -> np.ndarray:
+        """Full step from host frames to records (used by the server producer)."""
+        Hc, Wc = frames_host.shape[1:3]
+        self.set_camera(Wc, Hc)
+        if not self.is_cuda:
+            frames = torch.from_numpy(np.ascontiguousarray(frames_host))
+            with torch.no_grad():
+                labels = self._infer_eager(frames)
+            return self.records_from_labels(labels, frame_ids, ts, streams)
+        with torch.cuda.stream(self.stream):
+            frames = torch.from_numpy(np.ascontiguousarray(frames_host)).pin_memory() \
+                .to(self.device, non_blocking=True)
+            labels, post = self.run_device(frames)
+            if post is not None:
+                recs = self._hip_post.fetch(post, frame_ids, ts, _per_frame(streams, len(frame_ids)),
+                                            self.W, self.H)
+            else:
+                recs = None
+        self.stream.synchronize()
+        if recs is None:
+            recs = self.records_from_labels(labels, frame_ids, ts, streams)
+        return recs

@@ -1,0 +1,147 @@
+"""T1/T5: wire compatibility of the v1 proto and servicer semantics.
+
+The expected bytes are hand-encoded from the reference schema
+(sem_seg_server.proto:14-50: label=1 string, score=2 float, area=3 float,
+centroid=4 message{cx=1 float, cy=2 float}; data=1 repeated; width=1/height=2 int32).
+"""
+import os
+import struct
+
+import grpc
+import numpy as np
+import pytest
+
+from semantic_segmentation_server_amd.api import proto as P
+from semantic_segmentation_server_amd.api import service as S
+from semantic_segmentation_server_amd.labels import load_labels
+from semantic_segmentation_server_amd.runtime.results import RECORD_DTYPE, ResultBuffer, ResultHub, make_records
+
+REF_PB2 = "/root/reference/sem_seg_server_pb2.py"
+
+
+def _f32(tag, v):
+    return bytes([tag]) + struct.pack("<f", v)
+
+
+def test_segmented_object_wire_bytes():
+    o = P.SegmentedObject(label="person", score=0.5, area=0.25, centroid=P.Centroid(cx=0.5, cy=0.75))
+    cen = _f32(0x0D, 0.5) + _f32(0x15, 0.75)
+    exp = b"\x0a\x06person" + _f32(0x15, 0.5) + _f32(0x1D, 0.25) + b"\x22" + bytes([len(cen)]) + cen
+    assert o.SerializeToString() == exp
+    assert P.SegmentedObject.FromString(exp) == o
+
+
+def test_padding_entry_serializes_empty():
+    d = P.SegmentedObjectData(data=[P.SegmentedObject()])
+    assert d.SerializeToString() == b"\x0a\x00"
+    assert not d.data[0].HasField("centroid")
+
+
+def test_camera_resolution_wire():
+    assert P.CameraResolution(width=640, height=480).SerializeToString() == b"\x08\x80\x05\x10\xe0\x03"
+    assert P.Empty().SerializeToString() == b""
+
+
+def test_service_names():
+    fd = P.POOL.FindFileByName("sem_seg_server.proto")
+    svc = fd.services_by_name["SemanticSegmentation"]
+    assert svc.full_name == "sem_seg_server.SemanticSegmentation"
+    assert [m.name for m in svc.methods] == ["GetSegmentedObjects", "GetCameraResolution"]
+    assert svc.methods_by_name["GetSegmentedObjects"].output_type.full_name == \
+        "sem_seg_server.SegmentedObjectData"
+
+
+@pytest.mark.skipif(not os.path.exists(REF_PB2), reason="reference not mounted")
+def test_descriptor_matches_reference_serialized_descriptor():
+    """Parse the reference's embedded FileDescriptorProto bytes (without executing
+    its module) and compare every message/field/method."""
+    import ast
+    from google.protobuf import descriptor_pb2
+    tree = ast.parse(open(REF_PB2).read())
+    blob = None
+    for node in ast.walk(tree):
+        if isinstance(node, ast.keyword) and node.arg == "serialized_pb":
+            blob = ast.literal_eval(node.value)
+    assert blob is not None
+    ref = descriptor_pb2.FileDescriptorProto.FromString(blob)
+    ours = P.v1_file_descriptor()
+    assert ref.package == ours.package
+
+    def msgs(fd):
+        out = {}
+
+        def walk(m, prefix):
+            out[prefix + m.name] = sorted((f.name, f.number, f.type, f.label, f.type_name) for f in m.field)
+            for n in m.nested_type:
+                walk(n, prefix + m.name + ".")
+        for m in fd.message_type:
+            walk(m, "")
+        return out
+    assert msgs(ref) == msgs(ours)
+    rs = {(m.name, m.input_type, m.output_type) for s in ref.service for m in s.method}
+    os_ = {(m.name, m.input_type, m.output_type) for s in ours.service for m in s.method}
+    assert rs == os_
+
+
+def _recs(labels):
+    return make_records([(l, 0.9, 0.1, 0.2, 0.3, 0, i, 0.0) for i, l in enumerate(labels)])
+
+
+def test_buffer_lifo_and_bound():
+    b = ResultBuffer(maxlen=3)
+    b.push_frame(_recs([1, 2]))   # frame 1 contours 0,1
+    b.push_frame(_recs([3, 4]))   # frame 2
+    assert b.drops == 1            # oldest (label 1) dropped
+    got = [int(r["label"]) for r in b.pop(5)]
+    assert got == [4, 3, 2]        # newest frame's last contour first
+    assert b.pop(1) == []
+
+
+def test_v1_get_segmented_objects_pads_and_pops():
+    hub = ResultHub(1)
+    labels = load_labels()
+    sv = S.SemanticSegmentationServicer(hub, labels, num_detections=3, camera_res=(640, 480))
+    hub.push_records(_recs([15, 7]))
+    r = sv.GetSegmentedObjects(P.Empty(), None)
+    assert len(r.data) == 3
+    assert [d.label for d in r.data] == ["car", "person", ""]
+    assert r.data[0].centroid.cx == pytest.approx(0.2)
+    assert not r.data[2].HasField("centroid")
+    r2 = sv.GetSegmentedObjects(P.Empty(), None)
+    assert [d.label for d in r2.data] == ["", "", ""]
+    assert sv.GetCameraResolution(P.Empty(), None).width == 640
+
+
+def test_unknown_label_is_stringified():
+    hub = ResultHub(1)
+    sv = S.SemanticSegmentationServicer(hub, {0: "background"}, num_detections=1)
+    hub.push_records(_recs([42]))
+    assert sv.GetSegmentedObjects(P.Empty(), None).data[0].label == "42"
+
+
+def test_grpc_loopback_v1_and_v2():
+    hub = ResultHub(2)
+    labels = load_labels()
+    server, port = S.make_server(4, 0, "127.0.0.1")
+    S.add_v1_servicer(S.SemanticSegmentationServicer(hub, labels, 3, (640, 480)), server)
+    S.add_v2_servicer(S.SemanticSegmentationV2Servicer(
+        hub, labels, 3, [dict(stream_id=1, width=320, height=240, rank=0, source="synthetic")]),
+        server)
+    server.start()
+    try:
+        hub.push_records(_recs([15]))
+        r = make_records([(7, 1.0, 0.5, 0.5, 0.5, 1, 99, 123.0)])
+        hub.push_records(r)
+        with grpc.insecure_channel(f"127.0.0.1:{port}") as ch:
+            st = S.SemanticSegmentationStub(ch)
+            assert st.GetCameraResolution(P.Empty()).height == 480
+            d = st.GetSegmentedObjects(P.Empty())
+            assert [x.label for x in d.data] == ["person", "", ""]
+            v2 = S.SemanticSegmentationV2Stub(ch)
+            t = v2.GetStreamSegmentedObjects(P.StreamRequest(stream_id=1, max_objects=2, pad=True))
+            assert len(t.data) == 2 and t.data[0].frame_id == 99 and t.data[0].object.label == "car"
+            assert v2.ListStreams(P.Empty()).streams[0].width == 320
+            assert v2.Health(P.Empty()).serving
+            assert v2.GetStats(P.Empty()).buffer_depth == 0
+    finally:
+        server.stop(0)

@@ -1,0 +1,105 @@
+"""T2: post-processing parity.
+
+* the exact host tracer on shapes whose OpenCV results are known by hand;
+* the component-statistics algorithm (what the GPU kernels implement) against
+  the exact tracer on random planted label maps: identical labels, areas,
+  centroids, scores and order;
+* the reference's palette/blur/gray/threshold rule (only car and person survive).
+"""
+import numpy as np
+import pytest
+
+from semantic_segmentation_server_amd.labels import pascal_colormap, pascal_foreground_gray
+from semantic_segmentation_server_amd.ops import native
+from semantic_segmentation_server_amd.postprocess import components as C
+from semantic_segmentation_server_amd.postprocess import reference as R
+from semantic_segmentation_server_amd.postprocess.synthetic import random_label_map
+
+H = native.host()
+
+
+def test_rectangle_contour_geometry():
+    m = np.zeros((10, 12), np.uint8)
+    m[2:8, 2:9] = 1
+    cs = H.find_contours(m)
+    assert len(cs) == 1
+    c = cs[0]
+    # OpenCV orders an outer rectangle counter-clockwise starting top-left
+    assert c["points"].tolist() == [[2, 2], [2, 7], [8, 7], [8, 2]]
+    assert H.contour_area(c["points"]) == 30.0
+    mo = H.moments(c["points"])
+    assert mo["m00"] == 30.0 and mo["m10"] / mo["m00"] == 5.0 and mo["m01"] / mo["m00"] == 4.5
+
+
+def test_hole_hierarchy_and_order():
+    m = np.zeros((20, 20), np.uint8)
+    m[1:19, 1:19] = 1
+    m[4:16, 4:16] = 0     # hole
+    m[7:13, 7:13] = 1     # nested blob inside the hole
+    m[2, 17] = 0
+    cs = H.find_contours(m)
+    kinds = [(c["is_hole"], c["parent"]) for c in cs]
+    # pre-order: outer, its hole(s) (newest first), nested outer
+    assert kinds[0] == (False, -1)
+    assert all(k[1] == 0 for k in kinds[1:] if k[0])
+    nested = [i for i, c in enumerate(cs) if not c["is_hole"] and c["parent"] >= 0]
+    assert len(nested) == 1 and cs[cs[nested[0]]["parent"]]["is_hole"]
+
+
+def test_fill_covers_holes():
+    m = np.zeros((10, 10), np.uint8)
+    m[1:9, 1:9] = 1
+    m[3:6, 3:6] = 0
+    c = H.find_contours(m)[0]
+    f = H.fill(c["points"], 10, 10)
+    assert (f > 0).sum() == 64
+
+
+def test_only_car_and_person_survive_threshold():
+    g = pascal_foreground_gray()
+    assert [i for i in range(21) if g[i] > 127] == [7, 15]
+    # a 3x3 blend of non-foreground classes never crosses the threshold
+    lab = np.full((5, 5), 19, np.uint8)
+    lab[1:4, 1:4] = 14
+    assert R.palette_mask_numpy(lab).max() == 0
+
+
+def test_mask_host_equals_numpy():
+    rng = np.random.default_rng(0)
+    for _ in range(5):
+        lab = random_label_map(rng, 67, 91)
+        assert np.array_equal(H.palette_mask(lab, R.palette_int32()), R.palette_mask_numpy(lab))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_components_match_exact_tracer(seed):
+    rng = np.random.default_rng(seed)
+    for _ in range(25):
+        h, w = int(rng.integers(5, 140)), int(rng.integers(5, 140))
+        lab = random_label_map(rng, h, w, n_blobs=int(rng.integers(1, 9)),
+                               noise=float(rng.choice([0.0, 0.01, 0.05])))
+        ma = float(rng.choice([0.0, 1.0, 10.0, 0.05 * h * w]))
+        a = R.segments_exact(lab, ma)
+        b = C.component_segments(lab, ma)
+        A = [(x[0], round(x[1], 9), x[2], x[3], x[4], x[6]) for x in a]
+        B = [(x[0], round(x[1], 9), x[2], x[3], x[4], x[6]) for x in b]
+        assert A == B, (seed, h, w, ma)
+
+
+def test_frame_records_normalisation():
+    lab = np.zeros((513, 513), np.uint8)
+    lab[100:300, 50:250] = 15          # person, inside the 513 x 384 letterbox crop
+    recs = R.frame_records(lab, 513, 384, 0.05)
+    assert len(recs) == 1
+    r = recs[0]
+    assert r["label"] == 15
+    # eroded by the blur at the blob border: polygon through the surviving pixels
+    assert r["area"] == pytest.approx(197 * 197 / (513 * 513), rel=1e-6)  # 198x198 px, polygon 197^2
+    assert r["cx"] == pytest.approx(149 / 513) and r["cy"] == pytest.approx(199 / 513)
+    assert r["score"] == 1.0
+
+
+def test_letterbox_crop_geometry():
+    assert R.letterbox_geometry(640, 480, 513, 513) == (513, 384, 513, 384)
+    assert R.letterbox_geometry(480, 640, 513, 513) == (384, 513, 384, 513)
+    assert R.letterbox_geometry(640, 480, 513, 513, keep_aspect_ratio=False) == (513, 513, 513, 513)
