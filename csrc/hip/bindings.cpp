@@ -22,15 +22,20 @@ PYBIND11_MODULE(_hip, m) {
   m.def("conv_gemm",
         [](uintptr_t in, uintptr_t w, uintptr_t bias, uintptr_t img_bias, uintptr_t res,
            uintptr_t out, int B, int IH, int IW, int Cin, int OH, int OW, int Cout, int KH, int KW,
-           int stride, int dil, int ldo, int co_off, int ldr, int act, uintptr_t stream) {
+           int stride, int dil, int ldo, int co_off, int ldr, int act, uintptr_t stream, int variant) {
           ConvParams p;
           p.in = P<const bf16>(in); p.w = P<const bf16>(w); p.bias = P<const float>(bias);
           p.img_bias = P<const float>(img_bias); p.res = P<const bf16>(res); p.out = P<bf16>(out);
           p.B = B; p.IH = IH; p.IW = IW; p.Cin = Cin; p.OH = OH; p.OW = OW; p.Cout = Cout;
           p.KH = KH; p.KW = KW; p.stride = stride; p.dil = dil; p.ldo = ldo; p.co_off = co_off;
-          p.ldr = ldr; p.act = act;
+          p.ldr = ldr; p.act = act; p.variant = variant;
           conv_gemm(p, S(stream));
-        });
+        },
+        py::arg("in"), py::arg("w"), py::arg("bias"), py::arg("img_bias"), py::arg("res"),
+        py::arg("out"), py::arg("B"), py::arg("IH"), py::arg("IW"), py::arg("Cin"), py::arg("OH"),
+        py::arg("OW"), py::arg("Cout"), py::arg("KH"), py::arg("KW"), py::arg("stride"),
+        py::arg("dil"), py::arg("ldo"), py::arg("co_off"), py::arg("ldr"), py::arg("act"),
+        py::arg("stream"), py::arg("variant") = 0);
 
   m.def("depthwise3x3",
         [](uintptr_t in, uintptr_t w, uintptr_t bias, uintptr_t out, int B, int IH, int IW, int C,

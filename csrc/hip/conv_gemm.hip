@@ -150,6 +150,233 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// LDS-staged variant for the compute-heavy shapes (M = B*OH*OW large).
+//
+// Block tile: BM = 32*MT pixels x BN = 32*NT output channels, 4 waves (2 x 2),
+// wave tile (16*MT) x (16*NT). K is walked in stages of 32*KS elements of one
+// tap: every thread loads its 16-byte chunks of the pixel tile (gathered through
+// the tap's spatial shift, zero outside the image) and of the weight tile into
+// registers, the registers land in an XOR-swizzled LDS image (chunk ^ (row & 7):
+// the 16 rows a ds_read_b128 lane group touches spread over 8 bank slots), and
+// the next stage's global loads are issued before the current stage's MFMAs so
+// their latency hides under the math (one barrier per stage, 2 LDS buffers).
+// Taps whose receptive shift puts every pixel of the block tile outside the
+// image are skipped block-uniformly.
+template <int MT, int NT, int KS>
+__global__ __launch_bounds__(256) void conv_gemm_lds_kernel(ConvArgs a) {
+  constexpr int BM = 32 * MT, BN = 32 * NT, BKE = 32 * KS;  // BKE: K elements per stage
+  constexpr int CPR = BKE / 8;                               // 16-B chunks per row
+  constexpr int PCH = BM * CPR / 256, WCH = (BN * CPR + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* sP = reinterpret_cast<bf16*>(smem);                  // [2][BM][BKE]
+  bf16* sW = sP + 2 * BM * BKE;                              // [2][BN][BKE]
+  int& s_tapmask = *reinterpret_cast<int*>(sW + 2 * BN * BKE);  // one LDS array only
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int M = a.B * a.OH * a.OW;
+  const int tiles_m = cdiv_dev(M, BM), tiles_n = cdiv_dev(a.Cout, BN);
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tn = bid % tiles_n, tm = bid / tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int taps = a.KH * a.KW;
+
+  // staged pixel rows of this thread
+  int rb[PCH], ry[PCH], rx[PCH], rkc[PCH], rrow[PCH];
+  bool rv[PCH];
+  int tapbits = 0;
+#pragma unroll
+  for (int i = 0; i < PCH; ++i) {
+    const int c = tid + 256 * i;
+    rrow[i] = c / CPR;
+    rkc[i] = c % CPR;
+    const int m = m0 + rrow[i];
+    rv[i] = m < M;
+    const int mm = rv[i] ? m : 0;
+    rb[i] = mm / (a.OH * a.OW);
+    const int rem = mm - rb[i] * a.OH * a.OW;
+    ry[i] = (rem / a.OW) * a.stride;
+    rx[i] = (rem % a.OW) * a.stride;
+    if (rv[i]) {
+      for (int t = 0; t < taps; ++t) {
+        const int iy = ry[i] + (t / a.KW - a.KH / 2) * a.dil;
+        const int ix = rx[i] + (t % a.KW - a.KW / 2) * a.dil;
+        if (iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW) tapbits |= 1 << t;
+      }
+    }
+  }
+  if (tid == 0) s_tapmask = 0;
+  __syncthreads();
+  if (tapbits) atomicOr(&s_tapmask, tapbits);
+  __syncthreads();
+  const int tapmask = s_tapmask;
+
+  const int cchunks = cdiv_dev(a.Cin, BKE);
+  const int total = taps * cchunks;
+  const long long wrow = (long long)taps * a.Cin;
+
+  bf16x8 pr[PCH], wr[WCH];
+  auto load = [&](int it) {
+    const int t = it / cchunks, c0 = (it % cchunks) * BKE;
+    const int dy = (t / a.KW - a.KH / 2) * a.dil, dx = (t % a.KW - a.KW / 2) * a.dil;
+#pragma unroll
+    for (int i = 0; i < PCH; ++i) {
+      const int iy = ry[i] + dy, ix = rx[i] + dx;
+      const int c = c0 + rkc[i] * 8;
+      const bool ok = rv[i] && c < a.Cin && iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW;
+      pr[i] = ok ? ld8(a.in + (((long long)rb[i] * a.IH + iy) * a.IW + ix) * a.Cin + c) : zero8();
+    }
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) {
+      const int cidx = tid + 256 * i;
+      const int n = cidx / CPR, c = c0 + (cidx % CPR) * 8;
+      const bool ok = cidx < BN * CPR && n0 + n < a.Cout && c < a.Cin;
+      wr[i] = ok ? ld8(a.w + (long long)(n0 + n) * wrow + (long long)t * a.Cin + c) : zero8();
+    }
+  };
+  auto store = [&](int buf) {
+    bf16* P = sP + buf * BM * BKE;
+    bf16* Wt = sW + buf * BN * BKE;
+#pragma unroll
+    for (int i = 0; i < PCH; ++i) {
+      const int r = rrow[i];
+      st8(P + r * BKE + ((rkc[i] ^ (r & (CPR - 1))) * 8), pr[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) {
+      const int cidx = tid + 256 * i;
+      if (cidx < BN * CPR) {
+        const int n = cidx / CPR, kc = cidx % CPR;
+        st8(Wt + n * BKE + ((kc ^ (n & (CPR - 1))) * 8), wr[i]);
+      }
+    }
+  };
+  auto next_valid = [&](int it) {
+    while (it < total && !((tapmask >> (it / cchunks)) & 1)) ++it;
+    return it;
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int r16 = lane & 15, kq = lane >> 4;
+  int it = next_valid(0);
+  int buf = 0;
+  if (it < total) {
+    load(it);
+    store(0);
+  }
+  __syncthreads();
+  while (it < total) {
+    const int nit = next_valid(it + 1);
+    if (nit < total) load(nit);
+    const bf16* P = sP + buf * BM * BKE;
+    const bf16* Wt = sW + buf * BN * BKE;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 bfr[MT], afr[NT];
+      const int kc = ks * 4 + kq;
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int r = wm * 16 * MT + i * 16 + r16;
+        bfr[i] = ld8(P + r * BKE + ((kc ^ (r & (CPR - 1))) * 8));
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = wn * 16 * NT + j * 16 + r16;
+        afr[j] = ld8(Wt + n * BKE + ((kc ^ (n & (CPR - 1))) * 8));
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[j], bfr[i], acc[i][j], 0, 0, 0);
+    }
+    if (nit < total) store(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+    it = nit;
+  }
+
+  // epilogue: lane holds channels n0 + wn*16*NT + j*16 + kq*4 + {0..3} of pixel m
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int m = m0 + wm * 16 * MT + i * 16 + r16;
+    if (m >= M) continue;
+    const int b = m / (a.OH * a.OW);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = n0 + wn * 16 * NT + j * 16 + kq * 4;
+      if (n >= a.Cout) continue;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      const bool full = n + 3 < a.Cout;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (n + q < a.Cout) {
+          v[q] += a.bias[n + q];
+          if (a.img_bias) v[q] += a.img_bias[(long long)b * a.Cout + n + q];
+        }
+      }
+      if (a.res) {
+        const bf16* rp = a.res + (long long)m * a.ldr + n;
+        if (full && (a.ldr & 3) == 0) {
+          const bf16x4 rv4 = *reinterpret_cast<const bf16x4*>(rp);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] += (float)rv4[q];
+        } else {
+          for (int q = 0; q < 4; ++q) if (n + q < a.Cout) v[q] += (float)rp[q];
+        }
+      }
+      bf16* op = a.out + (long long)m * a.ldo + a.co_off + n;
+      if (full && ((a.ldo | a.co_off) & 3) == 0) {
+        bf16x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = (bf16)apply_act(v[q], a.act);
+        *reinterpret_cast<bf16x4*>(op) = o;
+      } else {
+        for (int q = 0; q < 4; ++q)
+          if (n + q < a.Cout) op[q] = (bf16)apply_act(v[q], a.act);
+      }
+    }
+  }
+}
+
+template <int MT, int NT, int KS>
+static void launch_conv_lds(const ConvArgs& a, hipStream_t s) {
+  const int M = a.B * a.OH * a.OW;
+  const int grid = cdiv(M, 32 * MT) * cdiv(a.Cout, 32 * NT);
+  const size_t lds = (size_t)2 * (32 * MT + 32 * NT) * 32 * KS * sizeof(bf16) + 16;
+  hipLaunchKernelGGL((conv_gemm_lds_kernel<MT, NT, KS>), dim3(grid), dim3(256), lds, s, a);
+  check_launch("conv_gemm_lds");
+}
+
+// channel-tile choice: NT in 1..6 (BN = 32*NT) minimising padded columns
+static int pick_nt(int Cout) {
+  if (Cout <= 192) return (Cout + 31) / 32;
+  int best = 4, waste = 1 << 30;
+  for (int nt = 6; nt >= 4; --nt) {
+    const int w = cdiv(Cout, 32 * nt) * 32 * nt - Cout;
+    if (w < waste) { waste = w; best = nt; }
+  }
+  return best;
+}
+
+template <int KS>
+static void dispatch_lds(const ConvArgs& a, hipStream_t s) {
+  switch (pick_nt(a.Cout)) {
+    case 1: launch_conv_lds<4, 1, KS>(a, s); break;
+    case 2: launch_conv_lds<4, 2, KS>(a, s); break;
+    case 3: launch_conv_lds<4, 3, KS>(a, s); break;
+    case 4: launch_conv_lds<4, 4, KS>(a, s); break;
+    case 5: launch_conv_lds<4, 5, KS>(a, s); break;
+    default: launch_conv_lds<4, 6, KS>(a, s); break;
+  }
+}
+
 template <int MT, int NT>
 static void launch_conv(const ConvArgs& a, hipStream_t s) {
   const int M = a.B * a.OH * a.OW;
@@ -165,7 +392,17 @@ void conv_gemm(const ConvParams& p, hipStream_t s) {
   ConvArgs a{p.in, p.w, p.bias, p.img_bias, p.res, p.out, p.B, p.IH, p.IW, p.Cin, p.OH, p.OW,
              p.Cout, p.KH, p.KW, p.stride, p.dil, p.ldo, p.co_off, p.ldr, p.act};
   const long long M = (long long)p.B * p.OH * p.OW;
-  // tile choice: wide channel tiles for wide outputs, narrow for the thin ones
+  const long long tiles = (M + 127) / 128 * cdiv(p.Cout, 32 * pick_nt(p.Cout));
+  const long long K = (long long)p.KH * p.KW * p.Cin;
+  if (p.variant == 2 || (p.variant == 0 && tiles >= 256 && K >= 512)) {
+    // LDS-staged MFMA path: deep K (ASPP atrous 2880, projections 576-1024) and
+    // enough 128-pixel tiles to fill the chip. Shallow-K layers are write-bound
+    // and measured faster on the register-fed kernel (rocprof, B=32 MNv2).
+    if (p.Cin <= 32) dispatch_lds<1>(a, s);
+    else dispatch_lds<2>(a, s);
+    return;
+  }
+  // direct path (small M, e.g. batch-1 33x33 maps): smaller tiles, more blocks
   if (p.Cout <= 32) {
     launch_conv<4, 1>(a, s);  // 128 px x 32 ch
   } else if (p.Cout <= 64 || M < 8192) {

@@ -19,6 +19,7 @@ struct ConvParams {
   int B = 0, IH = 0, IW = 0, Cin = 0, OH = 0, OW = 0, Cout = 0;
   int KH = 1, KW = 1, stride = 1, dil = 1;
   int ldo = 0, co_off = 0, ldr = 0, act = 0;
+  int variant = 0;  // 0 auto, 1 direct (register-fed), 2 LDS-staged
 };
 void conv_gemm(const ConvParams& p, hipStream_t s);
 

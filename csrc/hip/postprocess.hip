@@ -8,13 +8,14 @@
 // tests check these kernels against it and against the exact host tracer.
 //
 // Pipeline (fixed launch sequence, no host round trip, hipGraph-capturable):
-//   k_mask_init  palette -> 3x3 box blur (REFLECT_101, rounded) -> BGR2GRAY on
-//                RGB (fixed point) -> > thr; union-find init
-//   k_merge      union-find (atomicMin, Playne-Hawick style): foreground
-//                8-connected, background 4-connected, border background joined
-//                to the virtual "outside" node 0
-//   k_compress   label = root (root = raster index of the component's first
-//                pixel + 1, 0 = outside)
+//   k_ccl_local  per 32x8 tile: palette -> 3x3 box blur (REFLECT_101, rounded) ->
+//                BGR2GRAY on RGB (fixed point) -> > thr, then union-find in LDS:
+//                foreground 8-connected, background 4-connected
+//   k_ccl_boundary  global union-find (atomicMin, Playne-Hawick style) only
+//                across tile edges; image-border background joins the virtual
+//                "outside" node 0
+//   k_compress   label = root with path halving (root = raster index of the
+//                component's first pixel + 1, 0 = outside)
 //   k_roots      per component: zero accumulators, parent in the border tree
 //   k_quads      per 2x2 quad: polygon pieces (full square / triangle) as exact
 //                integer moments a00 = 2A, a10 = 6*int x, a01 = 6*int y
@@ -118,10 +119,21 @@ __device__ int find_root(int32_t* L, int x) {
   return x;
 }
 
+__device__ __forceinline__ int find_halving(int32_t* L, int x) {
+  int y = ld_relaxed(L + x);
+  while (y != x) {
+    const int z = ld_relaxed(L + y);
+    if (z != y) __hip_atomic_store(L + x, z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    x = y;
+    y = z;
+  }
+  return x;
+}
+
 __device__ void unite(int32_t* L, int a, int b) {
   for (int guard = 0; guard < (1 << 24); ++guard) {
-    a = find_root(L, a);
-    b = find_root(L, b);
+    a = find_halving(L, a);
+    b = find_halving(L, b);
     if (a == b) return;
     if (a < b) {
       const int old = atomicMin(L + b, a);
@@ -135,60 +147,137 @@ __device__ void unite(int32_t* L, int a, int b) {
   }
 }
 
-// ---------------------------------------------------------------- mask + init
-__global__ __launch_bounds__(256) void k_mask_init(KArgs a, const int32_t* __restrict__ pal) {
-  __shared__ int spal[256 * 3];
-  for (int i = threadIdx.x; i < 256 * 3; i += blockDim.x) spal[i] = pal[i];
-  __syncthreads();
-  const int b = blockIdx.y;
-  const int N = a.ch * a.cw;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
-  if (p == 0) f.L[0] = 0;
-  if (p >= N) return;
-  const int y = p / a.cw, x = p - y * a.cw;
-  const uint8_t* lab = a.labels + (size_t)b * a.H * a.W;
-  int s0 = 0, s1 = 0, s2 = 0;
-#pragma unroll
-  for (int dy = -1; dy <= 1; ++dy) {
-    const int yy = reflect101(y + dy, a.ch);
-#pragma unroll
-    for (int dx = -1; dx <= 1; ++dx) {
-      const int xx = reflect101(x + dx, a.cw);
-      const int l = lab[yy * a.W + xx];
-      s0 += spal[l * 3 + 0];
-      s1 += spal[l * 3 + 1];
-      s2 += spal[l * 3 + 2];
-    }
-  }
-  const int c0 = (s0 * 2 + 9) / 18, c1 = (s1 * 2 + 9) / 18, c2 = (s2 * 2 + 9) / 18;
-  const int g = (c0 * 1868 + c1 * 9617 + c2 * 4899 + (1 << 13)) >> 14;
-  f.mask[p] = g > a.thr ? 1 : 0;
-  f.L[p + 1] = p + 1;
+// ---------------------------------------------------------------- mask + local CCL
+// One 256-thread block = one TW x TH pixel tile. Each thread computes its pixel's
+// mask bit (palette -> 3x3 blur -> gray -> threshold) and the tile's connected
+// components are resolved with union-find on LDS labels; the global label of a
+// pixel is then the raster index (+1) of its tile-local root, which is also the
+// tile-local minimum, so the global min-root invariant is preserved.
+constexpr int TW = 32, TH = 8;
+
+__device__ __forceinline__ int lds_ld(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// ---------------------------------------------------------------- merge
-__global__ __launch_bounds__(256) void k_merge(KArgs a) {
+__device__ int lfind(int* l, int x) {
+  int y = lds_ld(l + x);
+  while (y != x) {
+    x = y;
+    y = lds_ld(l + x);
+  }
+  return x;
+}
+
+__device__ void lunite(int* l, int a, int b) {
+  for (;;) {
+    a = lfind(l, a);
+    b = lfind(l, b);
+    if (a == b) return;
+    if (a < b) {
+      const int old = atomicMin(l + b, a);
+      if (old == b) return;
+      b = old;
+    } else {
+      const int old = atomicMin(l + a, b);
+      if (old == a) return;
+      a = old;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_ccl_local(KArgs a, const int32_t* __restrict__ pal) {
+  __shared__ int spal[256 * 3];
+  __shared__ int lbl[TW * TH];
+  __shared__ uint8_t msk[TW * TH];
+  for (int i = threadIdx.x; i < 256 * 3; i += blockDim.x) spal[i] = pal[i];
+  const int b = blockIdx.z;
+  const int tx = threadIdx.x % TW, ty = threadIdx.x / TW;
+  const int x = blockIdx.x * TW + tx, y = blockIdx.y * TH + ty;
+  const bool in = x < a.cw && y < a.ch;
+  FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) f.L[0] = 0;
+  __syncthreads();
+  uint8_t m = 0;
+  if (in) {
+    const uint8_t* lab = a.labels + (size_t)b * a.H * a.W;
+    int s0 = 0, s1 = 0, s2 = 0;
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int yy = reflect101(y + dy, a.ch);
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int xx = reflect101(x + dx, a.cw);
+        const int l = lab[yy * a.W + xx];
+        s0 += spal[l * 3 + 0];
+        s1 += spal[l * 3 + 1];
+        s2 += spal[l * 3 + 2];
+      }
+    }
+    const int c0 = (s0 * 2 + 9) / 18, c1 = (s1 * 2 + 9) / 18, c2 = (s2 * 2 + 9) / 18;
+    const int g = (c0 * 1868 + c1 * 9617 + c2 * 4899 + (1 << 13)) >> 14;
+    m = g > a.thr ? 1 : 0;
+    f.mask[y * a.cw + x] = m;
+  }
+  const int me = threadIdx.x;
+  msk[me] = in ? m : 2;  // 2 = outside the crop (never joins anything)
+  lbl[me] = me;
+  __syncthreads();
+  if (in) {
+    if (m) {
+      if (tx > 0 && msk[me - 1] == 1) lunite(lbl, me, me - 1);
+      if (ty > 0) {
+        const int up = me - TW;
+        if (msk[up] == 1) lunite(lbl, me, up);
+        if (tx > 0 && msk[up - 1] == 1) lunite(lbl, me, up - 1);
+        if (tx + 1 < TW && msk[up + 1] == 1) lunite(lbl, me, up + 1);
+      }
+    } else {
+      if (tx > 0 && msk[me - 1] == 0) lunite(lbl, me, me - 1);
+      if (ty > 0 && msk[me - TW] == 0) lunite(lbl, me, me - TW);
+    }
+  }
+  __syncthreads();
+  if (in) {
+    const int r = lfind(lbl, me);
+    const int rx = blockIdx.x * TW + r % TW, ry = blockIdx.y * TH + r / TW;
+    f.L[y * a.cw + x + 1] = ry * a.cw + rx + 1;
+  }
+}
+
+// Cross-tile merges (and image-border background -> outside node 0). Only
+// pixels on a tile's left column / top row or on the image border do work.
+__global__ __launch_bounds__(256) void k_ccl_boundary(KArgs a) {
   const int b = blockIdx.y;
   const int N = a.ch * a.cw;
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= N) return;
-  FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
   const int y = p / a.cw, x = p - y * a.cw;
+  const bool left = x > 0 && (x % TW) == 0;
+  const bool top = y > 0 && (y % TH) == 0;
+  const bool edge = x == 0 || y == 0 || x == a.cw - 1 || y == a.ch - 1;
+  const bool rtile = (x % TW) == TW - 1 && x + 1 < a.cw && y > 0;  // up-right neighbour in next tile
+  if (!left && !top && !edge && !rtile) return;
+  FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
   const uint8_t m = f.mask[p];
   const int me = p + 1;
   if (m) {
-    if (x > 0 && f.mask[p - 1]) unite(f.L, me, me - 1);
+    if (left && f.mask[p - 1]) unite(f.L, me, me - 1);
     if (y > 0) {
       const int up = p - a.cw;
-      if (f.mask[up]) unite(f.L, me, up + 1);
-      if (x > 0 && f.mask[up - 1]) unite(f.L, me, up);
-      if (x + 1 < a.cw && f.mask[up + 1]) unite(f.L, me, up + 2);
+      if (top) {
+        if (f.mask[up]) unite(f.L, me, up + 1);
+        if (x > 0 && f.mask[up - 1]) unite(f.L, me, up);
+        if (x + 1 < a.cw && f.mask[up + 1]) unite(f.L, me, up + 2);
+      } else {
+        // same tile row: diagonals that cross a vertical tile edge
+        if (left && f.mask[up - 1]) unite(f.L, me, up);
+        if (rtile && f.mask[up + 1]) unite(f.L, me, up + 2);
+      }
     }
   } else {
-    if (x > 0 && !f.mask[p - 1]) unite(f.L, me, me - 1);
-    if (y > 0 && !f.mask[p - a.cw]) unite(f.L, me, me - a.cw);
-    if (x == 0 || y == 0 || x == a.cw - 1 || y == a.ch - 1) unite(f.L, me, 0);
+    if (left && !f.mask[p - 1]) unite(f.L, me, me - 1);
+    if (top && !f.mask[p - a.cw]) unite(f.L, me, me - a.cw);
+    if (edge) unite(f.L, me, 0);
   }
 }
 
@@ -198,7 +287,12 @@ __global__ __launch_bounds__(256) void k_compress(KArgs a) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= N) return;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
-  f.L[p + 1] = find_root(f.L, p + 1);
+  // Read-only traversal: a path-halving store here could overwrite another
+  // thread's final root store with a stale grandparent (observed: 1 pixel in ~1M
+  // left pointing at a non-root). Every concurrent store below writes a root, so
+  // plain traversal always terminates at the true root.
+  const int r = find_root(f.L, p + 1);
+  __hip_atomic_store(f.L + p + 1, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------- roots
@@ -540,8 +634,9 @@ void postprocess(const PostParams& p, hipStream_t s) {
     return e ? atoi(e) : 99;
   }();
   int st = 0;
-  if (st++ < stages) hipLaunchKernelGGL(k_mask_init, gp, blk, 0, s, a, p.palette);
-  if (st++ < stages) hipLaunchKernelGGL(k_merge, gp, blk, 0, s, a);
+  const dim3 gt(cdiv(p.crop_w, TW), cdiv(p.crop_h, TH), p.B);
+  if (st++ < stages) hipLaunchKernelGGL(k_ccl_local, gt, blk, 0, s, a, p.palette);
+  if (st++ < stages) hipLaunchKernelGGL(k_ccl_boundary, gp, blk, 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_compress, gp, blk, 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_roots, gp, blk, 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_quads, gq, blk, 0, s, a);

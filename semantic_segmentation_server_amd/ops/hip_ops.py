@@ -61,8 +61,8 @@ def conv_gemm(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out: torch.T
               B: int, IH: int, IW: int, Cin: int, OH: int, OW: int, Cout: int, k: int = 1,
               stride: int = 1, dil: int = 1, ldo: Optional[int] = None, co_off: int = 0,
               act=None, res: Optional[torch.Tensor] = None, ldr: Optional[int] = None,
-              img_bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """NHWC implicit-GEMM conv. x: [B,IH,IW,Cin] bf16; w: [Cout,k,k,Cin] bf16;
+              img_bias: Optional[torch.Tensor] = None, variant: int = 0) -> torch.Tensor:
+    """NHWC implicit-GEMM conv (variant: 0 auto, 1 register-fed, 2 LDS-staged). x: [B,IH,IW,Cin] bf16; w: [Cout,k,k,Cin] bf16;
     out: [B,OH,OW,ldo] bf16 written at channel offset co_off."""
     ldo = Cout if ldo is None else ldo
     ldr = Cout if ldr is None else ldr
@@ -80,7 +80,7 @@ def conv_gemm(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out: torch.T
         _chk(img_bias, torch.float32, "img_bias", B * Cout)
     _hip_mod().conv_gemm(_ptr(x), _ptr(w), _ptr(bias), _ptr(img_bias), _ptr(res), _ptr(out), B, IH,
                          IW, Cin, OH, OW, Cout, k, k, stride, dil, ldo, co_off, ldr, ACT[act],
-                         _stream())
+                         _stream(), variant)
     _dbg('conv_gemm')
     return out
 

@@ -45,8 +45,13 @@ def _nchw(x):
     (2, 21, 23, 64, 64, 3, 2, 1, "relu", False, 0, 0),
     (2, 21, 23, 64, 256, 1, 2, 1, None, False, 0, 0),
     (3, 9, 11, 8, 40, 3, 1, 2, "relu", False, 0, 0),
+    (2, 33, 33, 960, 160, 1, 1, 1, None, True, 0, 0),
+    (2, 33, 33, 96, 576, 1, 1, 1, "relu6", False, 0, 0),
+    (2, 65, 65, 144, 32, 1, 1, 1, None, False, 0, 0),
+    (1, 33, 33, 1024, 256, 1, 1, 1, "relu", False, 0, 0),
 ])
-def test_conv_gemm(B, H, W, Cin, Cout, k, stride, dil, act, res, ldo_pad, co_off):
+@pytest.mark.parametrize("variant", [1, 2])
+def test_conv_gemm(B, H, W, Cin, Cout, k, stride, dil, act, res, ldo_pad, co_off, variant):
     K = _hip()
     g = torch.Generator(device="cpu").manual_seed(1)
     x = torch.randn(B, Cin, H, W, generator=g).to(torch.bfloat16)
@@ -67,7 +72,7 @@ def test_conv_gemm(B, H, W, Cin, Cout, k, stride, dil, act, res, ldo_pad, co_off
     K.conv_gemm(_nhwc(x).to(DEV), w.permute(0, 2, 3, 1).contiguous().to(DEV), b.to(DEV), out,
                 B=B, IH=H, IW=W, Cin=Cin, OH=OH, OW=OW, Cout=Cout, k=k, stride=stride, dil=dil,
                 ldo=ldo, co_off=co_off, act=act,
-                res=None if r is None else _nhwc(r).to(DEV))
+                res=None if r is None else _nhwc(r).to(DEV), variant=variant)
     torch.cuda.synchronize()
     got = out[..., co_off:co_off + Cout]
     assert _rel(_nchw(got).cpu(), ref) < 1e-2
