@@ -37,6 +37,19 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("dil"), py::arg("ldo"), py::arg("co_off"), py::arg("ldr"), py::arg("act"),
         py::arg("stream"), py::arg("variant") = 0);
 
+  m.def("fused_ir",
+        [](uintptr_t in, uintptr_t we, uintptr_t be, uintptr_t wd, uintptr_t bd, uintptr_t wp,
+           uintptr_t bp, uintptr_t out, int B, int IH, int IW, int Cin, int CinP, int hidP,
+           int Cout, int OH, int OW, int stride, int residual, uintptr_t stream) {
+          FusedIRParams p;
+          p.in = P<const bf16>(in); p.we = P<const bf16>(we); p.be = P<const float>(be);
+          p.wd = P<const float>(wd); p.bd = P<const float>(bd); p.wp = P<const bf16>(wp);
+          p.bp = P<const float>(bp); p.out = P<bf16>(out);
+          p.B = B; p.IH = IH; p.IW = IW; p.Cin = Cin; p.CinP = CinP; p.hidP = hidP; p.Cout = Cout;
+          p.OH = OH; p.OW = OW; p.stride = stride; p.residual = residual;
+          fused_inverted_residual(p, S(stream));
+        });
+
   m.def("depthwise3x3",
         [](uintptr_t in, uintptr_t w, uintptr_t bias, uintptr_t out, int B, int IH, int IW, int C,
            int OH, int OW, int stride, int dil, int act, uintptr_t stream) {

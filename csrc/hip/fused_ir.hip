@@ -1,0 +1,258 @@
+// Fused MobileNetV2 inverted-residual block for gfx950:
+//   out = project( relu6( dw3x3( relu6( expand(x) ) ) ) ) [+ x]
+// in ONE kernel, for the high-resolution blocks (257^2 / 129^2 / 65^2 maps) where
+// the unfused pipeline is purely HBM-bound: the 6x-expanded tensor and the
+// depthwise output never leave the CU.
+//
+// Workgroup = one (4*GPW) x 16 output tile of one image, 4 waves; wave w owns
+// output rows GPW*w .. GPW*w+GPW-1 (16-pixel MFMA column groups).
+//   1. The input tile with its halo ((8-1)*s+3) x ((16-1)*s+3) pixels x Cin is
+//      staged once in LDS (zero outside the image and beyond Cin).
+//   2. The hidden dimension is streamed in 32-channel chunks:
+//      a. expand on MFMA (v_mfma_f32_16x16x32_bf16, A = expand weights,
+//         B = input-tile pixels from LDS) + bias + ReLU6 -> LDS chunk E
+//         (zeroed outside the image: the depthwise zero-padding applies to the
+//         expanded tensor, not to relu6(bias));
+//      b. 3x3 depthwise on the VALU from E: each lane computes 8 channels of one
+//         output pixel, which is exactly its B fragment for the projection MFMA
+//         (lane l: pixel l&15, channels 8*(l>>4)..+7), so the depthwise result
+//         goes straight from registers into the MFMA;
+//      c. project on MFMA into fp32 register accumulators.
+//   3. Epilogue: + bias (+ residual read from the LDS input tile), bf16 store.
+// Host-side packing pads Cin to a multiple of 32 and hid to a multiple of 32
+// with zero weights, so every MFMA is full and no K masking is needed.
+#include "common.h"
+#include "kernels.h"
+
+namespace ssa {
+namespace {
+
+constexpr int TW = 16;
+
+struct IRArgs {
+  const bf16* in;   // [B, IH, IW, Cin]
+  const bf16* we;   // [hidP, CinP] (null: no expansion, hid == Cin)
+  const float* be;  // [hidP]
+  const float* wd;  // [9, hidP]
+  const float* bd;  // [hidP]
+  const bf16* wp;   // [CoutP, hidP]
+  const float* bp;  // [CoutP]
+  bf16* out;        // [B, OH, OW, Cout]
+  int B, IH, IW, Cin, CinP, hidP, Cout, OH, OW, stride, residual;
+};
+
+template <int NSUB, bool EXPAND, int GPW>
+__global__ __launch_bounds__(256) void fused_ir_kernel(IRArgs a) {
+  constexpr int TH = 4 * GPW;  // wave w owns output rows GPW*w .. GPW*w + GPW-1
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int s = a.stride;
+  const int TIH = (TH - 1) * s + 3, TIW = (TW - 1) * s + 3;
+  const int in_px = TIH * TIW;
+  const int in_groups = (in_px + 15) / 16;
+  const int CinP = a.CinP;
+  // LDS rows padded by 16 B: a 64-B (or 128-B) row stride puts the 16 lanes of a
+  // ds_read_b128 group on 4 bank slots; +16 B spreads them over all 16.
+  const int XS = CinP + 8, ES = 32 + 8;                   // row strides (elements)
+  bf16* X = reinterpret_cast<bf16*>(smem);                // [in_groups*16][XS]
+  bf16* E = X + (size_t)in_groups * 16 * XS;              // [in_groups*16][ES]
+
+  const int tiles_x = cdiv_dev(a.OW, TW), tiles_y = cdiv_dev(a.OH, TH);
+  const int b = blockIdx.x / (tiles_x * tiles_y);
+  const int t = blockIdx.x % (tiles_x * tiles_y);
+  const int oy0 = (t / tiles_x) * TH, ox0 = (t % tiles_x) * TW;
+  const int iy0 = oy0 * s - 1, ix0 = ox0 * s - 1;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+
+  // ---- 1. stage the input tile (16-byte chunks, zero outside image / Cin)
+  const int cpp = CinP / 8;
+  for (int i = tid; i < in_groups * 16 * cpp; i += 256) {
+    const int ip = i / cpp, c = (i % cpp) * 8;
+    const int ty = ip / TIW, tx = ip % TIW;
+    const int iy = iy0 + ty, ix = ix0 + tx;
+    bf16x8 v = zero8();
+    if (ip < in_px && c < a.Cin && iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW)
+      v = ld8(a.in + (((long long)b * a.IH + iy) * a.IW + ix) * a.Cin + c);
+    st8(X + (size_t)ip * XS + c, v);
+  }
+  __syncthreads();
+
+  f32x4 acc[GPW][NSUB];
+#pragma unroll
+  for (int g = 0; g < GPW; ++g)
+#pragma unroll
+    for (int n = 0; n < NSUB; ++n) acc[g][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int hid = EXPAND ? a.hidP : CinP;
+  for (int c0 = 0; c0 < hid; c0 += 32) {
+    // ---- 2a. expand chunk -> E (MFMA), or alias the input channels
+    if (EXPAND) {
+      // chunk weights and biases: loop-invariant over the pixel groups
+      bf16x8 wfr[2][2];
+      float bias[2][4];
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        const bf16* wrow = a.we + (size_t)(c0 + sub * 16 + r16) * CinP;
+        wfr[sub][0] = ld8(wrow + kq * 8);
+        wfr[sub][1] = CinP > 32 ? ld8(wrow + 32 + kq * 8) : zero8();
+        const float4 bv = *reinterpret_cast<const float4*>(a.be + c0 + sub * 16 + kq * 4);
+        bias[sub][0] = bv.x; bias[sub][1] = bv.y; bias[sub][2] = bv.z; bias[sub][3] = bv.w;
+      }
+      for (int gi = wid; gi < in_groups; gi += 4) {
+        const int ip = gi * 16 + r16;
+        const int ty = ip / TIW, tx = ip - ty * TIW;
+        const int iy = iy0 + ty, ix = ix0 + tx;
+        const bool inside = ip < in_px && iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW;
+        const bf16x8 x0 = ld8(X + (size_t)ip * XS + kq * 8);
+        const bf16x8 x1 = CinP > 32 ? ld8(X + (size_t)ip * XS + 32 + kq * 8) : zero8();
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+          f32x4 e = {0.f, 0.f, 0.f, 0.f};
+          e = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[sub][0], x0, e, 0, 0, 0);
+          if (CinP > 32) e = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[sub][1], x1, e, 0, 0, 0);
+          // lane holds hidden channels c0 + sub*16 + kq*4 + q of input pixel ip
+          bf16x4 o;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float v = fminf(fmaxf(e[q] + bias[sub][q], 0.f), 6.f);
+            o[q] = (bf16)(inside ? v : 0.f);
+          }
+          *reinterpret_cast<bf16x4*>(E + (size_t)ip * ES + sub * 16 + kq * 4) = o;
+        }
+      }
+      __syncthreads();
+    }
+    const bf16* src = EXPAND ? E : X + c0;
+    const int sstride = EXPAND ? ES : XS;
+
+    // ---- 2b. depthwise for this lane's 8 channels of its two output pixels
+    // (both pixels per tap, so each tap's weights are loaded once and live briefly)
+    const float4 b0 = *reinterpret_cast<const float4*>(a.bd + c0 + kq * 8);
+    const float4 b1 = *reinterpret_cast<const float4*>(a.bd + c0 + kq * 8 + 4);
+    float d[GPW][8];
+#pragma unroll
+    for (int g = 0; g < GPW; ++g) {
+      d[g][0] = b0.x; d[g][1] = b0.y; d[g][2] = b0.z; d[g][3] = b0.w;
+      d[g][4] = b1.x; d[g][5] = b1.y; d[g][6] = b1.z; d[g][7] = b1.w;
+    }
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int tap = ky * 3 + kx;
+        const float4 w0 = *reinterpret_cast<const float4*>(a.wd + tap * a.hidP + c0 + kq * 8);
+        const float4 w1 = *reinterpret_cast<const float4*>(a.wd + tap * a.hidP + c0 + kq * 8 + 4);
+        const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+        for (int g = 0; g < GPW; ++g) {
+          const int ip = ((wid * GPW + g) * s + ky) * TIW + r16 * s + kx;
+          const bf16x8 v = ld8(src + (size_t)ip * sstride + kq * 8);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) d[g][q] += (float)v[q] * wv[q];
+        }
+      }
+    bf16x8 dfrag[GPW];
+#pragma unroll
+    for (int g = 0; g < GPW; ++g)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) dfrag[g][q] = (bf16)fminf(fmaxf(d[g][q], 0.f), 6.f);
+
+    // ---- 2c. project chunk (MFMA), A = projection weights
+#pragma unroll
+    for (int n = 0; n < NSUB; ++n) {
+      const bf16x8 af = ld8(a.wp + (size_t)(n * 16 + r16) * a.hidP + c0 + kq * 8);
+#pragma unroll
+      for (int g = 0; g < GPW; ++g)
+        acc[g][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, dfrag[g], acc[g][n], 0, 0, 0);
+    }
+    if (EXPAND) __syncthreads();  // E is rewritten by the next chunk
+  }
+
+  // ---- 3. epilogue: lane holds out channels n*16 + kq*4 + q of pixel (ty, r16)
+#pragma unroll
+  for (int g = 0; g < GPW; ++g) {
+    const int ty = wid * GPW + g, tx = r16;
+    const int oy = oy0 + ty, ox = ox0 + tx;
+    if (oy >= a.OH || ox >= a.OW) continue;
+    bf16* op = a.out + (((long long)b * a.OH + oy) * a.OW + ox) * a.Cout;
+    const bf16* rp = X + (size_t)((ty * s + 1) * TIW + tx * s + 1) * (a.CinP + 8);
+#pragma unroll
+    for (int n = 0; n < NSUB; ++n) {
+      const int co = n * 16 + kq * 4;
+      if (co >= a.Cout) continue;
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[q] = acc[g][n][q] + a.bp[co + q];
+        if (a.residual) v[q] += (float)rp[co + q];
+      }
+      if (co + 3 < a.Cout && (a.Cout & 3) == 0) {
+        bf16x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = (bf16)v[q];
+        *reinterpret_cast<bf16x4*>(op + co) = o;
+      } else {
+        for (int q = 0; q < 4; ++q)
+          if (co + q < a.Cout) op[co + q] = (bf16)v[q];
+      }
+    }
+  }
+}
+
+template <int NSUB, bool EXPAND, int GPW>
+void launch_ir(const IRArgs& a, hipStream_t st) {
+  constexpr int TH = 4 * GPW;
+  const int s = a.stride;
+  const int in_px = ((TH - 1) * s + 3) * ((TW - 1) * s + 3);
+  const int in_groups = (in_px + 15) / 16;
+  const size_t lds = (size_t)in_groups * 16 * (a.CinP + 8 + (EXPAND ? 40 : 0)) * sizeof(bf16);
+  const int grid = a.B * cdiv(a.OH, TH) * cdiv(a.OW, TW);
+  static bool attr_set = false;  // > 64 KB of dynamic LDS needs the opt-in attribute
+  if (!attr_set) {
+    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_ir_kernel<NSUB, EXPAND, GPW>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
+          "fused_ir attr");
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((fused_ir_kernel<NSUB, EXPAND, GPW>), dim3(grid), dim3(256), lds, st, a);
+  check_launch("fused_ir");
+}
+
+}  // namespace
+
+void fused_inverted_residual(const FusedIRParams& p, hipStream_t st) {
+  if (p.stride != 1 && p.stride != 2) throw std::invalid_argument("fused_ir: stride must be 1 or 2");
+  if (p.CinP % 32 || p.hidP % 32 || p.CinP < p.Cin || p.CinP > 64)
+    throw std::invalid_argument("fused_ir: CinP must be 32 or 64 and >= Cin");
+  if (p.residual && (p.stride != 1 || p.Cin != p.Cout)) throw std::invalid_argument("fused_ir: bad residual");
+  if (p.Cin % 8) throw std::invalid_argument("fused_ir: Cin must be a multiple of 8");
+  IRArgs a{p.in, p.we, p.be, p.wd, p.bd, p.wp, p.bp, p.out, p.B, p.IH, p.IW, p.Cin, p.CinP,
+           p.hidP, p.Cout, p.OH, p.OW, p.stride, p.residual};
+  const int nsub = (p.Cout + 15) / 16;
+  const bool ex = p.we != nullptr;
+  if (!ex && p.hidP != p.CinP) throw std::invalid_argument("fused_ir: no-expand needs hidP == CinP");
+  // stride 2: 4-row tiles (9 x 33 input tile, ~49 KB LDS, 3 workgroups/CU);
+  // stride 1: 8-row tiles (10 x 18 input tile)
+#define IR_CASE(N)                                                   \
+  case N:                                                            \
+    if (p.stride == 2) {                                             \
+      if (ex) launch_ir<N, true, 1>(a, st);                          \
+      else launch_ir<N, false, 1>(a, st);                            \
+    } else {                                                         \
+      if (ex) launch_ir<N, true, 2>(a, st);                          \
+      else launch_ir<N, false, 2>(a, st);                            \
+    }                                                                \
+    break;
+  switch (nsub) {
+    IR_CASE(1)
+    IR_CASE(2)
+    IR_CASE(3)
+    IR_CASE(4)
+    IR_CASE(6)
+    default:
+      throw std::invalid_argument("fused_ir: unsupported Cout");
+  }
+#undef IR_CASE
+}
+
+}  // namespace ssa

@@ -23,6 +23,23 @@ struct ConvParams {
 };
 void conv_gemm(const ConvParams& p, hipStream_t s);
 
+// Fused MobileNetV2 inverted residual (expand 1x1 + ReLU6 -> dw 3x3 + ReLU6 ->
+// project 1x1 [+ residual]), dilation 1. Weights are host-padded: CinP, hidP
+// multiples of 32 (CinP <= 64), CoutP = 16 * ceil(Cout / 16).
+struct FusedIRParams {
+  const bf16* in = nullptr;   // [B, IH, IW, Cin]
+  const bf16* we = nullptr;   // [hidP, CinP] or null (no expansion: hidP == CinP)
+  const float* be = nullptr;  // [hidP]
+  const float* wd = nullptr;  // [9, hidP]
+  const float* bd = nullptr;  // [hidP]
+  const bf16* wp = nullptr;   // [CoutP, hidP]
+  const float* bp = nullptr;  // [CoutP]
+  bf16* out = nullptr;        // [B, OH, OW, Cout]
+  int B = 0, IH = 0, IW = 0, Cin = 0, CinP = 0, hidP = 0, Cout = 0, OH = 0, OW = 0;
+  int stride = 1, residual = 0;
+};
+void fused_inverted_residual(const FusedIRParams& p, hipStream_t s);
+
 // Depthwise KxK (K=3) conv, NHWC, pad = dil, bias + act. w: [9, C] fp32.
 void depthwise3x3(const bf16* in, const float* w, const float* bias, bf16* out, int B, int IH,
                   int IW, int C, int OH, int OW, int stride, int dil, int act, hipStream_t s);

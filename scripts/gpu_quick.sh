@@ -5,7 +5,7 @@ cd "$(dirname "$0")/.."
 REPO=$PWD
 mkdir -p gpurun_out
 export SSA_NO_AUTOBUILD=1
-timeout -k 10 600 python -m pytest tests/ -q -m gpu -x > gpurun_out/q_tests.log 2>&1
+timeout -k 10 600 python -m pytest tests/ -q -m gpu -x -s > gpurun_out/q_tests.log 2>&1
 rc=$?
 tail -6 gpurun_out/q_tests.log
 [ $rc -gt 1 ] && exit $rc

@@ -21,6 +21,7 @@ Layout decisions (MI355X-first, not a translation of the tflite graph):
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
@@ -47,6 +48,44 @@ def _pack_dw(layer: ConvBNAct, dev) -> Tuple[torch.Tensor, torch.Tensor]:
             b.contiguous().to(dev, torch.float32))
 
 
+class Choice:
+    """A plan step with alternative implementations; ``autotune`` keeps the
+    fastest on the actual shapes (timed with HIP events at plan build)."""
+
+    def __init__(self, name: str, variants: List[Tuple[str, List[Callable]]]):
+        self.name = name
+        self.variants = variants
+        self.pick = 0
+
+    def __call__(self, *args):
+        for op in self.variants[self.pick][1]:
+            op(*args)
+
+    def autotune(self, args, reps: int = 5) -> None:
+        mode = os.environ.get("SSA_FUSED_IR", "auto")
+        if mode in ("0", "1"):
+            want = "unfused" if mode == "0" else "fused"
+            self.pick = next((i for i, (n, _) in enumerate(self.variants) if n == want), 0)
+            return
+        if len(self.variants) < 2:
+            return
+        times = []
+        for _, ops in self.variants:
+            for _ in range(2):
+                for op in ops:
+                    op(*args)
+            st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            st.record()
+            for _ in range(reps):
+                for op in ops:
+                    op(*args)
+            en.record()
+            en.synchronize()
+            times.append(st.elapsed_time(en) / reps)
+        self.pick = min(range(len(times)), key=times.__getitem__)
+        self.times = times
+
+
 def _pack_stem(layer: ConvBNAct, dev) -> Tuple[torch.Tensor, torch.Tensor]:
     w, b = layer.fold()  # [Cout, 3, k, k] -> [k, k, 3, Cout]
     return (w.permute(2, 3, 1, 0).reshape(-1, w.shape[0]).contiguous().to(dev, torch.float32),
@@ -70,11 +109,22 @@ class HipDeepLab:
         if self.kind == "mnv2":
             for blk in bb.blocks:
                 s = blk.spec
-                self.blocks.append(dict(
+                d = dict(
                     spec=s,
                     expand=_pack_dense(blk.expand, dev) if blk.expand is not None else None,
                     dw=_pack_dw(blk.dw, dev),
-                    project=_pack_dense(blk.project, dev)))
+                    project=_pack_dense(blk.project, dev))
+                if s.dilation == 1 and s.cin <= 64 and s.cout <= 96 and s.cin % 8 == 0:
+                    ew = eb = None
+                    if blk.expand is not None:
+                        ew, eb = blk.expand.fold()
+                        ew = ew[:, :, 0, 0]
+                    dwf, dbf = blk.dw.fold()
+                    pwf, pbf = blk.project.fold()
+                    d["fused"] = K.pack_fused_ir(
+                        ew, eb, dwf[:, 0], dbf, pwf[:, :, 0, 0], pbf, Cin=s.cin, hid=s.hidden,
+                        Cout=s.cout, stride=s.stride, residual=s.residual, device=dev)
+                self.blocks.append(d)
         else:
             for blk in bb.blocks:
                 self.blocks.append(dict(
@@ -171,12 +221,30 @@ class HipDeepLab:
         ops.append(lambda *_, h=h, w=w: K.upsample_argmax(
             logits, labels, B=B, h=h, w=w, K=self.num_classes, ldk=self.ldk, H=H, W=W))
         self._plans[key] = (ops, bufs)
+        self._autotune(ops, B, Hc, Wc)
         return self._plans[key]
+
+    def _autotune(self, ops, B, Hc, Wc) -> None:
+        if torch.cuda.is_current_stream_capturing():
+            return
+        dev = self.device
+        frames = torch.zeros((B, Hc, Wc, 3), dtype=torch.uint8, device=dev)
+        lx = torch.zeros(self.W, dtype=torch.int32, device=dev)
+        ly = torch.zeros(self.H, dtype=torch.int32, device=dev)
+        for op in ops:  # populate every buffer once
+            op(frames, lx, ly)
+        for op in ops:
+            if isinstance(op, Choice):
+                op.autotune((frames, lx, ly))
+        torch.cuda.synchronize(dev)
+        self.choices = {op.name: op.variants[op.pick][0] for op in ops if isinstance(op, Choice)}
 
     def _mnv2_block(self, ops, buf, i, blk, x, B, h, w, c):
         s = blk["spec"]
         hid = s.hidden
         inp = x
+        unfused: List[Callable] = []
+        outer_ops, ops = ops, unfused
         if blk["expand"] is not None:
             ew, eb = blk["expand"]
             e = buf(f"b{i}_exp", B, h, w, hid)
@@ -195,6 +263,12 @@ class HipDeepLab:
         ops.append(lambda *_, d=d, out=out, OH=OH, OW=OW, res=res: K.conv_gemm(
             d, pw_, pb_, out, B=B, IH=OH, IW=OW, Cin=hid, OH=OH, OW=OW, Cout=s.cout, k=1,
             act=None, res=res))
+        variants = [("unfused", unfused)]
+        if "fused" in blk:
+            fp = blk["fused"]
+            variants.insert(0, ("fused", [lambda *_, x=inp, out=out, h=h, w=w, OH=OH, OW=OW:
+                                          K.fused_ir(x, fp, out, B=B, IH=h, IW=w, OH=OH, OW=OW)]))
+        outer_ops.append(Choice(f"block{i}", variants))
         return out, OH, OW, s.cout
 
     def _resnet_block(self, ops, buf, i, blk, x, B, h, w, c):

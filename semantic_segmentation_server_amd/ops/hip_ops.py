@@ -85,6 +85,60 @@ def conv_gemm(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out: torch.T
     return out
 
 
+def fused_ir(x, packed: dict, out, *, B, IH, IW, OH, OW):
+    """Fused inverted residual. ``packed`` from ``pack_fused_ir``."""
+    P = packed
+    _chk(x, torch.bfloat16, "x", B * IH * IW * P["Cin"])
+    _chk(out, torch.bfloat16, "out", B * OH * OW * P["Cout"])
+    if P["we"] is not None:
+        _chk(P["we"], torch.bfloat16, "we", P["hidP"] * P["CinP"])
+    _chk(P["wd"], torch.float32, "wd", 9 * P["hidP"])
+    _chk(P["wp"], torch.bfloat16, "wp", P["CoutP"] * P["hidP"])
+    exp_oh = (IH - 1) // P["stride"] + 1
+    if (OH, OW) != (exp_oh, (IW - 1) // P["stride"] + 1):
+        raise ValueError("fused_ir: output size mismatch")
+    _hip_mod().fused_ir(_ptr(x), _ptr(P["we"]), _ptr(P["be"]), _ptr(P["wd"]), _ptr(P["bd"]),
+                        _ptr(P["wp"]), _ptr(P["bp"]), _ptr(out), B, IH, IW, P["Cin"], P["CinP"],
+                        P["hidP"], P["Cout"], OH, OW, P["stride"], int(P["residual"]), _stream())
+    _dbg('fused_ir')
+    return out
+
+
+def pack_fused_ir(we, be, wd, bd, wp, bp, *, Cin, hid, Cout, stride, residual, device) -> dict:
+    """Zero-pad folded block weights to the fused kernel's layout.
+
+    we: [hid, Cin] (or None when the block has no expansion), wd: [hid, 3, 3],
+    wp: [Cout, hid]; biases fp32."""
+    r32 = lambda v: (v + 31) // 32 * 32
+    CinP = r32(Cin)
+    hidP = r32(hid) if we is not None else CinP
+    CoutP = (Cout + 15) // 16 * 16
+    f32 = dict(dtype=torch.float32, device=device)
+    out = dict(Cin=Cin, CinP=CinP, hidP=hidP, Cout=Cout, CoutP=CoutP, stride=stride,
+               residual=residual, we=None)
+    if we is not None:
+        t = torch.zeros(hidP, CinP, **f32)
+        t[:hid, :Cin] = we
+        out["we"] = t.to(torch.bfloat16).contiguous()
+    b = torch.zeros(hidP, **f32)
+    if be is not None:
+        b[:hid] = be
+    out["be"] = b
+    t = torch.zeros(9, hidP, **f32)
+    t[:, :hid] = wd.reshape(hid, 9).t()
+    out["wd"] = t.contiguous()
+    b = torch.zeros(hidP, **f32)
+    b[:hid] = bd
+    out["bd"] = b
+    t = torch.zeros(CoutP, hidP, **f32)
+    t[:Cout, :hid] = wp
+    out["wp"] = t.to(torch.bfloat16).contiguous()
+    b = torch.zeros(CoutP, **f32)
+    b[:Cout] = bp
+    out["bp"] = b
+    return out
+
+
 def depthwise3x3(x, w, bias, out, *, B, IH, IW, C, OH, OW, stride=1, dil=1, act="relu6"):
     """x: [B,IH,IW,C] bf16; w: [9, C] fp32; out: [B,OH,OW,C] bf16."""
     _chk(x, torch.bfloat16, "x", B * IH * IW * C)

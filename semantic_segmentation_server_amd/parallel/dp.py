@@ -79,9 +79,13 @@ class DataParallelPipeline:
                                           device=dev)
         self.K = int(engine.cfg.max_segments)
         self.rec_width = 1 + 5 * self.K
+        cdev = dev if ctx.backend == "nccl" else "cpu"
         if ctx.is_root and ctx.initialized:
             self.gather_buf = torch.empty((ctx.world, self.B, self.rec_width), dtype=torch.float32,
-                                          device=dev if ctx.backend == "nccl" else "cpu")
+                                          device=cdev)
+            self.meta_buf = torch.empty((ctx.world, self.B, 3), dtype=torch.float64, device=cdev)
+        self.meta = torch.zeros((self.B, 3), dtype=torch.float64, device=cdev)
+        self.meta_host = torch.zeros((self.B, 3), dtype=torch.float64, pin_memory=self.cuda)
         self.host_rec = torch.empty((ctx.world, self.B, self.rec_width), dtype=torch.float32,
                                     pin_memory=self.cuda)
         self.frames_done = 0
@@ -117,33 +121,51 @@ class DataParallelPipeline:
         return self.staging[s]
 
     # ---------------------------------------------------------------- step
-    def step(self, frame_ids=None, ts=None) -> np.ndarray:
-        """Run one step on the prefetched frames; returns rank-0 records (else empty)."""
+    def step(self, frame_ids=None, ts=None, streams=None) -> np.ndarray:
+        """Run one step on the prefetched frames; returns rank-0 records (else empty).
+
+        ``frame_ids``/``ts``/``streams`` describe this rank's B frames (defaults:
+        running counters, 0.0, rank * S + i % S). They travel with the records
+        through the gather so rank 0 can tag every record with its origin.
+        """
+        B = self.B
+        fids = list(frame_ids) if frame_ids is not None else \
+            list(range(self.frames_done // self.ctx.world, self.frames_done // self.ctx.world + B))
+        tss = list(ts) if ts is not None else [0.0] * B
+        strm = list(streams) if streams is not None else \
+            [self.ctx.rank * self.S + i % self.S for i in range(B)]
         frames = self._frames_for_step()
         labels, packed = self.engine.run_device(frames)
         if packed is None:  # host post-processing path (torch backend / exact mode)
-            recs = self.engine.records_from_labels(labels, list(range(self.B)), [0.0] * self.B, 0)
-            return recs
+            self.frames_done += B * self.ctx.world
+            return self.engine.records_from_labels(labels, fids, tss, strm)
         if self.ctx.initialized:
+            self.meta_host[:, 0] = torch.tensor(fids, dtype=torch.float64)
+            self.meta_host[:, 1] = torch.tensor(strm, dtype=torch.float64)
+            self.meta_host[:, 2] = torch.tensor(tss, dtype=torch.float64)
+            self.meta.copy_(self.meta_host, non_blocking=True)
             send = packed if self.ctx.backend == "nccl" else packed.cpu()
             dst = list(self.gather_buf.unbind(0)) if self.ctx.is_root else None
             dist.gather(send, dst, dst=0)
+            mdst = list(self.meta_buf.unbind(0)) if self.ctx.is_root else None
+            dist.gather(self.meta, mdst, dst=0)
             src = self.gather_buf if self.ctx.is_root else None
         else:
             src = packed.unsqueeze(0)
-        self.frames_done += self.B * self.ctx.world
+        self.frames_done += B * self.ctx.world
         if not self.ctx.is_root:
             return np.zeros(0, RECORD_DTYPE)
         self.host_rec.copy_(src, non_blocking=True)
+        if self.ctx.initialized:
+            meta = self.meta_buf.cpu().numpy().reshape(-1, 3)
+        else:
+            meta = np.stack([np.asarray(fids, np.float64), np.asarray(strm, np.float64),
+                             np.asarray(tss, np.float64)], 1)
         if self.cuda:
             torch.cuda.current_stream(self.dev).synchronize()
         flat = self.host_rec.numpy().reshape(-1, self.rec_width)
-        n = flat.shape[0]
-        fids = frame_ids if frame_ids is not None else list(range(self.frames_done - n, self.frames_done))
-        tss = ts if ts is not None else [0.0] * n
-        # stream id: rank * S + (frame index within rank) % S
-        strm = [(i // self.B) * self.S + (i % self.B) % self.S for i in range(n)]
-        recs = unpack_records(flat, self.K, fids, tss, strm)
+        recs = unpack_records(flat, self.K, meta[:, 0].astype(np.int64), meta[:, 2],
+                              meta[:, 1].astype(np.int64))
         self.records_out += len(recs)
         if self.hub is not None:
             self.hub.push_records(recs)

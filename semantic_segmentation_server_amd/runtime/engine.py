@@ -130,8 +130,27 @@ class Engine:
 
     def _step_device(self, frames: torch.Tensor):
         labels = self._infer_eager(frames)
-        post = self._device_post(labels) if self._use_device_post() else None
-        return labels, post
+        if self._use_device_post():
+            return labels, self._device_post(labels)
+        if not self.is_cuda and self.cfg.contour_mode != "none":
+            return labels, self._host_packed(labels)
+        return labels, None
+
+    def _host_packed(self, labels: torch.Tensor) -> torch.Tensor:
+        """CPU path: host post-processing packed like the device output
+        ([B, 1 + 5K] float32: count, then (label, score, area, cx, cy) per record),
+        so the data-parallel gather is identical on CPU (gloo) and GPU (RCCL)."""
+        K = self.cfg.max_segments
+        B = labels.shape[0]
+        recs = self.records_from_labels(labels, [0] * B, [0.0] * B, list(range(B)))
+        out = torch.zeros((B, 1 + 5 * K), dtype=torch.float32)
+        for b in range(B):
+            r = recs[recs["stream"] == b][:K]
+            out[b, 0] = len(r)
+            if len(r):
+                vals = np.stack([r["label"].astype(np.float32), r["score"], r["area"], r["cx"], r["cy"]], 1)
+                out[b, 1:1 + 5 * len(r)] = torch.from_numpy(vals.reshape(-1))
+        return out
 
     def _capture(self, B: int) -> None:
         Hc, Wc = self.cam[1], self.cam[0]

@@ -103,3 +103,44 @@ def test_unpack_records_order():
     packed[1, 0] = 0
     r = unpack_records(packed, K, [5, 6], [1.0, 2.0], [0, 1])
     assert r["label"].tolist() == [7, 15] and r["frame"].tolist() == [5, 5]
+
+
+def _serve_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import grpc
+    from semantic_segmentation_server_amd import config as C
+    from semantic_segmentation_server_amd.api import proto as P
+    from semantic_segmentation_server_amd.api.service import SemanticSegmentationStub, SemanticSegmentationV2Stub
+    from semantic_segmentation_server_amd.parallel import dist as D
+    from semantic_segmentation_server_amd.parallel.serving import DistributedServer
+    ctx = D.init("gloo")
+    cfg = C.parse(["--port", "0", "--host", "127.0.0.1", "--device", "cpu", "--input_size", "65",
+                   "--batch", "2", "--streams", "2", "--gpus", str(world)])
+    srv = DistributedServer(cfg, ctx, max_steps=3)
+    srv.run()
+    D.barrier(ctx)
+    if ctx.is_root:
+        with grpc.insecure_channel(f"127.0.0.1:{srv.port}") as ch:
+            d = SemanticSegmentationStub(ch).GetSegmentedObjects(P.Empty())
+            v2 = SemanticSegmentationV2Stub(ch)
+            ls = v2.ListStreams(P.Empty())
+            h = v2.Health(P.Empty())
+        q.put((len(d.data), [s.stream_id for s in ls.streams], h.world_size, srv.steps,
+               srv.metrics.snapshot()["frames"]))
+    srv.stop()
+    D.destroy(ctx)
+
+
+def test_distributed_server_cpu():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_serve_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    n, streams, world, steps, frames = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert n == 3 and streams == [0, 1, 2, 3] and world == 2 and steps == 3 and frames == 12

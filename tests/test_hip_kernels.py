@@ -286,3 +286,44 @@ def test_engine_step_records_flow():
     frames, ids, ts = src.read_batch(2)
     recs = eng.step(frames, ids, ts, 0)
     assert recs.dtype.names[0] == "label"
+
+
+@pytest.mark.parametrize("cin,cout,t,stride,H", [
+    (32, 16, 1, 1, 37),    # block 0: no expansion
+    (16, 24, 6, 2, 41),    # block 1: stride 2
+    (24, 24, 6, 1, 33),    # block 2: residual
+    (24, 32, 6, 2, 29),
+    (32, 64, 6, 2, 21),
+    (64, 64, 6, 1, 19),    # 33x33-stage shapes, CinP 64
+    (64, 96, 6, 1, 17),
+])
+def test_fused_inverted_residual(cin, cout, t, stride, H):
+    from semantic_segmentation_server_amd.models.layers import init_random
+    from semantic_segmentation_server_amd.models.mobilenetv2 import InvertedResidual, IRSpec
+    K = _hip()
+    spec = IRSpec(cin, cout, t, stride, 1)
+    blk = InvertedResidual(spec)
+    init_random(blk, seed=cin + cout)
+    for m in blk.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.uniform_(-0.2, 0.2)
+            m.running_var.uniform_(0.5, 2.0)
+    blk.eval()
+    g = torch.Generator().manual_seed(9)
+    B, W = 2, H + 6
+    x = torch.randn(B, cin, H, W, generator=g).to(torch.bfloat16)
+    with torch.no_grad():
+        ref = blk(x.float())
+    OH, OW = ref.shape[-2:]
+    ew = eb = None
+    if blk.expand is not None:
+        ew, eb = blk.expand.fold()
+        ew = ew[:, :, 0, 0]
+    dwf, dbf = blk.dw.fold()
+    pwf, pbf = blk.project.fold()
+    packed = K.pack_fused_ir(ew, eb, dwf[:, 0], dbf, pwf[:, :, 0, 0], pbf, Cin=cin, hid=spec.hidden,
+                             Cout=cout, stride=stride, residual=spec.residual, device=DEV)
+    out = torch.empty(B, OH, OW, cout, dtype=torch.bfloat16, device=DEV)
+    K.fused_ir(_nhwc(x).to(DEV), packed, out, B=B, IH=H, IW=W, OH=OH, OW=OW)
+    torch.cuda.synchronize()
+    assert _rel(_nchw(out).cpu(), ref) < 2e-2
