@@ -50,6 +50,19 @@ PYBIND11_MODULE(_hip, m) {
           fused_inverted_residual(p, S(stream));
         });
 
+  m.def("dw_project",
+        [](uintptr_t hid_in, uintptr_t wd, uintptr_t bd, uintptr_t wp, uintptr_t bp, uintptr_t res,
+           uintptr_t out, int B, int IH, int IW, int hid, int Cout, int OH, int OW, int stride,
+           int dil, uintptr_t stream) {
+          DwProjectParams p;
+          p.hid_in = P<const bf16>(hid_in); p.wd = P<const float>(wd); p.bd = P<const float>(bd);
+          p.wp = P<const bf16>(wp); p.bp = P<const float>(bp); p.res = P<const bf16>(res);
+          p.out = P<bf16>(out);
+          p.B = B; p.IH = IH; p.IW = IW; p.hid = hid; p.Cout = Cout; p.OH = OH; p.OW = OW;
+          p.stride = stride; p.dil = dil;
+          dw_project(p, S(stream));
+        });
+
   m.def("depthwise3x3",
         [](uintptr_t in, uintptr_t w, uintptr_t bias, uintptr_t out, int B, int IH, int IW, int C,
            int OH, int OW, int stride, int dil, int act, uintptr_t stream) {
@@ -71,8 +84,10 @@ PYBIND11_MODULE(_hip, m) {
     maxpool3x3s2(P<const bf16>(in), P<bf16>(out), B, IH, IW, C, OH, OW, S(stream));
   });
 
-  m.def("global_avgpool", [](uintptr_t in, uintptr_t out, int B, int HW, int C, uintptr_t stream) {
-    global_avgpool(P<const bf16>(in), P<float>(out), B, HW, C, S(stream));
+  m.def("gap_workspace_floats", &gap_workspace_floats);
+  m.def("global_avgpool", [](uintptr_t in, uintptr_t out, uintptr_t ws, int B, int HW, int C,
+                             uintptr_t stream) {
+    global_avgpool(P<const bf16>(in), P<float>(out), P<float>(ws), B, HW, C, S(stream));
   });
 
   m.def("matvec", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t out, int B, int N, int K,

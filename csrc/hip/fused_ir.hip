@@ -255,4 +255,125 @@ void fused_inverted_residual(const FusedIRParams& p, hipStream_t st) {
 #undef IR_CASE
 }
 
+namespace {
+
+// ---------------------------------------------------------------------------
+// Depthwise + projection fusion for the low-resolution, wide blocks (33x33 maps,
+// hid 384..960, dilation 1/2) where full fusion would recompute the expansion
+// over large halos: the expanded tensor comes from the MFMA GEMM as usual, but the
+// depthwise result never leaves registers — each lane's 8 depthwise channels of
+// one pixel are its B fragment for the projection MFMA.
+// Workgroup: 64 consecutive output pixels (4 waves x 16) x one slice of NSUB*16
+// output channels (blockIdx.y); K loop over the hidden channels in 32-chunks.
+struct DPArgs {
+  const bf16* hid_in;  // [B, IH, IW, hid] expanded activations
+  const float* wd;     // [9, hid]
+  const float* bd;     // [hid]
+  const bf16* wp;      // [CoutP, hid]
+  const float* bp;     // [CoutP]
+  const bf16* res;     // optional [B, OH, OW, Cout]
+  bf16* out;           // [B, OH, OW, Cout]
+  int B, IH, IW, hid, Cout, OH, OW, stride, dil;
+};
+
+template <int NSUB>
+__global__ __launch_bounds__(256) void dw_project_kernel(DPArgs a) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+  const int M = a.B * a.OH * a.OW;
+  const int m = blockIdx.x * 64 + wid * 16 + r16;
+  const bool valid = m < M;
+  const int mm = valid ? m : 0;
+  const int b = mm / (a.OH * a.OW);
+  const int rem = mm - b * a.OH * a.OW;
+  const int oy = rem / a.OW, ox = rem % a.OW;
+  const int n0 = blockIdx.y * NSUB * 16;
+  long long off[9];
+  bool ok[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int iy = oy * a.stride + (t / 3 - 1) * a.dil, ix = ox * a.stride + (t % 3 - 1) * a.dil;
+    ok[t] = valid && iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW;
+    off[t] = (((long long)b * a.IH + iy) * a.IW + ix) * a.hid;
+  }
+  f32x4 acc[NSUB];
+#pragma unroll
+  for (int n = 0; n < NSUB; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < a.hid; c0 += 32) {
+    const int c = c0 + kq * 8;
+    bf16x8 v[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) v[t] = ok[t] ? ld8(a.hid_in + off[t] + c) : zero8();
+    const float4 b0 = *reinterpret_cast<const float4*>(a.bd + c);
+    const float4 b1 = *reinterpret_cast<const float4*>(a.bd + c + 4);
+    float d[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const float4 w0 = *reinterpret_cast<const float4*>(a.wd + t * a.hid + c);
+      const float4 w1 = *reinterpret_cast<const float4*>(a.wd + t * a.hid + c + 4);
+      d[0] += (float)v[t][0] * w0.x; d[1] += (float)v[t][1] * w0.y;
+      d[2] += (float)v[t][2] * w0.z; d[3] += (float)v[t][3] * w0.w;
+      d[4] += (float)v[t][4] * w1.x; d[5] += (float)v[t][5] * w1.y;
+      d[6] += (float)v[t][6] * w1.z; d[7] += (float)v[t][7] * w1.w;
+    }
+    bf16x8 df;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) df[q] = (bf16)fminf(fmaxf(d[q], 0.f), 6.f);
+#pragma unroll
+    for (int n = 0; n < NSUB; ++n) {
+      const bf16x8 af = ld8(a.wp + (size_t)(n0 + n * 16 + r16) * a.hid + c);
+      acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, df, acc[n], 0, 0, 0);
+    }
+  }
+  if (!valid) return;
+  bf16* op = a.out + (long long)mm * a.Cout;
+#pragma unroll
+  for (int n = 0; n < NSUB; ++n) {
+    const int co = n0 + n * 16 + kq * 4;
+    if (co >= a.Cout) continue;
+    float vv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      vv[q] = acc[n][q] + a.bp[co + q];
+      if (a.res && co + q < a.Cout) vv[q] += (float)a.res[(long long)mm * a.Cout + co + q];
+    }
+    if (co + 3 < a.Cout && (a.Cout & 3) == 0) {
+      bf16x4 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = (bf16)vv[q];
+      *reinterpret_cast<bf16x4*>(op + co) = o;
+    } else {
+      for (int q = 0; q < 4; ++q)
+        if (co + q < a.Cout) op[co + q] = (bf16)vv[q];
+    }
+  }
+}
+
+}  // namespace (dw_project)
+
+void dw_project(const DwProjectParams& p, hipStream_t st) {
+  if (p.hid % 32) throw std::invalid_argument("dw_project: hid must be a multiple of 32");
+  DPArgs a{p.hid_in, p.wd, p.bd, p.wp, p.bp, p.res, p.out, p.B, p.IH, p.IW, p.hid, p.Cout,
+           p.OH, p.OW, p.stride, p.dil};
+  const int M = p.B * p.OH * p.OW;
+  const int nsub_total = (p.Cout + 15) / 16;
+  // channel slices of up to 5 subtiles (80 channels): more workgroups, fewer VGPRs
+  int nsub = nsub_total;
+  for (int cand : {5, 4, 3, 2, 1})
+    if (nsub_total % cand == 0 && nsub_total / cand <= 4) { nsub = cand; break; }
+  if (nsub_total <= 6) nsub = nsub_total;
+  const dim3 grid(cdiv(M, 64), nsub_total / nsub);
+#define DP_CASE(N) \
+  case N: hipLaunchKernelGGL(dw_project_kernel<N>, grid, dim3(256), 0, st, a); break;
+  switch (nsub) {
+    DP_CASE(1) DP_CASE(2) DP_CASE(3) DP_CASE(4) DP_CASE(5) DP_CASE(6)
+    default: throw std::invalid_argument("dw_project: unsupported Cout");
+  }
+#undef DP_CASE
+  check_launch("dw_project");
+}
+
+namespace {  // reopen for nothing (keeps the file's namespace structure simple)
+}  // namespace
+
 }  // namespace ssa

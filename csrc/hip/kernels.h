@@ -40,6 +40,21 @@ struct FusedIRParams {
 };
 void fused_inverted_residual(const FusedIRParams& p, hipStream_t s);
 
+// Depthwise 3x3 (+bias, ReLU6) fused with the 1x1 projection (+bias [+ residual]):
+// the depthwise output stays in registers as the projection's MFMA operand.
+// Weights: wd [9, hid] fp32, wp [CoutP, hid] bf16 (CoutP = 16 * ceil(Cout / 16)).
+struct DwProjectParams {
+  const bf16* hid_in = nullptr;  // [B, IH, IW, hid]
+  const float* wd = nullptr;
+  const float* bd = nullptr;
+  const bf16* wp = nullptr;
+  const float* bp = nullptr;
+  const bf16* res = nullptr;     // optional [B, OH, OW, Cout]
+  bf16* out = nullptr;           // [B, OH, OW, Cout]
+  int B = 0, IH = 0, IW = 0, hid = 0, Cout = 0, OH = 0, OW = 0, stride = 1, dil = 1;
+};
+void dw_project(const DwProjectParams& p, hipStream_t s);
+
 // Depthwise KxK (K=3) conv, NHWC, pad = dil, bias + act. w: [9, C] fp32.
 void depthwise3x3(const bf16* in, const float* w, const float* bias, bf16* out, int B, int IH,
                   int IW, int C, int OH, int OW, int stride, int dil, int act, hipStream_t s);
@@ -56,8 +71,10 @@ void stem_conv(const uint8_t* frames, const int32_t* lut_x, const int32_t* lut_y
 void maxpool3x3s2(const bf16* in, bf16* out, int B, int IH, int IW, int C, int OH, int OW,
                   hipStream_t s);
 
-// Global average pool NHWC bf16 [B, H, W, C] -> fp32 [B, C].
-void global_avgpool(const bf16* in, float* out, int B, int HW, int C, hipStream_t s);
+// Global average pool NHWC bf16 [B, H, W, C] -> fp32 [B, C]; ws: fp32 workspace of
+// gap_workspace_floats(B, C) elements (pixel-slice partial sums).
+size_t gap_workspace_floats(int B, int C);
+void global_avgpool(const bf16* in, float* out, float* ws, int B, int HW, int C, hipStream_t s);
 
 // out[b, n] = act(sum_k W[n, k] * x[b, k] + bias[n]), fp32 everywhere (tiny).
 void matvec(const float* x, const float* w, const float* bias, float* out, int B, int N, int K,

@@ -192,38 +192,58 @@ void maxpool3x3s2(const bf16* in, bf16* out, int B, int IH, int IW, int C, int O
 }
 
 // ---------------------------------------------------------------- GAP
-// grid (B, C/8/64 blocks): each lane owns 8 channels and strides over pixels;
-// the 4 waves of a block split the pixels and reduce through LDS.
-__global__ __launch_bounds__(256) void gap_kernel(const bf16* __restrict__ in,
-                                                  float* __restrict__ out, int HW, int C) {
-  const int b = blockIdx.x;
+// Two passes so the reduction fills the chip: grid (B, S slices of the pixels,
+// channel blocks); each lane owns 8 channels, the 4 waves of a block split the
+// slice's pixels and reduce through LDS into part[b][slice][C]; a tiny second
+// kernel sums the slices (deterministic, no float atomics).
+constexpr int kGapSlices = 16;
+
+__global__ __launch_bounds__(256) void gap_partial_kernel(const bf16* __restrict__ in,
+                                                          float* __restrict__ part, int HW, int C) {
+  const int b = blockIdx.x, sl = blockIdx.y;
   const int CG = C >> 3;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int cg = blockIdx.y * 64 + lane;
-  __shared__ float part[4][64][8];
+  const int cg = blockIdx.z * 64 + lane;
+  __shared__ float red[4][64][8];
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int p0 = (int)((long long)HW * sl / kGapSlices), p1 = (int)((long long)HW * (sl + 1) / kGapSlices);
   if (cg < CG) {
     const bf16* base = in + (long long)b * HW * C + cg * 8;
-    for (int p = wid; p < HW; p += 4) {
+    for (int p = p0 + wid; p < p1; p += 4) {
       const bf16x8 v = ld8(base + (long long)p * C);
 #pragma unroll
       for (int q = 0; q < 8; ++q) acc[q] += (float)v[q];
     }
   }
 #pragma unroll
-  for (int q = 0; q < 8; ++q) part[wid][lane][q] = acc[q];
+  for (int q = 0; q < 8; ++q) red[wid][lane][q] = acc[q];
   __syncthreads();
   if (wid == 0 && cg < CG) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const float s = part[0][lane][q] + part[1][lane][q] + part[2][lane][q] + part[3][lane][q];
-      out[(long long)b * C + cg * 8 + q] = s / (float)HW;
-    }
+    for (int q = 0; q < 8; ++q)
+      part[((long long)b * kGapSlices + sl) * C + cg * 8 + q] =
+          red[0][lane][q] + red[1][lane][q] + red[2][lane][q] + red[3][lane][q];
   }
 }
 
-void global_avgpool(const bf16* in, float* out, int B, int HW, int C, hipStream_t s) {
-  hipLaunchKernelGGL(gap_kernel, dim3(B, cdiv(C / 8, 64)), dim3(256), 0, s, in, out, HW, C);
+__global__ void gap_reduce_kernel(const float* __restrict__ part, float* __restrict__ out, int B,
+                                  int HW, int C) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * C) return;
+  const int b = i / C, c = i % C;
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < kGapSlices; ++k) s += part[((long long)b * kGapSlices + k) * C + c];
+  out[i] = s / (float)HW;
+}
+
+size_t gap_workspace_floats(int B, int C) { return (size_t)B * kGapSlices * C; }
+
+void global_avgpool(const bf16* in, float* out, float* ws, int B, int HW, int C, hipStream_t s) {
+  hipLaunchKernelGGL(gap_partial_kernel, dim3(B, kGapSlices, cdiv(C / 8, 64)), dim3(256), 0, s, in,
+                     ws, HW, C);
+  hipLaunchKernelGGL(gap_reduce_kernel, dim3(cdiv((long long)B * C, 256)), dim3(256), 0, s, ws, out,
+                     B, HW, C);
   check_launch("global_avgpool");
 }
 

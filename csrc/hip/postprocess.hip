@@ -260,12 +260,20 @@ __global__ __launch_bounds__(256) void k_ccl_boundary(KArgs a) {
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
   const uint8_t m = f.mask[p];
   const int me = p + 1;
+  // Skip unions already implied by the previous pixel along the same tile edge:
+  // if it has the same class, the same tile-local root and its partner across the
+  // edge has the same local root as ours, it issued the identical union. (Local
+  // roots are still in L: tile-local writes are the only writes before this pass
+  // apart from root links, which keep equal roots equal.)
+  auto lroot = [&](int q) { return f.L[q + 1]; };
   if (m) {
     if (left && f.mask[p - 1]) unite(f.L, me, me - 1);
     if (y > 0) {
       const int up = p - a.cw;
       if (top) {
-        if (f.mask[up]) unite(f.L, me, up + 1);
+        const bool dup = x > 0 && (x % TW) != 0 && f.mask[p - 1] && lroot(p - 1) == lroot(p);
+        if (f.mask[up] && !(dup && f.mask[up - 1] && lroot(up - 1) == lroot(up)))
+          unite(f.L, me, up + 1);
         if (x > 0 && f.mask[up - 1]) unite(f.L, me, up);
         if (x + 1 < a.cw && f.mask[up + 1]) unite(f.L, me, up + 2);
       } else {
@@ -275,9 +283,22 @@ __global__ __launch_bounds__(256) void k_ccl_boundary(KArgs a) {
       }
     }
   } else {
-    if (left && !f.mask[p - 1]) unite(f.L, me, me - 1);
-    if (top && !f.mask[p - a.cw]) unite(f.L, me, me - a.cw);
-    if (edge) unite(f.L, me, 0);
+    if (left && !f.mask[p - 1]) {
+      const bool dup = y > 0 && (y % TH) != 0 && !f.mask[p - a.cw] && !f.mask[p - a.cw - 1] &&
+                       lroot(p - a.cw) == lroot(p) && lroot(p - a.cw - 1) == lroot(p - 1);
+      if (!dup) unite(f.L, me, me - 1);
+    }
+    if (top && !f.mask[p - a.cw]) {
+      const bool dup = x > 0 && (x % TW) != 0 && !f.mask[p - 1] && !f.mask[p - a.cw - 1] &&
+                       lroot(p - 1) == lroot(p) && lroot(p - a.cw - 1) == lroot(p - a.cw);
+      if (!dup) unite(f.L, me, me - a.cw);
+    }
+    if (edge) {
+      // one union per run of border pixels sharing a tile-local root
+      const int prev = (y == 0 || y == a.ch - 1) ? (x > 0 && (x % TW) != 0 ? p - 1 : -1)
+                                                 : ((y % TH) != 0 ? p - a.cw : -1);
+      if (prev < 0 || f.mask[prev] || lroot(prev) != lroot(p)) unite(f.L, me, 0);
+    }
   }
 }
 

@@ -124,6 +124,9 @@ class HipDeepLab:
                     d["fused"] = K.pack_fused_ir(
                         ew, eb, dwf[:, 0], dbf, pwf[:, :, 0, 0], pbf, Cin=s.cin, hid=s.hidden,
                         Cout=s.cout, stride=s.stride, residual=s.residual, device=dev)
+                elif s.hidden % 32 == 0 and blk.expand is not None:
+                    pwf, pbf = blk.project.fold()
+                    d["dwproj"] = K.pack_project_padded(pwf[:, :, 0, 0], pbf, s.cout, s.hidden, dev)
                 self.blocks.append(d)
         else:
             for blk in bb.blocks:
@@ -205,7 +208,10 @@ class HipDeepLab:
             gap = buf("gap", B, c, dtype=torch.float32)
             pooled = buf("pooled", B, A, dtype=torch.float32)
             img_bias = buf("img_bias", B, A, dtype=torch.float32)
-            ops.append(lambda *_, x=x, h=h, w=w, c=c: K.global_avgpool(x, gap, B=B, HW=h * w, C=c))
+            gws = K.gap_workspace(B, c, dev)
+            bufs["gap_ws"] = gws
+            ops.append(lambda *_, x=x, h=h, w=w, c=c: K.global_avgpool(x, gap, B=B, HW=h * w, C=c,
+                                                                       ws=gws))
             ops.append(lambda *_, c=c: K.matvec(gap, self.pool_w, self.pool_b, pooled, B=B, N=A,
                                                 K=c, act="relu"))
             ops.append(lambda *_: K.matvec(pooled, self.proj_pool_w, None, img_bias, B=B, N=A, K=A))
@@ -238,6 +244,13 @@ class HipDeepLab:
                 op.autotune((frames, lx, ly))
         torch.cuda.synchronize(dev)
         self.choices = {op.name: op.variants[op.pick][0] for op in ops if isinstance(op, Choice)}
+        if os.environ.get("SSA_LOG_AUTOTUNE", "0") == "1":
+            import sys
+            for op in ops:
+                if isinstance(op, Choice) and hasattr(op, "times"):
+                    print(f"[autotune B={B}] {op.name}: " + ", ".join(
+                        f"{n}={t * 1e3:.1f}us" for (n, _), t in zip(op.variants, op.times)) +
+                        f" -> {op.variants[op.pick][0]}", file=sys.stderr)
 
     def _mnv2_block(self, ops, buf, i, blk, x, B, h, w, c):
         s = blk["spec"]
@@ -251,6 +264,7 @@ class HipDeepLab:
             ops.append(lambda *_, x=x, e=e, h=h, w=w, c=c: K.conv_gemm(
                 x, ew, eb, e, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w, Cout=hid, k=1, act="relu6"))
             x = e
+        unfused_expand_out = x
         OH, OW = conv_out_hw(h, w, 3, s.stride, s.dilation)
         dw_w, dw_b = blk["dw"]
         d = buf(f"b{i}_dw", B, OH, OW, hid)
@@ -264,6 +278,13 @@ class HipDeepLab:
             d, pw_, pb_, out, B=B, IH=OH, IW=OW, Cin=hid, OH=OH, OW=OW, Cout=s.cout, k=1,
             act=None, res=res))
         variants = [("unfused", unfused)]
+        if "dwproj" in blk:
+            dpw, dpb = blk["dwproj"]
+            e = unfused_expand_out
+            variants.append(("dwproj", [unfused[0], lambda *_, e=e, out=out, h=h, w=w, OH=OH, OW=OW,
+                                        res=res: K.dw_project(
+                e, dw_w, dw_b, dpw, dpb, out, B=B, IH=h, IW=w, hid=hid, Cout=s.cout, OH=OH, OW=OW,
+                stride=s.stride, dil=s.dilation, res=res)]))
         if "fused" in blk:
             fp = blk["fused"]
             variants.insert(0, ("fused", [lambda *_, x=inp, out=out, h=h, w=w, OH=OH, OW=OW:

@@ -104,6 +104,36 @@ def fused_ir(x, packed: dict, out, *, B, IH, IW, OH, OW):
     return out
 
 
+def dw_project(hid_in, wd, bd, wp, bp, out, *, B, IH, IW, hid, Cout, OH, OW, stride=1, dil=1,
+               res=None):
+    """Depthwise 3x3 + ReLU6 fused with the 1x1 projection. wp: [CoutP, hid] bf16."""
+    CoutP = (Cout + 15) // 16 * 16
+    if hid % 32:
+        raise ValueError("dw_project: hid must be a multiple of 32")
+    _chk(hid_in, torch.bfloat16, "hid_in", B * IH * IW * hid)
+    _chk(wd, torch.float32, "wd", 9 * hid)
+    _chk(bd, torch.float32, "bd", hid)
+    _chk(wp, torch.bfloat16, "wp", CoutP * hid)
+    _chk(bp, torch.float32, "bp", CoutP)
+    _chk(out, torch.bfloat16, "out", B * OH * OW * Cout)
+    if res is not None:
+        _chk(res, torch.bfloat16, "res", B * OH * OW * Cout)
+    _hip_mod().dw_project(_ptr(hid_in), _ptr(wd), _ptr(bd), _ptr(wp), _ptr(bp), _ptr(res), _ptr(out),
+                          B, IH, IW, hid, Cout, OH, OW, stride, dil, _stream())
+    _dbg('dw_project')
+    return out
+
+
+def pack_project_padded(wp, bp, Cout, hid, device):
+    """Projection weights [Cout, hid] -> zero-padded [CoutP, hid] bf16 + [CoutP] fp32."""
+    CoutP = (Cout + 15) // 16 * 16
+    w = torch.zeros(CoutP, hid, dtype=torch.float32, device=device)
+    w[:Cout] = wp
+    b = torch.zeros(CoutP, dtype=torch.float32, device=device)
+    b[:Cout] = bp
+    return w.to(torch.bfloat16).contiguous(), b
+
+
 def pack_fused_ir(we, be, wd, bd, wp, bp, *, Cin, hid, Cout, stride, residual, device) -> dict:
     """Zero-pad folded block weights to the fused kernel's layout.
 
@@ -178,10 +208,17 @@ def maxpool3x3s2(x, out, *, B, IH, IW, C, OH, OW):
     return out
 
 
-def global_avgpool(x, out, *, B, HW, C):
+def gap_workspace(B, C, device) -> torch.Tensor:
+    return torch.empty(int(_hip_mod().gap_workspace_floats(B, C)), dtype=torch.float32, device=device)
+
+
+def global_avgpool(x, out, *, B, HW, C, ws=None):
     _chk(x, torch.bfloat16, "x", B * HW * C)
     _chk(out, torch.float32, "out", B * C)
-    _hip_mod().global_avgpool(_ptr(x), _ptr(out), B, HW, C, _stream())
+    if ws is None:
+        ws = gap_workspace(B, C, x.device)
+    _chk(ws, torch.float32, "ws", int(_hip_mod().gap_workspace_floats(B, C)))
+    _hip_mod().global_avgpool(_ptr(x), _ptr(out), _ptr(ws), B, HW, C, _stream())
     _dbg('global_avgpool')
     return out
 

@@ -327,3 +327,30 @@ def test_fused_inverted_residual(cin, cout, t, stride, H):
     K.fused_ir(_nhwc(x).to(DEV), packed, out, B=B, IH=H, IW=W, OH=OH, OW=OW)
     torch.cuda.synchronize()
     assert _rel(_nchw(out).cpu(), ref) < 2e-2
+
+
+@pytest.mark.parametrize("hid,cout,stride,dil,res", [(576, 96, 1, 1, True), (576, 160, 1, 1, False),
+                                                     (960, 160, 1, 2, True), (960, 320, 1, 2, False),
+                                                     (384, 64, 2, 1, False)])
+def test_dw_project(hid, cout, stride, dil, res):
+    K = _hip()
+    g = torch.Generator().manual_seed(10)
+    B, H = 2, 21
+    x = F.relu6(torch.randn(B, hid, H, H, generator=g) * 2).to(torch.bfloat16)
+    wd = torch.randn(hid, 1, 3, 3, generator=g) / 3
+    bd = torch.randn(hid, generator=g) * 0.1
+    wp = torch.randn(cout, hid, generator=g) / hid ** 0.5
+    bp = torch.randn(cout, generator=g) * 0.1
+    d = F.relu6(F.conv2d(x.float(), wd, bd, stride, dil, dil, groups=hid)).to(torch.bfloat16).float()
+    ref = F.conv2d(d, wp.to(torch.bfloat16).float()[:, :, None, None], bp)
+    OH, OW = ref.shape[-2:]
+    r = torch.randn(B, cout, OH, OW, generator=g).to(torch.bfloat16) if res else None
+    if res:
+        ref = ref + r.float()
+    wpp, bpp = K.pack_project_padded(wp, bp, cout, hid, DEV)
+    out = torch.empty(B, OH, OW, cout, dtype=torch.bfloat16, device=DEV)
+    K.dw_project(_nhwc(x).to(DEV), wd.reshape(hid, 9).t().contiguous().to(DEV), bd.to(DEV), wpp, bpp,
+                 out, B=B, IH=H, IW=H, hid=hid, Cout=cout, OH=OH, OW=OW, stride=stride, dil=dil,
+                 res=None if r is None else _nhwc(r).to(DEV))
+    torch.cuda.synchronize()
+    assert _rel(_nchw(out).cpu(), ref) < 1e-2
