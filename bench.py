@@ -56,6 +56,8 @@ def main() -> int:
     p.add_argument("--no-graph", dest="graph", action="store_false")
     p.add_argument("--rpc", type=int, default=2000, help="GetSegmentedObjects calls to time (0: skip)")
     p.add_argument("--dtype", default="bf16")
+    p.add_argument("--streams", type=int, default=1,
+                   help="concurrent camera streams per GPU, each with its own HIP stream + hipGraph")
     a = p.parse_args()
 
     import numpy as np
@@ -74,9 +76,13 @@ def main() -> int:
                    ingest=a.ingest, camera_width=cam_w, camera_height=cam_h,
                    num_classes=21 if a.arch == "mnv2" else 19,
                    dataset="pascal" if a.arch == "mnv2" else "cityscapes")
-    engine = Engine(cfg, ctx.device)
-    hub = ResultHub(ctx.world, maxlen=4096) if ctx.is_root else None
-    pipe = DataParallelPipeline(ctx, engine, cam_w, cam_h, a.batch, a.ingest, hub)
+    if a.streams > 1:
+        from semantic_segmentation_server_amd.runtime.multistream import StreamGroup
+        engine = StreamGroup(cfg, ctx.device, a.streams)
+    else:
+        engine = Engine(cfg, ctx.device)
+    hub = ResultHub(ctx.world * a.streams, maxlen=4096) if ctx.is_root else None
+    pipe = DataParallelPipeline(ctx, engine, cam_w, cam_h, a.batch, a.ingest, hub, a.streams)
 
     # synthetic camera frames, pinned; distinct per rank
     src = SyntheticSource(cam_w, cam_h, stream=ctx.rank, seed=1, pool=max(2, min(a.batch, 8)))
@@ -132,7 +138,7 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": a.dtype,
-            "data": "synthetic 640x480 BGR frames, random-init weights",
+            "data": f"synthetic {a.camera} BGR frames, random-init weights",
             "config": {
                 "model": "DeepLabv3-MobileNetV2" if a.arch == "mnv2" else "DeepLabv3-ResNet50",
                 "aspp": a.aspp,
@@ -147,6 +153,7 @@ def main() -> int:
                 "backend": a.backend,
                 "hipgraph": bool(a.graph and ctx.device.type == "cuda"),
                 "contour_mode": a.contour_mode,
+                "streams_per_gpu": a.streams,
             },
             "p50_get_segmented_objects_ms": rpc.get("p50_ms") if rpc else None,
             "p99_get_segmented_objects_ms": rpc.get("p99_ms") if rpc else None,

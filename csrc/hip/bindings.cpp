@@ -73,11 +73,39 @@ PYBIND11_MODULE(_hip, m) {
   m.def("stem_conv",
         [](uintptr_t frames, uintptr_t lut_x, uintptr_t lut_y, uintptr_t w, uintptr_t bias,
            uintptr_t out, int B, int Hc, int Wc, int H, int W, int OH, int OW, int Cout, int K,
-           int stride, int act, uintptr_t stream) {
+           int stride, int act, uintptr_t stream, float out_inv_scale) {
           stem_conv(P<const uint8_t>(frames), P<const int32_t>(lut_x), P<const int32_t>(lut_y),
-                    P<const float>(w), P<const float>(bias), P<bf16>(out), B, Hc, Wc, H, W, OH, OW,
-                    Cout, K, stride, act, S(stream));
+                    P<const float>(w), P<const float>(bias), P<void>(out), B, Hc, Wc, H, W, OH, OW,
+                    Cout, K, stride, act, S(stream), out_inv_scale);
+        },
+        py::arg("frames"), py::arg("lut_x"), py::arg("lut_y"), py::arg("w"), py::arg("bias"),
+        py::arg("out"), py::arg("B"), py::arg("Hc"), py::arg("Wc"), py::arg("H"), py::arg("W"),
+        py::arg("OH"), py::arg("OW"), py::arg("Cout"), py::arg("K"), py::arg("stride"),
+        py::arg("act"), py::arg("stream"), py::arg("out_inv_scale") = 0.f);
+
+  m.def("conv_i8",
+        [](uintptr_t in, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t img_bias,
+           uintptr_t res, float res_scale, uintptr_t out, float inv_out_scale, int out_mode, int B,
+           int IH, int IW, int Cin, int OH, int OW, int Cout, int KH, int KW, int stride, int dil,
+           int ldo, int co_off, int act, uintptr_t stream) {
+          ConvI8Params p;
+          p.in = P<const int8_t>(in); p.w = P<const int8_t>(w); p.scale = P<const float>(scale);
+          p.bias = P<const float>(bias); p.img_bias = P<const float>(img_bias);
+          p.res = P<const int8_t>(res); p.res_scale = res_scale; p.out = P<void>(out);
+          p.inv_out_scale = inv_out_scale; p.out_mode = out_mode;
+          p.B = B; p.IH = IH; p.IW = IW; p.Cin = Cin; p.OH = OH; p.OW = OW; p.Cout = Cout;
+          p.KH = KH; p.KW = KW; p.stride = stride; p.dil = dil; p.ldo = ldo; p.co_off = co_off;
+          p.act = act;
+          conv_i8(p, S(stream));
         });
+  m.def("maxpool3x3s2_i8", [](uintptr_t in, uintptr_t out, int B, int IH, int IW, int C, int OH,
+                              int OW, uintptr_t stream) {
+    maxpool3x3s2_i8(P<const int8_t>(in), P<int8_t>(out), B, IH, IW, C, OH, OW, S(stream));
+  });
+  m.def("global_avgpool_i8", [](uintptr_t in, uintptr_t out, uintptr_t ws, int B, int HW, int C,
+                                float scale, uintptr_t stream) {
+    global_avgpool_i8(P<const int8_t>(in), P<float>(out), P<float>(ws), B, HW, C, scale, S(stream));
+  });
 
   m.def("maxpool3x3s2", [](uintptr_t in, uintptr_t out, int B, int IH, int IW, int C, int OH,
                            int OW, uintptr_t stream) {

@@ -1,0 +1,229 @@
+// int8 implicit-GEMM convolution on the CDNA4 int8 MFMA (v_mfma_i32_16x16x64_i8),
+// NHWC int8 activations (per-tensor symmetric scale), int8 weights (per output
+// channel), exact int32 accumulation, fused epilogue:
+//
+//   v = acc * scale[n] + bias[n] + img_bias[b][n] + res_i8 * res_scale
+//   v = act(v);  out = out_mode == I8 ? clamp(round(v * inv_out_scale)) : bf16(v)
+//
+// scale[n] = in_scale * w_scale[n] is folded on the host. Used by the int8
+// DeepLabv3-ResNet50 config (bottleneck 1x1/3x3 incl. strided, ASPP branches into
+// a shared-scale concat buffer, projection, and the bf16-output logits layer).
+// Mapping mirrors conv_gemm: A = weights (rows = out channels), B = pixels, so a
+// lane's accumulator holds 4 consecutive output channels of one pixel; each
+// fragment is one 16-byte load of 16 consecutive K elements
+// (lane l: row/col l&15, k = 16*(l>>4) .. +15).
+#include "common.h"
+#include "kernels.h"
+
+namespace ssa {
+namespace {
+
+typedef int i32x4v __attribute__((ext_vector_type(4)));
+
+struct I8Args {
+  const int8_t* in; const int8_t* w; const float* scale; const float* bias;
+  const float* img_bias; const int8_t* res; float res_scale; void* out; float inv_out_scale;
+  int out_mode;  // 0 int8, 1 bf16
+  int B, IH, IW, Cin, OH, OW, Cout, KH, KW, stride, dil, ldo, co_off, act;
+};
+
+__device__ __forceinline__ i32x4v ld16(const int8_t* p) { return *reinterpret_cast<const i32x4v*>(p); }
+
+template <int MT, int NT>
+__global__ __launch_bounds__(256) void conv_i8_kernel(I8Args a) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int M = a.B * a.OH * a.OW;
+  const int tiles_m = cdiv_dev(M, 32 * MT), tiles_n = cdiv_dev(a.Cout, 32 * NT);
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tn = bid % tiles_n, tm = bid / tiles_n;
+  const int pix0 = tm * 32 * MT + wm * 16 * MT;
+  const int ch0 = tn * 32 * NT + wn * 16 * NT;
+  const int r = lane & 15, kq = lane >> 4;
+  int pb[MT], py[MT], px[MT];
+  bool pvalid[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int m = pix0 + i * 16 + r;
+    pvalid[i] = m < M;
+    const int mm = pvalid[i] ? m : 0;
+    pb[i] = mm / (a.OH * a.OW);
+    const int rem = mm - pb[i] * a.OH * a.OW;
+    py[i] = (rem / a.OW) * a.stride;
+    px[i] = (rem % a.OW) * a.stride;
+  }
+  bool wvalid[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) wvalid[j] = (ch0 + j * 16 + r) < a.Cout;
+  i32x4v acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = i32x4v{0, 0, 0, 0};
+  const i32x4v zero = {0, 0, 0, 0};
+  const int taps = a.KH * a.KW;
+  const long long wrow = (long long)taps * a.Cin;
+  for (int t = 0; t < taps; ++t) {
+    const int dy = (t / a.KW - a.KH / 2) * a.dil, dx = (t % a.KW - a.KW / 2) * a.dil;
+    long long off[MT];
+    bool ok[MT];
+    bool any = false;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int iy = py[i] + dy, ix = px[i] + dx;
+      ok[i] = pvalid[i] && iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW;
+      off[i] = (((long long)pb[i] * a.IH + iy) * a.IW + ix) * a.Cin;
+      any |= ok[i];
+    }
+    if (!__any(any)) continue;
+    const int8_t* wt = a.w + (long long)t * a.Cin;
+    for (int c0 = 0; c0 < a.Cin; c0 += 64) {
+      const int c = c0 + kq * 16;
+      const bool cok = c < a.Cin;
+      i32x4v bfr[MT], afr[NT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) bfr[i] = (ok[i] && cok) ? ld16(a.in + off[i] + c) : zero;
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        afr[j] = (wvalid[j] && cok) ? ld16(wt + (long long)(ch0 + j * 16 + r) * wrow + c) : zero;
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[j], bfr[i], acc[i][j], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int m = pix0 + i * 16 + r;
+    if (m >= M) continue;
+    const int b = pb[i];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = ch0 + j * 16 + kq * 4;
+      if (n >= a.Cout) continue;
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (n + q >= a.Cout) { v[q] = 0.f; continue; }
+        v[q] = (float)acc[i][j][q] * a.scale[n + q] + a.bias[n + q];
+        if (a.img_bias) v[q] += a.img_bias[(long long)b * a.Cout + n + q];
+        if (a.res) v[q] += (float)a.res[(long long)m * a.Cout + n + q] * a.res_scale;
+        v[q] = apply_act(v[q], a.act);
+      }
+      const long long o = (long long)m * a.ldo + a.co_off + n;
+      if (a.out_mode == 0) {
+        int8_t* op = static_cast<int8_t*>(a.out) + o;
+        char4 pk;
+        signed char qv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          qv[q] = (signed char)fminf(fmaxf(rintf(v[q] * a.inv_out_scale), -127.f), 127.f);
+        if (n + 3 < a.Cout && ((a.ldo | a.co_off) & 3) == 0) {
+          pk = make_char4(qv[0], qv[1], qv[2], qv[3]);
+          *reinterpret_cast<char4*>(op) = pk;
+        } else {
+          for (int q = 0; q < 4; ++q) if (n + q < a.Cout) op[q] = qv[q];
+        }
+      } else {
+        bf16* op = static_cast<bf16*>(a.out) + o;
+        for (int q = 0; q < 4; ++q) if (n + q < a.Cout) op[q] = (bf16)v[q];
+      }
+    }
+  }
+}
+
+template <int MT, int NT>
+void launch_i8(const I8Args& a, hipStream_t s) {
+  const int M = a.B * a.OH * a.OW;
+  const int grid = cdiv(M, 32 * MT) * cdiv(a.Cout, 32 * NT);
+  hipLaunchKernelGGL((conv_i8_kernel<MT, NT>), dim3(grid), dim3(256), 0, s, a);
+  check_launch("conv_i8");
+}
+
+// ---- int8 helpers: max pool and global average pool on int8 NHWC
+__global__ void maxpool_i8_kernel(const int8_t* __restrict__ in, int8_t* __restrict__ out, int B,
+                                  int IH, int IW, int C, int OH, int OW) {
+  const int CG = C >> 4;
+  const long long total = (long long)B * OH * OW * CG;
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int cg = (int)(t % CG);
+  long long pix = t / CG;
+  const int ox = (int)(pix % OW);
+  pix /= OW;
+  const int oy = (int)(pix % OH);
+  const int b = (int)(pix / OH);
+  signed char m[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) m[q] = -128;
+  for (int ky = 0; ky < 3; ++ky) {
+    const int iy = oy * 2 + ky - 1;
+    if (iy < 0 || iy >= IH) continue;
+    for (int kx = 0; kx < 3; ++kx) {
+      const int ix = ox * 2 + kx - 1;
+      if (ix < 0 || ix >= IW) continue;
+      const int4 v = *reinterpret_cast<const int4*>(in + (((long long)b * IH + iy) * IW + ix) * C + cg * 16);
+      const signed char* pv = reinterpret_cast<const signed char*>(&v);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) m[q] = pv[q] > m[q] ? pv[q] : m[q];
+    }
+  }
+  *reinterpret_cast<int4*>(out + t * 16) = *reinterpret_cast<int4*>(m);
+}
+
+__global__ __launch_bounds__(256) void gap_i8_kernel(const int8_t* __restrict__ in, float* __restrict__ part,
+                                                     int HW, int C, int slices) {
+  const int b = blockIdx.x, sl = blockIdx.y;
+  const int c = blockIdx.z * 256 + threadIdx.x;
+  if (c >= C) return;
+  const int p0 = (int)((long long)HW * sl / slices), p1 = (int)((long long)HW * (sl + 1) / slices);
+  int s = 0;
+  for (int p = p0; p < p1; ++p) s += in[((long long)b * HW + p) * C + c];
+  part[((long long)b * slices + sl) * C + c] = (float)s;
+}
+
+__global__ void gap_i8_reduce(const float* __restrict__ part, float* __restrict__ out, int B, int C,
+                              int slices, float scale) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * C) return;
+  const int b = i / C, c = i % C;
+  float s = 0.f;
+  for (int k = 0; k < slices; ++k) s += part[((long long)b * slices + k) * C + c];
+  out[i] = s * scale;
+}
+
+}  // namespace
+
+void conv_i8(const ConvI8Params& p, hipStream_t s) {
+  if (p.Cin % 16) throw std::invalid_argument("conv_i8: Cin must be a multiple of 16");
+  if (p.ldo < p.co_off + p.Cout) throw std::invalid_argument("conv_i8: bad ldo/co_off");
+  I8Args a{p.in, p.w, p.scale, p.bias, p.img_bias, p.res, p.res_scale, p.out, p.inv_out_scale,
+           p.out_mode, p.B, p.IH, p.IW, p.Cin, p.OH, p.OW, p.Cout, p.KH, p.KW, p.stride, p.dil,
+           p.ldo, p.co_off, p.act};
+  const long long M = (long long)p.B * p.OH * p.OW;
+  if (p.Cout <= 32) launch_i8<4, 1>(a, s);
+  else if (p.Cout <= 64 || M < 8192) launch_i8<2, 2>(a, s);
+  else launch_i8<2, 4>(a, s);
+}
+
+void maxpool3x3s2_i8(const int8_t* in, int8_t* out, int B, int IH, int IW, int C, int OH, int OW,
+                     hipStream_t s) {
+  if (C % 16) throw std::invalid_argument("maxpool_i8: C % 16");
+  const long long total = (long long)B * OH * OW * (C / 16);
+  hipLaunchKernelGGL(maxpool_i8_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, in, out, B, IH, IW,
+                     C, OH, OW);
+  check_launch("maxpool_i8");
+}
+
+void global_avgpool_i8(const int8_t* in, float* out, float* ws, int B, int HW, int C, float scale,
+                       hipStream_t s) {
+  const int slices = 16;
+  hipLaunchKernelGGL(gap_i8_kernel, dim3(B, slices, cdiv(C, 256)), dim3(256), 0, s, in, ws, HW, C,
+                     slices);
+  hipLaunchKernelGGL(gap_i8_reduce, dim3(cdiv((long long)B * C, 256)), dim3(256), 0, s, ws, out, B,
+                     C, slices, scale / (float)HW);
+  check_launch("gap_i8");
+}
+
+}  // namespace ssa

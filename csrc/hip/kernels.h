@@ -23,6 +23,30 @@ struct ConvParams {
 };
 void conv_gemm(const ConvParams& p, hipStream_t s);
 
+// int8 implicit-GEMM conv (int8 MFMA, int32 accumulate). scale[n] = in_scale *
+// w_scale[n]; out_mode 0 -> int8 out (round(v * inv_out_scale), clamp +-127),
+// 1 -> bf16 out. res (optional) is int8 [M, Cout] with res_scale.
+struct ConvI8Params {
+  const int8_t* in = nullptr;   // [B, IH, IW, Cin]
+  const int8_t* w = nullptr;    // [Cout, KH, KW, Cin]
+  const float* scale = nullptr; // [Cout]
+  const float* bias = nullptr;  // [Cout]
+  const float* img_bias = nullptr;
+  const int8_t* res = nullptr;
+  float res_scale = 0.f;
+  void* out = nullptr;
+  float inv_out_scale = 1.f;
+  int out_mode = 0;
+  int B = 0, IH = 0, IW = 0, Cin = 0, OH = 0, OW = 0, Cout = 0;
+  int KH = 1, KW = 1, stride = 1, dil = 1, ldo = 0, co_off = 0, act = 0;
+};
+void conv_i8(const ConvI8Params& p, hipStream_t s);
+void maxpool3x3s2_i8(const int8_t* in, int8_t* out, int B, int IH, int IW, int C, int OH, int OW,
+                     hipStream_t s);
+// int8 GAP -> fp32 mean * scale; ws: B * 16 * C floats
+void global_avgpool_i8(const int8_t* in, float* out, float* ws, int B, int HW, int C, float scale,
+                       hipStream_t s);
+
 // Fused MobileNetV2 inverted residual (expand 1x1 + ReLU6 -> dw 3x3 + ReLU6 ->
 // project 1x1 [+ residual]), dilation 1. Weights are host-padded: CinP, hidP
 // multiples of 32 (CinP <= 64), CoutP = 16 * ceil(Cout / 16).
@@ -63,9 +87,10 @@ void depthwise3x3(const bf16* in, const float* w, const float* bias, bf16* out, 
 // model pixel (y, x) = frame[lut_y[y], lut_x[x]] (or 0 where a lut is -1), RGB,
 // x/127.5 - 1 -> KxK stride-s conv (pad K/2) 3 -> Cout, bias + act, NHWC bf16.
 // w: [K*K*3, Cout] fp32 (tap-major, then input channel).
+// out_inv_scale > 0: int8 output round(v * out_inv_scale) (int8 pipelines).
 void stem_conv(const uint8_t* frames, const int32_t* lut_x, const int32_t* lut_y, const float* w,
-               const float* bias, bf16* out, int B, int Hc, int Wc, int H, int W, int OH, int OW,
-               int Cout, int K, int stride, int act, hipStream_t s);
+               const float* bias, void* out, int B, int Hc, int Wc, int H, int W, int OH, int OW,
+               int Cout, int K, int stride, int act, hipStream_t s, float out_inv_scale = 0.f);
 
 // 3x3 stride-2 pad-1 max pool, NHWC bf16 (ResNet stem).
 void maxpool3x3s2(const bf16* in, bf16* out, int B, int IH, int IW, int C, int OH, int OW,

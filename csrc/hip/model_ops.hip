@@ -73,9 +73,9 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ f
                                                    const int32_t* __restrict__ lut_y,
                                                    const float* __restrict__ w,
                                                    const float* __restrict__ bias,
-                                                   bf16* __restrict__ out, int B, int Hc, int Wc,
+                                                   void* __restrict__ outv, int B, int Hc, int Wc,
                                                    int H, int W, int OH, int OW, int K,
-                                                   int stride, int act) {
+                                                   int stride, int act, float out_inv_scale) {
   extern __shared__ __attribute__((aligned(16))) float sw[];  // [K*K*3][COUT] + bias
   const int nw = K * K * 3 * COUT;
   for (int i = threadIdx.x; i < nw; i += blockDim.x) sw[i] = w[i];
@@ -116,7 +116,19 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ f
         for (int n = 0; n < COUT; ++n) acc[n] += rgb[c] * wt[c * COUT + n];
     }
   }
-  bf16* op = out + t * COUT;
+  if (out_inv_scale > 0.f) {  // int8 output for the int8 pipelines
+    int8_t* op = static_cast<int8_t*>(outv) + t * COUT;
+#pragma unroll
+    for (int n = 0; n < COUT; n += 8) {
+      signed char q8[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        q8[q] = (signed char)fminf(fmaxf(rintf(apply_act(acc[n + q], act) * out_inv_scale), -127.f), 127.f);
+      *reinterpret_cast<int2*>(op + n) = *reinterpret_cast<int2*>(q8);
+    }
+    return;
+  }
+  bf16* op = static_cast<bf16*>(outv) + t * COUT;
 #pragma unroll
   for (int n = 0; n < COUT; n += 8) {
     bf16x8 o;
@@ -127,15 +139,15 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint8_t* __restrict__ f
 }
 
 void stem_conv(const uint8_t* frames, const int32_t* lut_x, const int32_t* lut_y, const float* w,
-               const float* bias, bf16* out, int B, int Hc, int Wc, int H, int W, int OH, int OW,
-               int Cout, int K, int stride, int act, hipStream_t s) {
+               const float* bias, void* out, int B, int Hc, int Wc, int H, int W, int OH, int OW,
+               int Cout, int K, int stride, int act, hipStream_t s, float out_inv_scale) {
   const long long total = (long long)B * OH * OW;
   const size_t lds = (size_t)(K * K * 3 * Cout + Cout) * sizeof(float);
   const int grid = cdiv(total, 256);
 #define STEM_CASE(C)                                                                          \
   case C:                                                                                     \
     hipLaunchKernelGGL(stem_kernel<C>, dim3(grid), dim3(256), lds, s, frames, lut_x, lut_y, w, \
-                       bias, out, B, Hc, Wc, H, W, OH, OW, K, stride, act);                  \
+                       bias, out, B, Hc, Wc, H, W, OH, OW, K, stride, act, out_inv_scale);   \
     break;
   switch (Cout) {
     STEM_CASE(16)

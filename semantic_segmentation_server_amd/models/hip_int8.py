@@ -1,0 +1,184 @@
+"""int8 DeepLabv3-ResNet50 on the gfx950 int8 MFMA kernels (BASELINE config 4).
+
+Same interface as ``HipDeepLab`` (``segment`` / ``logits``). The plan:
+
+  fused letterbox+stem conv (fp32 math, int8 out) -> int8 max pool
+  -> 16 bottlenecks: conv1 1x1, conv2 3x3 (strided / dilated), [down 1x1],
+     conv3 1x1 with the int8 identity fused as a dequantised residual, ReLU,
+     requantised int8 out
+  -> ASPP: 1x1 + three atrous 3x3 branches written into one int8 concat buffer
+     (shared scale); image pooling in fp32 folded into the projection's per-image
+     bias; projection int8 -> logits conv with bf16 output
+  -> fused bilinear upsample + argmax.
+
+Scales come from ``models.quant.calibrate`` on synthetic frames.
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, List, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from ..ops import hip_ops as K
+from ..ops.hip_ops import conv_out_hw
+from .deeplab import DeepLabV3, synthetic_normalized
+from .quant import calibrate, pack_int8
+
+
+class HipDeepLabInt8:
+    def __init__(self, model: DeepLabV3, device: torch.device, cfg=None,
+                 scales: Optional[Dict[str, float]] = None, calib_hw: int = 257):
+        self.device = device
+        self.model = model
+        self.H = self.W = int(cfg.input_size) if cfg is not None else 1025
+        self.num_classes = model.num_classes
+        self.ldk = (self.num_classes + 7) // 8 * 8
+        if scales is None:
+            x = synthetic_normalized(4, calib_hw, calib_hw, torch.Generator().manual_seed(11))
+            m32 = model.float()
+            if device.type == "cuda":
+                import copy
+                m32 = copy.deepcopy(model).float().to(device)
+                x = x.to(device)
+            scales = calibrate(m32, x)
+        self.scales = scales
+        S = scales
+        dev = device
+        bb = model.backbone
+        sw, sb = bb.stem.fold()
+        self.stem_w = sw.permute(2, 3, 1, 0).reshape(-1, sw.shape[0]).contiguous().to(dev, torch.float32)
+        self.stem_b = sb.to(dev, torch.float32)
+        self.stem_meta = (bb.stem.k, bb.stem.stride, bb.stem.cout)
+        self.blocks = []
+        s_in = S["stem"]  # max pool keeps the scale
+        for i, blk in enumerate(bb.blocks):
+            d = dict(blk=blk, s_in=s_in)
+            d["c1"] = pack_int8(blk.conv1, s_in, dev)
+            d["c2"] = pack_int8(blk.conv2, S[f"b{i}.c1"], dev)
+            d["c3"] = pack_int8(blk.conv3, S[f"b{i}.c2"], dev)
+            d["down"] = pack_int8(blk.down, s_in, dev) if blk.down is not None else None
+            d["s_res"] = S[f"b{i}.down"] if blk.down is not None else s_in
+            self.blocks.append(d)
+            s_in = S[f"b{i}.out"]
+        self.s_feat = s_in
+        a = model.aspp
+        self.A = a.cout
+        self.aspp_b0 = pack_int8(a.b0, s_in, dev)
+        self.aspp_atrous = [(pack_int8(br, s_in, dev), br.dilation) for br in a.atrous]
+        self.cat_c = (1 + len(a.atrous)) * a.cout
+        self.proj = pack_int8(a.project, S["aspp.cat"], dev, wslice=slice(0, self.cat_c))
+        pw, _ = a.project.fold()
+        self.proj_pool_w = pw[:, self.cat_c:, 0, 0].contiguous().to(dev, torch.float32)
+        qw, qb = a.pool.fold()
+        self.pool_w = qw[:, :, 0, 0].contiguous().to(dev, torch.float32)
+        self.pool_b = qb.to(dev, torch.float32)
+        self.logits_p = pack_int8(model.logits, S["aspp.proj"], dev)
+        self._plans: Dict[tuple, Tuple[List[Callable], Dict[str, torch.Tensor]]] = {}
+
+    def _plan(self, B: int, Hc: int, Wc: int):
+        key = (B, Hc, Wc)
+        if key in self._plans:
+            return self._plans[key]
+        dev, S = self.device, self.scales
+        bufs: Dict[str, torch.Tensor] = {}
+        ops: List[Callable] = []
+
+        def buf(name, *shape, dtype=torch.int8):
+            t = torch.empty(shape, dtype=dtype, device=dev)
+            bufs[name] = t
+            return t
+
+        H, W = self.H, self.W
+        k, st, c = self.stem_meta
+        OH, OW = conv_out_hw(H, W, k, st, 1)
+        x = buf("stem", B, OH, OW, c)
+        ops.append(lambda frames, lx, ly, x=x, OH=OH, OW=OW, c=c: K.stem_conv(
+            frames, lx, ly, self.stem_w, self.stem_b, x, H=H, W=W, OH=OH, OW=OW, Cout=c, k=k,
+            stride=st, act="relu", out_scale=S["stem"]))
+        PH, PW = conv_out_hw(OH, OW, 3, 2, 1)
+        y = buf("pool0", B, PH, PW, c)
+        ops.append(lambda *_, x=x, y=y, OH=OH, OW=OW, PH=PH, PW=PW, c=c: K.maxpool3x3s2_i8(
+            x, y, B=B, IH=OH, IW=OW, C=c, OH=PH, OW=PW))
+        x, h, w = y, PH, PW
+        for i, d in enumerate(self.blocks):
+            x, h, w, c = self._block(ops, buf, i, d, x, B, h, w, c)
+        # ASPP
+        A = self.A
+        cat = buf("aspp_cat", B, h, w, self.cat_c)
+        s_cat = S["aspp.cat"]
+        w8, sc, bi = self.aspp_b0
+        ops.append(lambda *_, x=x, h=h, w=w, c=c: K.conv_i8(
+            x, w8, sc, bi, cat, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w, Cout=A, ldo=self.cat_c,
+            co_off=0, act="relu", out_scale=s_cat))
+        for j, ((aw, asc, ab), rate) in enumerate(self.aspp_atrous):
+            ops.append(lambda *_, x=x, h=h, w=w, c=c, aw=aw, asc=asc, ab=ab, rate=rate, j=j: K.conv_i8(
+                x, aw, asc, ab, cat, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w, Cout=A, k=3, dil=rate,
+                ldo=self.cat_c, co_off=(j + 1) * A, act="relu", out_scale=s_cat))
+        gap = buf("gap", B, c, dtype=torch.float32)
+        gws = buf("gap_ws", B * 16 * c, dtype=torch.float32)
+        pooled = buf("pooled", B, A, dtype=torch.float32)
+        img_bias = buf("img_bias", B, A, dtype=torch.float32)
+        ops.append(lambda *_, x=x, h=h, w=w, c=c: K.global_avgpool_i8(
+            x, gap, gws, B=B, HW=h * w, C=c, scale=self.s_feat))
+        ops.append(lambda *_, c=c: K.matvec(gap, self.pool_w, self.pool_b, pooled, B=B, N=A, K=c,
+                                            act="relu"))
+        ops.append(lambda *_: K.matvec(pooled, self.proj_pool_w, None, img_bias, B=B, N=A, K=A))
+        proj = buf("aspp_proj", B, h, w, A)
+        pw8, psc, pb = self.proj
+        ops.append(lambda *_, h=h, w=w: K.conv_i8(
+            cat, pw8, psc, pb, proj, B=B, IH=h, IW=w, Cin=self.cat_c, OH=h, OW=w, Cout=A,
+            act="relu", img_bias=img_bias, out_scale=S["aspp.proj"]))
+        logits = buf("logits", B, h, w, self.ldk, dtype=torch.bfloat16)
+        lw8, lsc, lb = self.logits_p
+        ops.append(lambda *_, h=h, w=w: K.conv_i8(
+            proj, lw8, lsc, lb, logits, B=B, IH=h, IW=w, Cin=A, OH=h, OW=w,
+            Cout=self.num_classes, ldo=self.ldk, act=None))
+        labels = buf("labels", B, H, W, dtype=torch.uint8)
+        ops.append(lambda *_, h=h, w=w: K.upsample_argmax(
+            logits, labels, B=B, h=h, w=w, K=self.num_classes, ldk=self.ldk, H=H, W=W))
+        self._plans[key] = (ops, bufs)
+        return self._plans[key]
+
+    def _block(self, ops, buf, i, d, x, B, h, w, c):
+        S = self.scales
+        m = d["blk"]
+        width, cout = m.conv1.cout, m.conv3.cout
+        OH, OW = conv_out_hw(h, w, 3, m.stride, m.dilation)
+        w1, s1, b1 = d["c1"]
+        t1 = buf(f"r{i}_c1", B, h, w, width)
+        ops.append(lambda *_, x=x, t1=t1, h=h, w=w, c=c: K.conv_i8(
+            x, w1, s1, b1, t1, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w, Cout=width, act="relu",
+            out_scale=S[f"b{i}.c1"]))
+        w2, s2, b2 = d["c2"]
+        t2 = buf(f"r{i}_c2", B, OH, OW, width)
+        ops.append(lambda *_, t1=t1, t2=t2, h=h, w=w, OH=OH, OW=OW: K.conv_i8(
+            t1, w2, s2, b2, t2, B=B, IH=h, IW=w, Cin=width, OH=OH, OW=OW, Cout=width, k=3,
+            stride=m.stride, dil=m.dilation, act="relu", out_scale=S[f"b{i}.c2"]))
+        if d["down"] is not None:
+            wd, sd, bd = d["down"]
+            idt = buf(f"r{i}_down", B, OH, OW, cout)
+            ops.append(lambda *_, x=x, idt=idt, h=h, w=w, c=c, OH=OH, OW=OW: K.conv_i8(
+                x, wd, sd, bd, idt, B=B, IH=h, IW=w, Cin=c, OH=OH, OW=OW, Cout=cout,
+                stride=m.stride, act=None, out_scale=S[f"b{i}.down"]))
+        else:
+            idt = x
+        w3, s3, b3 = d["c3"]
+        out = buf(f"r{i}_out", B, OH, OW, cout)
+        ops.append(lambda *_, t2=t2, out=out, idt=idt, OH=OH, OW=OW: K.conv_i8(
+            t2, w3, s3, b3, out, B=B, IH=OH, IW=OW, Cin=width, OH=OH, OW=OW, Cout=cout,
+            act="relu", res=idt, res_scale=d["s_res"], out_scale=S[f"b{i}.out"]))
+        return out, OH, OW, cout
+
+    def segment(self, frames, lut_x, lut_y):
+        B, Hc, Wc, _ = frames.shape
+        ops, bufs = self._plan(B, Hc, Wc)
+        frames = frames.contiguous()
+        for op in ops:
+            op(frames, lut_x, lut_y)
+        return bufs["labels"]
+
+    def logits(self, frames, lut_x, lut_y):
+        self.segment(frames, lut_x, lut_y)
+        B, Hc, Wc, _ = frames.shape
+        return self._plans[(B, Hc, Wc)][1]["logits"][..., : self.num_classes]

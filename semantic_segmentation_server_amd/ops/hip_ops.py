@@ -183,7 +183,8 @@ def depthwise3x3(x, w, bias, out, *, B, IH, IW, C, OH, OW, stride=1, dil=1, act=
     return out
 
 
-def stem_conv(frames, lut_x, lut_y, w, bias, out, *, H, W, OH, OW, Cout, k, stride, act):
+def stem_conv(frames, lut_x, lut_y, w, bias, out, *, H, W, OH, OW, Cout, k, stride, act,
+              out_scale=None):
     """frames: [B,Hc,Wc,3] uint8 BGR; luts int32 [W]/[H]; w: [k*k*3, Cout] fp32."""
     B, Hc, Wc, C3 = frames.shape
     if C3 != 3:
@@ -193,10 +194,54 @@ def stem_conv(frames, lut_x, lut_y, w, bias, out, *, H, W, OH, OW, Cout, k, stri
     _chk(lut_y, torch.int32, "lut_y", H)
     _chk(w, torch.float32, "w", k * k * 3 * Cout)
     _chk(bias, torch.float32, "bias", Cout)
-    _chk(out, torch.bfloat16, "out", B * OH * OW * Cout)
+    _chk(out, torch.int8 if out_scale else torch.bfloat16, "out", B * OH * OW * Cout)
     _hip_mod().stem_conv(_ptr(frames), _ptr(lut_x), _ptr(lut_y), _ptr(w), _ptr(bias), _ptr(out), B,
-                         Hc, Wc, H, W, OH, OW, Cout, k, stride, ACT[act], _stream())
+                         Hc, Wc, H, W, OH, OW, Cout, k, stride, ACT[act], _stream(),
+                         1.0 / out_scale if out_scale else 0.0)
     _dbg('stem_conv')
+    return out
+
+
+def conv_i8(x, w8, scale, bias, out, *, B, IH, IW, Cin, OH, OW, Cout, k=1, stride=1, dil=1,
+            ldo=None, co_off=0, act=None, res=None, res_scale=0.0, img_bias=None,
+            out_scale=None) -> torch.Tensor:
+    """int8 NHWC conv. out int8 (out_scale given: v / out_scale rounded) or bf16."""
+    ldo = Cout if ldo is None else ldo
+    if Cin % 16:
+        raise ValueError("conv_i8: Cin must be a multiple of 16")
+    if co_off + Cout > ldo:
+        raise ValueError("conv_i8: co_off + Cout > ldo")
+    _chk(x, torch.int8, "x", B * IH * IW * Cin)
+    _chk(w8, torch.int8, "w", Cout * k * k * Cin)
+    _chk(scale, torch.float32, "scale", Cout)
+    _chk(bias, torch.float32, "bias", Cout)
+    mode = 0 if out_scale is not None else 1
+    _chk(out, torch.int8 if mode == 0 else torch.bfloat16, "out", B * OH * OW * ldo)
+    if res is not None:
+        _chk(res, torch.int8, "res", B * OH * OW * Cout)
+    if img_bias is not None:
+        _chk(img_bias, torch.float32, "img_bias", B * Cout)
+    _hip_mod().conv_i8(_ptr(x), _ptr(w8), _ptr(scale), _ptr(bias), _ptr(img_bias), _ptr(res),
+                       float(res_scale), _ptr(out), 1.0 / out_scale if mode == 0 else 1.0, mode, B,
+                       IH, IW, Cin, OH, OW, Cout, k, k, stride, dil, ldo, co_off, ACT[act], _stream())
+    _dbg('conv_i8')
+    return out
+
+
+def maxpool3x3s2_i8(x, out, *, B, IH, IW, C, OH, OW):
+    _chk(x, torch.int8, "x", B * IH * IW * C)
+    _chk(out, torch.int8, "out", B * OH * OW * C)
+    _hip_mod().maxpool3x3s2_i8(_ptr(x), _ptr(out), B, IH, IW, C, OH, OW, _stream())
+    _dbg('maxpool_i8')
+    return out
+
+
+def global_avgpool_i8(x, out, ws, *, B, HW, C, scale):
+    _chk(x, torch.int8, "x", B * HW * C)
+    _chk(out, torch.float32, "out", B * C)
+    _chk(ws, torch.float32, "ws", B * 16 * C)
+    _hip_mod().global_avgpool_i8(_ptr(x), _ptr(out), _ptr(ws), B, HW, C, float(scale), _stream())
+    _dbg('gap_i8')
     return out
 
 

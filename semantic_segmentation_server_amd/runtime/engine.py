@@ -82,6 +82,11 @@ class Engine:
             self.model = self.model.to(self.device, self.dtype)
             if self.is_cuda:
                 self.model = self.model.to(memory_format=torch.channels_last)
+        elif cfg.dtype == "int8":
+            if cfg.arch != "resnet50":
+                raise ValueError("--dtype int8 is implemented for --arch resnet50 (config 4)")
+            from ..models.hip_int8 import HipDeepLabInt8
+            self._hip_model = HipDeepLabInt8(self.model, self.device, cfg)
         else:
             from ..models.hip_model import HipDeepLab
             self._hip_model = HipDeepLab(self.model, self.device, cfg)

@@ -354,3 +354,90 @@ def test_dw_project(hid, cout, stride, dil, res):
                  res=None if r is None else _nhwc(r).to(DEV))
     torch.cuda.synchronize()
     assert _rel(_nchw(out).cpu(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("Cin,Cout,k,stride,dil,res,mode", [
+    (64, 256, 1, 1, 1, True, "i8"), (256, 64, 3, 2, 1, False, "i8"), (512, 512, 3, 1, 2, False, "i8"),
+    (256, 19, 1, 1, 1, False, "bf16"), (1024, 256, 1, 1, 1, False, "i8")])
+def test_conv_i8(Cin, Cout, k, stride, dil, res, mode):
+    K = _hip()
+    g = torch.Generator().manual_seed(12)
+    B, H = 2, 17
+    x8 = torch.randint(-127, 128, (B, Cin, H, H), generator=g, dtype=torch.int32)
+    w8 = torch.randint(-127, 128, (Cout, Cin, k, k), generator=g, dtype=torch.int32)
+    sc = torch.rand(Cout, generator=g) * 1e-4
+    bi = torch.randn(Cout, generator=g)
+    acc = F.conv2d(x8.double(), w8.double(), None, stride, dil * (k // 2), dil)  # exact
+    ref = acc.float() * sc.view(1, -1, 1, 1) + bi.view(1, -1, 1, 1)
+    OH, OW = ref.shape[-2:]
+    r8 = None
+    if res:
+        r8 = torch.randint(-127, 128, (B, Cout, OH, OW), generator=g, dtype=torch.int32)
+        ref = ref + r8.float() * 0.02
+    ref = torch.relu(ref)
+    xin = _nhwc(x8.to(torch.int8)).to(DEV)
+    wk = w8.to(torch.int8).permute(0, 2, 3, 1).contiguous().to(DEV)
+    if mode == "i8":
+        out = torch.empty(B, OH, OW, Cout, dtype=torch.int8, device=DEV)
+        K.conv_i8(xin, wk, sc.to(DEV), bi.to(DEV), out, B=B, IH=H, IW=H, Cin=Cin, OH=OH, OW=OW,
+                  Cout=Cout, k=k, stride=stride, dil=dil, act="relu",
+                  res=None if r8 is None else _nhwc(r8.to(torch.int8)).to(DEV), res_scale=0.02,
+                  out_scale=0.05)
+        torch.cuda.synchronize()
+        exp = torch.clamp(torch.round(ref / 0.05), -127, 127)
+        diff = (_nchw(out).cpu().float() - exp).abs()
+        assert diff.max() <= 1 and (diff > 0).float().mean() < 1e-3
+    else:
+        out = torch.empty(B, OH, OW, Cout, dtype=torch.bfloat16, device=DEV)
+        K.conv_i8(xin, wk, sc.to(DEV), bi.to(DEV), out, B=B, IH=H, IW=H, Cin=Cin, OH=OH, OW=OW,
+                  Cout=Cout, k=k, stride=stride, dil=dil, act="relu")
+        torch.cuda.synchronize()
+        assert _rel(_nchw(out).cpu(), ref) < 5e-3
+
+
+def test_int8_resnet50_matches_fake_quant():
+    from semantic_segmentation_server_amd.models.deeplab import build_model
+    from semantic_segmentation_server_amd.models.hip_int8 import HipDeepLabInt8
+    from semantic_segmentation_server_amd.models.quant import fake_quant_forward
+    from semantic_segmentation_server_amd.ops import reference_ops as R
+    S = 129
+    from semantic_segmentation_server_amd.models.quant import calibrate
+    from semantic_segmentation_server_amd.runtime.sources import SyntheticSource
+    model = build_model("resnet50", 19, calibrate_hw=65)
+    lx, ly, *_ = R.letterbox_luts(160, 120, S, S)
+    f, _, _ = SyntheticSource(160, 120, pool=2, seed=13).read_batch(2)
+    frames = torch.from_numpy(f)
+    x = R.preprocess(frames, lx, ly)
+    scales = calibrate(model.float(), x)  # calibrate on the evaluation distribution
+    hm = HipDeepLabInt8(model, torch.device(DEV), _small_cfg(arch="resnet50", dtype="int8"),
+                        scales=scales)
+    ref = fake_quant_forward(model.float(), hm.scales, x)
+    with torch.no_grad():
+        fp = model.float()(x)
+    got = _nchw(hm.logits(frames.to(DEV), torch.tensor(lx, device=DEV),
+                          torch.tensor(ly, device=DEV)).float()).cpu()
+    e_fq, e_fp = _rel(got, ref), _rel(got, fp)
+    print(f"int8 resnet50: rel err vs fake-quant {e_fq:.4f}, vs fp32 {e_fp:.4f}")
+    assert e_fq < 0.03
+    assert e_fp < 0.15
+    agree = (got.argmax(1) == fp.argmax(1)).float().mean().item()
+    assert agree > 0.95, agree
+
+
+def test_stream_group_matches_single_engine():
+    from semantic_segmentation_server_amd.runtime.engine import Engine
+    from semantic_segmentation_server_amd.runtime.multistream import StreamGroup
+    from semantic_segmentation_server_amd.runtime.sources import SyntheticSource
+    cfg = _small_cfg(graph=True, batch=4)
+    grp = StreamGroup(cfg, torch.device(DEV), 2)
+    one = Engine(cfg, torch.device(DEV))
+    for e in (grp, one):
+        e.set_camera(200, 150)
+    f, _, _ = SyntheticSource(200, 150, pool=4).read_batch(4)
+    d = torch.from_numpy(f).to(DEV)
+    _, p1 = one.run_device(d)
+    p1 = p1.clone()
+    for _ in range(2):
+        _, p2 = grp.run_device(d)
+    torch.cuda.synchronize()
+    assert torch.equal(p1, p2)
