@@ -40,15 +40,23 @@ PYBIND11_MODULE(_hip, m) {
   m.def("fused_ir",
         [](uintptr_t in, uintptr_t we, uintptr_t be, uintptr_t wd, uintptr_t bd, uintptr_t wp,
            uintptr_t bp, uintptr_t out, int B, int IH, int IW, int Cin, int CinP, int hidP,
-           int Cout, int OH, int OW, int stride, int residual, uintptr_t stream) {
+           int Cout, int OH, int OW, int stride, int residual, uintptr_t stream, int dil, int TY,
+           int TX) {
           FusedIRParams p;
           p.in = P<const bf16>(in); p.we = P<const bf16>(we); p.be = P<const float>(be);
           p.wd = P<const float>(wd); p.bd = P<const float>(bd); p.wp = P<const bf16>(wp);
           p.bp = P<const float>(bp); p.out = P<bf16>(out);
           p.B = B; p.IH = IH; p.IW = IW; p.Cin = Cin; p.CinP = CinP; p.hidP = hidP; p.Cout = Cout;
           p.OH = OH; p.OW = OW; p.stride = stride; p.residual = residual;
+          p.dil = dil; p.TY = TY; p.TX = TX;
           fused_inverted_residual(p, S(stream));
-        });
+        },
+        py::arg("in"), py::arg("we"), py::arg("be"), py::arg("wd"), py::arg("bd"), py::arg("wp"),
+        py::arg("bp"), py::arg("out"), py::arg("B"), py::arg("IH"), py::arg("IW"), py::arg("Cin"),
+        py::arg("CinP"), py::arg("hidP"), py::arg("Cout"), py::arg("OH"), py::arg("OW"),
+        py::arg("stride"), py::arg("residual"), py::arg("stream"), py::arg("dil") = 1,
+        py::arg("TY") = 0, py::arg("TX") = 0);
+  m.def("fused_ir_tile_lds", &fused_ir_tile_lds);
 
   m.def("dw_project",
         [](uintptr_t hid_in, uintptr_t wd, uintptr_t bd, uintptr_t wp, uintptr_t bp, uintptr_t res,

@@ -61,8 +61,12 @@ struct FusedIRParams {
   bf16* out = nullptr;        // [B, OH, OW, Cout]
   int B = 0, IH = 0, IW = 0, Cin = 0, CinP = 0, hidP = 0, Cout = 0, OH = 0, OW = 0;
   int stride = 1, residual = 0;
+  int dil = 1;         // tile kernel only
+  int TY = 0, TX = 0;  // > 0: general 2-D tile kernel (any dilation, CinP <= 160, CoutP <= 320)
 };
 void fused_inverted_residual(const FusedIRParams& p, hipStream_t s);
+// LDS bytes the tile kernel needs for a (TY, TX) tile (0 if the shape is unsupported).
+size_t fused_ir_tile_lds(int CinP, int stride, int dil, int TY, int TX);
 
 // Depthwise 3x3 (+bias, ReLU6) fused with the 1x1 projection (+bias [+ residual]):
 // the depthwise output stays in registers as the projection's MFMA operand.

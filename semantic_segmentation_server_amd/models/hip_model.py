@@ -48,6 +48,22 @@ def _pack_dw(layer: ConvBNAct, dev) -> Tuple[torch.Tensor, torch.Tensor]:
             b.contiguous().to(dev, torch.float32))
 
 
+_TILES = [(8, 16), (4, 16), (11, 11), (5, 11), (8, 13), (5, 13)]
+
+
+def _tile_candidates(OH: int, OW: int, CinP: int, stride: int, dil: int) -> List[Tuple[int, int]]:
+    """2-D output tiles for the general fused-IR kernel: at most 8 MFMA pixel groups,
+    LDS within one CU's 160 KB, and at most 25 % of the tiled area wasted."""
+    out = []
+    for ty, tx in _TILES:
+        if -(-ty * tx // 16) > 8 or K.fused_ir_tile_lds(CinP, stride, dil, ty, tx) > 160 * 1024:
+            continue
+        covered = -(-OH // ty) * ty * -(-OW // tx) * tx
+        if covered <= 1.25 * OH * OW:
+            out.append((ty, tx))
+    return out
+
+
 class Choice:
     """A plan step with alternative implementations; ``autotune`` keeps the
     fastest on the actual shapes (timed with HIP events at plan build)."""
@@ -114,17 +130,25 @@ class HipDeepLab:
                     expand=_pack_dense(blk.expand, dev) if blk.expand is not None else None,
                     dw=_pack_dw(blk.dw, dev),
                     project=_pack_dense(blk.project, dev))
-                if s.dilation == 1 and s.cin <= 64 and s.cout <= 96 and s.cin % 8 == 0:
+                row_ok = s.dilation == 1 and s.cin <= 64 and s.cout <= 96 and s.cin % 8 == 0
+                tile_ok = (blk.expand is not None and s.cin % 8 == 0 and
+                           (-(-s.cout // 16), -(-s.cin // 32)) in K.FUSED_TILE_SHAPES)
+                if row_ok or tile_ok:
                     ew = eb = None
                     if blk.expand is not None:
                         ew, eb = blk.expand.fold()
                         ew = ew[:, :, 0, 0]
                     dwf, dbf = blk.dw.fold()
                     pwf, pbf = blk.project.fold()
-                    d["fused"] = K.pack_fused_ir(
+                    packed = K.pack_fused_ir(
                         ew, eb, dwf[:, 0], dbf, pwf[:, :, 0, 0], pbf, Cin=s.cin, hid=s.hidden,
-                        Cout=s.cout, stride=s.stride, residual=s.residual, device=dev)
-                elif s.hidden % 32 == 0 and blk.expand is not None:
+                        Cout=s.cout, stride=s.stride, residual=s.residual, device=dev,
+                        dil=s.dilation)
+                    if row_ok:
+                        d["fused"] = packed
+                    if tile_ok:
+                        d["fused_tile"] = packed
+                if s.hidden % 32 == 0 and blk.expand is not None and not row_ok:
                     pwf, pbf = blk.project.fold()
                     d["dwproj"] = K.pack_project_padded(pwf[:, :, 0, 0], pbf, s.cout, s.hidden, dev)
                 self.blocks.append(d)
@@ -285,6 +309,12 @@ class HipDeepLab:
                                         res=res: K.dw_project(
                 e, dw_w, dw_b, dpw, dpb, out, B=B, IH=h, IW=w, hid=hid, Cout=s.cout, OH=OH, OW=OW,
                 stride=s.stride, dil=s.dilation, res=res)]))
+        if "fused_tile" in blk:
+            fp = blk["fused_tile"]
+            for tile in _tile_candidates(OH, OW, fp["CinP"], s.stride, s.dilation):
+                variants.insert(0, (f"tile{tile[0]}x{tile[1]}", [
+                    lambda *_, x=inp, out=out, h=h, w=w, OH=OH, OW=OW, tile=tile: K.fused_ir(
+                        x, fp, out, B=B, IH=h, IW=w, OH=OH, OW=OW, tile=tile)]))
         if "fused" in blk:
             fp = blk["fused"]
             variants.insert(0, ("fused", [lambda *_, x=inp, out=out, h=h, w=w, OH=OH, OW=OW:

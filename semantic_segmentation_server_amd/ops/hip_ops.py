@@ -85,9 +85,15 @@ def conv_gemm(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out: torch.T
     return out
 
 
-def fused_ir(x, packed: dict, out, *, B, IH, IW, OH, OW):
-    """Fused inverted residual. ``packed`` from ``pack_fused_ir``."""
+def fused_ir(x, packed: dict, out, *, B, IH, IW, OH, OW, tile=None):
+    """Fused inverted residual. ``packed`` from ``pack_fused_ir``.
+
+    ``tile=(TY, TX)`` selects the general 2-D tile kernel (any dilation, Cin <= 160,
+    Cout <= 320); ``None`` the 16-wide row-tile kernel (dilation 1, Cin <= 64)."""
     P = packed
+    TY, TX = tile if tile is not None else (0, 0)
+    if tile is None and P.get("dil", 1) != 1:
+        raise ValueError("fused_ir: dilated blocks need the tile kernel")
     _chk(x, torch.bfloat16, "x", B * IH * IW * P["Cin"])
     _chk(out, torch.bfloat16, "out", B * OH * OW * P["Cout"])
     if P["we"] is not None:
@@ -99,7 +105,8 @@ def fused_ir(x, packed: dict, out, *, B, IH, IW, OH, OW):
         raise ValueError("fused_ir: output size mismatch")
     _hip_mod().fused_ir(_ptr(x), _ptr(P["we"]), _ptr(P["be"]), _ptr(P["wd"]), _ptr(P["bd"]),
                         _ptr(P["wp"]), _ptr(P["bp"]), _ptr(out), B, IH, IW, P["Cin"], P["CinP"],
-                        P["hidP"], P["Cout"], OH, OW, P["stride"], int(P["residual"]), _stream())
+                        P["hidP"], P["Cout"], OH, OW, P["stride"], int(P["residual"]), _stream(),
+                        P.get("dil", 1), TY, TX)
     _dbg('fused_ir')
     return out
 
@@ -134,7 +141,16 @@ def pack_project_padded(wp, bp, Cout, hid, device):
     return w.to(torch.bfloat16).contiguous(), b
 
 
-def pack_fused_ir(we, be, wd, bd, wp, bp, *, Cin, hid, Cout, stride, residual, device) -> dict:
+# (Cout/16, CinP/32) shapes the tile kernel is instantiated for (fused_ir.hip)
+FUSED_TILE_SHAPES = {(4, 2), (6, 2), (6, 3), (10, 3), (10, 5), (20, 5), (4, 1), (2, 1)}
+
+
+def fused_ir_tile_lds(CinP, stride, dil, TY, TX) -> int:
+    return int(_hip_mod().fused_ir_tile_lds(CinP, stride, dil, TY, TX))
+
+
+def pack_fused_ir(we, be, wd, bd, wp, bp, *, Cin, hid, Cout, stride, residual, device,
+                  dil=1) -> dict:
     """Zero-pad folded block weights to the fused kernel's layout.
 
     we: [hid, Cin] (or None when the block has no expansion), wd: [hid, 3, 3],
@@ -145,7 +161,7 @@ def pack_fused_ir(we, be, wd, bd, wp, bp, *, Cin, hid, Cout, stride, residual, d
     CoutP = (Cout + 15) // 16 * 16
     f32 = dict(dtype=torch.float32, device=device)
     out = dict(Cin=Cin, CinP=CinP, hidP=hidP, Cout=Cout, CoutP=CoutP, stride=stride,
-               residual=residual, we=None)
+               residual=residual, we=None, dil=dil)
     if we is not None:
         t = torch.zeros(hidP, CinP, **f32)
         t[:hid, :Cin] = we

@@ -329,6 +329,48 @@ def test_fused_inverted_residual(cin, cout, t, stride, H):
     assert _rel(_nchw(out).cpu(), ref) < 2e-2
 
 
+@pytest.mark.parametrize("cin,cout,stride,dil,H,tile", [
+    (64, 64, 1, 1, 33, (11, 11)),    # residual, CinP 64
+    (64, 96, 1, 1, 33, (5, 11)),
+    (96, 96, 1, 1, 33, (11, 11)),    # CinP 96
+    (96, 160, 1, 1, 33, (11, 11)),
+    (160, 160, 1, 2, 33, (11, 11)),  # dilation 2 + residual, CinP 160
+    (160, 320, 1, 2, 33, (5, 11)),   # Cout 320
+    (160, 160, 1, 2, 29, (8, 16)),   # partial tiles at the right/bottom edge
+    (24, 32, 2, 1, 65, (8, 16)),     # stride 2, CinP 32
+    (32, 64, 2, 1, 65, (5, 11)),
+])
+def test_fused_ir_tile(cin, cout, stride, dil, H, tile):
+    from semantic_segmentation_server_amd.models.layers import init_random
+    from semantic_segmentation_server_amd.models.mobilenetv2 import InvertedResidual, IRSpec
+    K = _hip()
+    spec = IRSpec(cin, cout, 6, stride, dil)
+    blk = InvertedResidual(spec)
+    init_random(blk, seed=cin + 3 * cout + dil)
+    for m in blk.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.uniform_(-0.2, 0.2)
+            m.running_var.uniform_(0.5, 2.0)
+    blk.eval()
+    g = torch.Generator().manual_seed(19)
+    B, W = 2, H + 4
+    x = torch.randn(B, cin, H, W, generator=g).to(torch.bfloat16)
+    with torch.no_grad():
+        ref = blk(x.float())
+    OH, OW = ref.shape[-2:]
+    ew, eb = blk.expand.fold()
+    dwf, dbf = blk.dw.fold()
+    pwf, pbf = blk.project.fold()
+    packed = K.pack_fused_ir(ew[:, :, 0, 0], eb, dwf[:, 0], dbf, pwf[:, :, 0, 0], pbf, Cin=cin,
+                             hid=spec.hidden, Cout=cout, stride=stride, residual=spec.residual,
+                             device=DEV, dil=dil)
+    out = torch.full((B, OH, OW, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
+    K.fused_ir(_nhwc(x).to(DEV), packed, out, B=B, IH=H, IW=W, OH=OH, OW=OW, tile=tile)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    assert _rel(_nchw(out).cpu(), ref) < 2e-2
+
+
 @pytest.mark.parametrize("hid,cout,stride,dil,res", [(576, 96, 1, 1, True), (576, 160, 1, 1, False),
                                                      (960, 160, 1, 2, True), (960, 320, 1, 2, False),
                                                      (384, 64, 2, 1, False)])
