@@ -345,6 +345,218 @@ __global__ __launch_bounds__(256) void conv_gemm_lds_kernel(ConvArgs a) {
   }
 }
 
+static int pick_nt(int Cout);
+// ---------------------------------------------------------------------------
+// LDS-DMA pipelined variant: operand tiles go global -> LDS with gfx950's
+// global_load_lds_dwordx4 (no VGPR staging, no ds_write pass), ST-stage ring with
+// ST-1 stages in flight across raw s_barriers and a counted vmcnt, so HBM/MALL
+// latency hides behind several K-steps of MFMA even at 1-2 blocks per CU (the
+// regime of every deep-K conv here: 128x128 tiles over M = B*33*33 or B*65*65).
+// One glds wave-instruction writes 1 KiB = 8 rows x 128 B lane-linearly, so the
+// XOR swizzle (phys chunk = logical ^ (row & 7)) is applied on the SOURCE
+// address; padded chunks (outside the image, beyond Cin/Cout, M tail) read from a
+// zero page, so the LDS image is always fully written.
+__device__ __attribute__((aligned(16))) int4 g_zero_page[8];
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+template <int MT, int NT, int ST>
+__global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs a) {
+  constexpr int BM = 32 * MT, BN = 32 * NT, ROWB = 128;  // BK = 64 bf16 per stage row
+  constexpr int GA = BM / 32, GB = BN / 32;              // glds per thread per stage
+  constexpr int SB = (BM + BN) * ROWB;
+  constexpr int VM_INFLIGHT = (ST - 2) * (GA + GB);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* s_tap = reinterpret_cast<int*>(smem + ST * SB);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int r16 = lane & 15, kq = lane >> 4;
+  const int M = a.B * a.OH * a.OW;
+  const int tiles_m = cdiv_dev(M, BM), tiles_n = cdiv_dev(a.Cout, BN);
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tn = bid % tiles_n, tm = bid / tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int taps = a.KH * a.KW;
+  const int grow = lane >> 3;        // row inside the 8-row group of one glds
+  const int lc = (lane & 7) ^ grow;  // logical K-chunk this lane fetches
+
+  int ay[GA], ax[GA], aoff[GA];
+  bool av[GA];
+  int tapbits = 0;
+#pragma unroll
+  for (int i = 0; i < GA; ++i) {
+    const int m = m0 + wid * (BM / 4) + i * 8 + grow;
+    av[i] = m < M;
+    const int mm = av[i] ? m : 0;
+    const int b = mm / (a.OH * a.OW);
+    const int rem = mm - b * a.OH * a.OW;
+    ay[i] = (rem / a.OW) * a.stride;
+    ax[i] = (rem % a.OW) * a.stride;
+    aoff[i] = ((b * a.IH + ay[i]) * a.IW + ax[i]) * a.Cin;
+    if (av[i])
+      for (int t = 0; t < taps; ++t) {
+        const int iy = ay[i] + (t / a.KW - a.KH / 2) * a.dil;
+        const int ix = ax[i] + (t % a.KW - a.KW / 2) * a.dil;
+        if (iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW) tapbits |= 1 << t;
+      }
+  }
+  int boff[GB];
+  bool bv[GB];
+#pragma unroll
+  for (int j = 0; j < GB; ++j) {
+    const int n = n0 + wid * (BN / 4) + j * 8 + grow;
+    bv[j] = n < a.Cout;
+    boff[j] = (bv[j] ? n : 0) * taps * a.Cin;
+  }
+  if (tid == 0) *s_tap = 0;
+  __syncthreads();
+  if (tapbits) atomicOr(s_tap, tapbits);
+  __syncthreads();
+  const int tapmask = __builtin_amdgcn_readfirstlane(*s_tap);
+  unsigned long long tl = 0;  // live taps, 4 bits each
+  int ntap = 0;
+  for (int t = 0; t < taps; ++t)
+    if ((tapmask >> t) & 1) { tl |= (unsigned long long)t << (4 * ntap); ++ntap; }
+  const int cch = cdiv_dev(a.Cin, 64);
+  const int total = ntap * cch;
+
+  int is_tap = 0, is_c = 0;  // issue cursor
+  auto issue = [&](int stage) {
+    const int t = (int)((tl >> (4 * is_tap)) & 15);
+    const int dy = (t / a.KW - a.KH / 2) * a.dil, dx = (t % a.KW - a.KW / 2) * a.dil;
+    const int c = is_c * 64 + lc * 8;
+    const bool cok = c < a.Cin;
+    const int doff = (dy * a.IW + dx) * a.Cin + c;
+    char* sA = smem + stage * SB;
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      const int iy = ay[i] + dy, ix = ax[i] + dx;
+      const bool ok = av[i] && cok && iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW;
+      const void* src = ok ? (const void*)(a.in + aoff[i] + doff) : (const void*)g_zero_page;
+      __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(sA + (wid * (BM / 4) + i * 8) * ROWB), 16, 0, 0);
+    }
+    char* sB = sA + BM * ROWB;
+    const int wofs = t * a.Cin + c;
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      const void* src = (bv[j] && cok) ? (const void*)(a.w + boff[j] + wofs) : (const void*)g_zero_page;
+      __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(sB + (wid * (BN / 4) + j * 8) * ROWB), 16, 0, 0);
+    }
+    if (++is_c == cch) { is_c = 0; ++is_tap; }
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < ST - 1; ++s)
+    if (s < total) issue(s);
+  for (int k = 0; k < total; ++k) {
+    if (k + ST - 2 < total) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_INFLIGHT) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (k + ST - 1 < total) issue((k + ST - 1) % ST);
+    const char* sA = smem + (k % ST) * SB;
+    const char* sB = sA + BM * ROWB;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int kc = ks * 4 + kq;
+      bf16x8 bfr[MT], afr[NT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int r = wm * 16 * MT + i * 16 + r16;
+        bfr[i] = *reinterpret_cast<const bf16x8*>(sA + r * ROWB + ((kc ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = wn * 16 * NT + j * 16 + r16;
+        afr[j] = *reinterpret_cast<const bf16x8*>(sB + n * ROWB + ((kc ^ (n & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[j], bfr[i], acc[i][j], 0, 0, 0);
+    }
+  }
+
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int m = m0 + wm * 16 * MT + i * 16 + r16;
+    if (m >= M) continue;
+    const int b = m / (a.OH * a.OW);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = n0 + wn * 16 * NT + j * 16 + kq * 4;
+      if (n >= a.Cout) continue;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      const bool full = n + 3 < a.Cout;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (n + q < a.Cout) {
+          v[q] += a.bias[n + q];
+          if (a.img_bias) v[q] += a.img_bias[(long long)b * a.Cout + n + q];
+        }
+      }
+      if (a.res) {
+        const bf16* rp = a.res + (long long)m * a.ldr + n;
+        if (full && (a.ldr & 3) == 0) {
+          const bf16x4 rv4 = *reinterpret_cast<const bf16x4*>(rp);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] += (float)rv4[q];
+        } else {
+          for (int q = 0; q < 4; ++q) if (n + q < a.Cout) v[q] += (float)rp[q];
+        }
+      }
+      bf16* op = a.out + (long long)m * a.ldo + a.co_off + n;
+      if (full && ((a.ldo | a.co_off) & 3) == 0) {
+        bf16x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = (bf16)apply_act(v[q], a.act);
+        *reinterpret_cast<bf16x4*>(op) = o;
+      } else {
+        for (int q = 0; q < 4; ++q)
+          if (n + q < a.Cout) op[q] = (bf16)apply_act(v[q], a.act);
+      }
+    }
+  }
+}
+
+template <int MT, int NT, int ST>
+static void launch_conv_glds(const ConvArgs& a, hipStream_t s) {
+  const int M = a.B * a.OH * a.OW;
+  const int grid = cdiv(M, 32 * MT) * cdiv(a.Cout, 32 * NT);
+  const size_t lds = (size_t)ST * (32 * MT + 32 * NT) * 128 + 16;
+  static bool attr_set = false;
+  if (!attr_set) {
+    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_glds_kernel<MT, NT, ST>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
+          "conv_glds attr");
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((conv_glds_kernel<MT, NT, ST>), dim3(grid), dim3(256), lds, s, a);
+  check_launch("conv_glds");
+}
+
+template <int ST>
+static void dispatch_glds(const ConvArgs& a, hipStream_t s) {
+  switch (pick_nt(a.Cout)) {
+    case 1: launch_conv_glds<4, 1, ST>(a, s); break;
+    case 2: launch_conv_glds<4, 2, ST>(a, s); break;
+    case 3: launch_conv_glds<4, 3, ST>(a, s); break;
+    case 4: launch_conv_glds<4, 4, ST>(a, s); break;
+    case 5: launch_conv_glds<4, 5, ST>(a, s); break;
+    default: launch_conv_glds<4, 6, ST>(a, s); break;
+  }
+}
+
 template <int MT, int NT, int KS>
 static void launch_conv_lds(const ConvArgs& a, hipStream_t s) {
   const int M = a.B * a.OH * a.OW;
@@ -394,6 +606,15 @@ void conv_gemm(const ConvParams& p, hipStream_t s) {
   const long long M = (long long)p.B * p.OH * p.OW;
   const long long tiles = (M + 127) / 128 * cdiv(p.Cout, 32 * pick_nt(p.Cout));
   const long long K = (long long)p.KH * p.KW * p.Cin;
+  if (p.variant == 3 || p.variant == 4) {
+    // int32 offsets inside the kernel
+    if ((long long)p.B * p.IH * p.IW * p.Cin >= (1LL << 31) || (long long)p.Cout * K >= (1LL << 31))
+      throw std::invalid_argument("conv_gemm glds: tensor too large for 32-bit offsets");
+    if (p.KH * p.KW > 16) throw std::invalid_argument("conv_gemm glds: at most 16 taps");
+    if (p.variant == 3) dispatch_glds<3>(a, s);
+    else dispatch_glds<2>(a, s);
+    return;
+  }
   if (p.variant == 2 || (p.variant == 0 && tiles >= 256 && K >= 512)) {
     // LDS-staged MFMA path: deep K (ASPP atrous 2880, projections 576-1024) and
     // enough 128-pixel tiles to fill the chip. Shallow-K layers are write-bound

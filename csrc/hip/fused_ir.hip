@@ -220,23 +220,31 @@ void launch_ir(const IRArgs& a, hipStream_t st) {
 
 
 // ---------------------------------------------------------------------------
-// General 2-D tile variant for the low-resolution wide blocks (33x33 maps at
-// output stride 16: Cin 64..160, hid 384..960, Cout 64..320, dilation 1 or 2).
-// 33 = 3 x 11, so an 11x11 (or 5x11) output tile covers the map with no waste,
-// where the 16-wide tiles above waste 31 % of every row. Output pixel p of the
-// tile is (p / TX, p % TX); 16-pixel MFMA groups are assigned GPW per wave, so
-// the lane -> pixel map is arbitrary and the depthwise reads use per-lane LDS
-// addresses. The expansion over the halo is recomputed per tile
-// ((TY-1)s+2d+1) x ((TX-1)s+2d+1); on these blocks that is ~12 % of the MFMA
-// peak at most, against 3 x [B,33,33,hid] bf16 round trips through HBM for the
-// unfused expand -> depthwise -> project chain.
+// General 2-D tile variant (any stride/dilation, Cin <= 160, Cout <= 320, with or
+// without expansion). Output pixel p of the tile is (p / TX, p % TX); 16-pixel
+// MFMA groups are assigned GPW per wave, so the lane -> pixel map is arbitrary
+// and the depthwise reads use per-lane LDS addresses. 33 = 3 x 11, so 11x11 /
+// 5x11 tiles cover the 33x33 maps with no waste where 16-wide tiles waste 31 %.
+//
+// Internals run in fp16 (PMC: the bf16/fp32 version was VALU-bound — 2k VALU
+// instructions per wave, ~45 % of the kernel — on bf16->f32 unpacking and scalar
+// FMAs): the expansion epilogue writes relu6(x) as fp16 into LDS, the depthwise
+// runs as v_pk_fma_f16 (2 MACs per instruction, no unpacking), and the projection
+// uses v_mfma_f32_16x16x32_f16 on fp16 weights, so the depthwise result feeds the
+// MFMA with no conversion. relu6-bounded activations lose nothing in fp16 (11-bit
+// mantissa vs bf16's 8); accumulation of the projection stays fp32.
+typedef _Float16 f16;
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
 struct IRTArgs {
-  const bf16* in; const bf16* we; const float* be; const float* wd; const float* bd;
-  const bf16* wp; const float* bp; bf16* out;
+  const bf16* in; const bf16* we; const float* be; const f16* wd; const f16* bd;
+  const f16* wp; const float* bp; bf16* out;
   int B, IH, IW, Cin, hidP, Cout, OH, OW, stride, dil, residual, TY, TX, tiles_y, tiles_x;
 };
 
-template <int NSUB, int KS, int GPW>
+template <int NSUB, int KS, int GPW, bool EXPAND>
 __global__ __launch_bounds__(256) void fused_ir_tile_kernel(IRTArgs a) {
   constexpr int CinP = KS * 32;
   constexpr int XS = CinP + 8, ES = 32 + 8;  // +16 B per LDS row: conflict-free ds_read_b128
@@ -245,8 +253,8 @@ __global__ __launch_bounds__(256) void fused_ir_tile_kernel(IRTArgs a) {
   const int TIH = (a.TY - 1) * s + 2 * dl + 1, TIW = (a.TX - 1) * s + 2 * dl + 1;
   const int in_px = TIH * TIW;
   const int in_groups = (in_px + 15) / 16;
-  bf16* X = reinterpret_cast<bf16*>(smem);
-  bf16* E = X + (size_t)in_groups * 16 * XS;
+  bf16* X = reinterpret_cast<bf16*>(smem);  // EXPAND only
+  f16* E = reinterpret_cast<f16*>(smem + (EXPAND ? (size_t)in_groups * 16 * XS * sizeof(bf16) : 0));
 
   const int ntile = a.tiles_y * a.tiles_x;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring tiles share halos: same XCD L2
@@ -256,19 +264,32 @@ __global__ __launch_bounds__(256) void fused_ir_tile_kernel(IRTArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int r16 = lane & 15, kq = lane >> 4;
 
-  constexpr int cpp = CinP / 8;
-  for (int i = tid; i < in_groups * 16 * cpp; i += 256) {
-    const int ip = i / cpp, c = (i % cpp) * 8;
-    const int ty = ip / TIW, tx = ip - ty * TIW;
-    const int iy = iy0 + ty, ix = ix0 + tx;
-    bf16x8 v = zero8();
-    if (ip < in_px && c < a.Cin && iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW)
-      v = ld8(a.in + (((long long)b * a.IH + iy) * a.IW + ix) * a.Cin + c);
-    st8(X + (size_t)ip * XS + c, v);
+  if (EXPAND) {
+    constexpr int cpp = CinP / 8;
+    for (int i = tid; i < in_groups * 16 * cpp; i += 256) {
+      const int ip = i / cpp, c = (i % cpp) * 8;
+      const int ty = ip / TIW, tx = ip - ty * TIW;
+      const int iy = iy0 + ty, ix = ix0 + tx;
+      bf16x8 v = zero8();
+      if (ip < in_px && c < a.Cin && iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW)
+        v = ld8(a.in + (((long long)b * a.IH + iy) * a.IW + ix) * a.Cin + c);
+      st8(X + (size_t)ip * XS + c, v);
+    }
+  } else {  // depthwise straight on the input: stage it as fp16 (hidP == CinP == 32)
+    for (int i = tid; i < in_groups * 16 * 4; i += 256) {
+      const int ip = i >> 2, c = (i & 3) * 8;
+      const int ty = ip / TIW, tx = ip - ty * TIW;
+      const int iy = iy0 + ty, ix = ix0 + tx;
+      f16x8 h = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (ip < in_px && c < a.Cin && iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW) {
+        const bf16x8 v = ld8(a.in + (((long long)b * a.IH + iy) * a.IW + ix) * a.Cin + c);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) h[q] = (f16)(float)v[q];
+      }
+      *reinterpret_cast<f16x8*>(E + (size_t)ip * ES + c) = h;
+    }
   }
 
-  // this lane's output pixel in each of its groups; pofs = LDS pixel of the
-  // receptive field's top-left tap
   int pofs[GPW], oyv[GPW], oxv[GPW];
   bool pval[GPW];
 #pragma unroll
@@ -287,19 +308,29 @@ __global__ __launch_bounds__(256) void fused_ir_tile_kernel(IRTArgs a) {
   for (int g = 0; g < GPW; ++g)
 #pragma unroll
     for (int n = 0; n < NSUB; ++n) acc[g][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const f16x8 h0 = {0, 0, 0, 0, 0, 0, 0, 0}, h6 = {6, 6, 6, 6, 6, 6, 6, 6};
 
   for (int c0 = 0; c0 < a.hidP; c0 += 32) {
-    // ---- expand chunk over the whole halo tile -> E
-    {
+    // this chunk's depthwise / projection weights: issued first, in flight under the expansion
+    f16x8 wdv[9];
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+      wdv[tap] = *reinterpret_cast<const f16x8*>(a.wd + tap * a.hidP + c0 + kq * 8);
+    const f16x8 bdv = *reinterpret_cast<const f16x8*>(a.bd + c0 + kq * 8);
+    f16x8 af[NSUB];
+#pragma unroll
+    for (int n = 0; n < NSUB; ++n)
+      af[n] = *reinterpret_cast<const f16x8*>(a.wp + (size_t)(n * 16 + r16) * a.hidP + c0 + kq * 8);
+
+    if (EXPAND) {
       bf16x8 wfr[2][KS];
-      float bias[2][4];
+      f32x4 bias[2];
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
         const bf16* wrow = a.we + (size_t)(c0 + sub * 16 + r16) * CinP;
 #pragma unroll
         for (int k = 0; k < KS; ++k) wfr[sub][k] = ld8(wrow + k * 32 + kq * 8);
-        const float4 bv = *reinterpret_cast<const float4*>(a.be + c0 + sub * 16 + kq * 4);
-        bias[sub][0] = bv.x; bias[sub][1] = bv.y; bias[sub][2] = bv.z; bias[sub][3] = bv.w;
+        bias[sub] = *reinterpret_cast<const f32x4*>(a.be + c0 + sub * 16 + kq * 4);
       }
       for (int gi = wid; gi < in_groups; gi += 4) {
         const int ip = gi * 16 + r16;
@@ -311,62 +342,44 @@ __global__ __launch_bounds__(256) void fused_ir_tile_kernel(IRTArgs a) {
         for (int k = 0; k < KS; ++k) xf[k] = ld8(X + (size_t)ip * XS + k * 32 + kq * 8);
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub) {
-          f32x4 e = {0.f, 0.f, 0.f, 0.f};
+          f32x4 e = bias[sub];
 #pragma unroll
           for (int k = 0; k < KS; ++k)
             e = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[sub][k], xf[k], e, 0, 0, 0);
-          bf16x4 o;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float v = fminf(fmaxf(e[q] + bias[sub][q], 0.f), 6.f);
-            o[q] = (bf16)(inside ? v : 0.f);
-          }
-          *reinterpret_cast<bf16x4*>(E + (size_t)ip * ES + sub * 16 + kq * 4) = o;
+          f16x4 o = {(f16)e[0], (f16)e[1], (f16)e[2], (f16)e[3]};
+          o = __builtin_elementwise_min(__builtin_elementwise_max(o, h0.lo), h6.lo);
+          if (!inside) o = h0.lo;  // zero padding applies to the expanded tensor
+          *reinterpret_cast<f16x4*>(E + (size_t)ip * ES + sub * 16 + kq * 4) = o;
         }
       }
+      __syncthreads();
     }
-    __syncthreads();
 
-    // ---- depthwise: lane -> 8 channels (kq*8..) of its pixel in each group
-    const float4 b0 = *reinterpret_cast<const float4*>(a.bd + c0 + kq * 8);
-    const float4 b1 = *reinterpret_cast<const float4*>(a.bd + c0 + kq * 8 + 4);
-    float d[GPW][8];
+    // ---- depthwise (packed fp16): lane -> 8 channels (kq*8..) of its pixel in each group
+    f16x8 d[GPW];
 #pragma unroll
-    for (int g = 0; g < GPW; ++g) {
-      d[g][0] = b0.x; d[g][1] = b0.y; d[g][2] = b0.z; d[g][3] = b0.w;
-      d[g][4] = b1.x; d[g][5] = b1.y; d[g][6] = b1.z; d[g][7] = b1.w;
-    }
+    for (int g = 0; g < GPW; ++g) d[g] = bdv;
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
-        const int tap = ky * 3 + kx;
-        const float4 w0 = *reinterpret_cast<const float4*>(a.wd + tap * a.hidP + c0 + kq * 8);
-        const float4 w1 = *reinterpret_cast<const float4*>(a.wd + tap * a.hidP + c0 + kq * 8 + 4);
-        const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
         const int toff = (ky * TIW + kx) * dl;
 #pragma unroll
         for (int g = 0; g < GPW; ++g) {
-          const bf16x8 v = ld8(E + (size_t)(pofs[g] + toff) * ES + kq * 8);
-#pragma unroll
-          for (int q = 0; q < 8; ++q) d[g][q] += (float)v[q] * wv[q];
+          const f16x8 v = *reinterpret_cast<const f16x8*>(E + (size_t)(pofs[g] + toff) * ES + kq * 8);
+          d[g] = v * wdv[ky * 3 + kx] + d[g];
         }
       }
-    bf16x8 dfrag[GPW];
 #pragma unroll
-    for (int g = 0; g < GPW; ++g)
-#pragma unroll
-      for (int q = 0; q < 8; ++q) dfrag[g][q] = (bf16)fminf(fmaxf(d[g][q], 0.f), 6.f);
+    for (int g = 0; g < GPW; ++g) d[g] = __builtin_elementwise_min(__builtin_elementwise_max(d[g], h0), h6);
 
-    // ---- project chunk
+    // ---- project chunk (fp16 MFMA, fp32 accumulate)
 #pragma unroll
-    for (int n = 0; n < NSUB; ++n) {
-      const bf16x8 af = ld8(a.wp + (size_t)(n * 16 + r16) * a.hidP + c0 + kq * 8);
+    for (int n = 0; n < NSUB; ++n)
 #pragma unroll
       for (int g = 0; g < GPW; ++g)
-        acc[g][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, dfrag[g], acc[g][n], 0, 0, 0);
-    }
-    __syncthreads();  // E is rewritten by the next chunk
+        acc[g][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[n], d[g], acc[g][n], 0, 0, 0);
+    if (EXPAND) __syncthreads();  // E is rewritten by the next chunk
   }
 
 #pragma unroll
@@ -382,7 +395,7 @@ __global__ __launch_bounds__(256) void fused_ir_tile_kernel(IRTArgs a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         v[q] = acc[g][n][q] + a.bp[co + q];
-        if (a.residual) v[q] += (float)rp[co + q];
+        if (EXPAND && a.residual) v[q] += (float)rp[co + q];
       }
       if (co + 3 < a.Cout && (a.Cout & 3) == 0) {
         bf16x4 o;
@@ -397,43 +410,55 @@ __global__ __launch_bounds__(256) void fused_ir_tile_kernel(IRTArgs a) {
   }
 }
 
-size_t tile_lds_bytes(int CinP, int stride, int dil, int TY, int TX) {
+size_t tile_lds_bytes(int CinP, int stride, int dil, int TY, int TX, bool expand = true) {
   const int in_px = ((TY - 1) * stride + 2 * dil + 1) * ((TX - 1) * stride + 2 * dil + 1);
-  return (size_t)((in_px + 15) / 16) * 16 * (CinP + 8 + 40) * sizeof(bf16);
+  return (size_t)((in_px + 15) / 16) * 16 * ((expand ? CinP + 8 : 0) + 40) * 2;
 }
 
-template <int NSUB, int KS, int GPW>
+template <int NSUB, int KS, int GPW, bool EX>
 void launch_ir_tile(const IRTArgs& a, size_t lds, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
-    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_ir_tile_kernel<NSUB, KS, GPW>),
+    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_ir_tile_kernel<NSUB, KS, GPW, EX>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
           "fused_ir_tile attr");
     attr_set = true;
   }
   const int grid = a.B * a.tiles_y * a.tiles_x;
-  hipLaunchKernelGGL((fused_ir_tile_kernel<NSUB, KS, GPW>), dim3(grid), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((fused_ir_tile_kernel<NSUB, KS, GPW, EX>), dim3(grid), dim3(256), lds, st, a);
   check_launch("fused_ir_tile");
 }
 
 void fused_ir_tile(const FusedIRParams& p, hipStream_t st) {
-  if (!p.we) throw std::invalid_argument("fused_ir_tile: needs an expansion layer");
+  if (!p.wd_h || !p.bd_h || !p.wp_h) throw std::invalid_argument("fused_ir_tile: needs the fp16 weights");
   if (p.dil < 1 || p.TX < 1 || p.TY < 1) throw std::invalid_argument("fused_ir_tile: bad tile");
   if (p.Cin % 8 || p.hidP % 32 || p.CinP % 32 || p.CinP < p.Cin)
     throw std::invalid_argument("fused_ir_tile: bad channel padding");
+  const bool ex = p.we != nullptr;
+  if (!ex && (p.CinP != 32 || p.hidP != 32 || p.residual))
+    throw std::invalid_argument("fused_ir_tile: no-expansion blocks need Cin <= 32 and no residual");
   if (p.residual && (p.stride != 1 || p.Cin != p.Cout)) throw std::invalid_argument("fused_ir_tile: bad residual");
   const int groups = (p.TY * p.TX + 15) / 16;
   const int gpw = (groups + 3) / 4;
-  const size_t lds = tile_lds_bytes(p.CinP, p.stride, p.dil, p.TY, p.TX);
+  const size_t lds = tile_lds_bytes(p.CinP, p.stride, p.dil, p.TY, p.TX, ex);
   if (gpw > 2 || lds > 160 * 1024) throw std::invalid_argument("fused_ir_tile: tile too large");
-  IRTArgs a{p.in, p.we, p.be, p.wd, p.bd, p.wp, p.bp, p.out, p.B, p.IH, p.IW, p.Cin, p.hidP,
+  IRTArgs a{p.in, p.we, p.be, reinterpret_cast<const f16*>(p.wd_h), reinterpret_cast<const f16*>(p.bd_h),
+            reinterpret_cast<const f16*>(p.wp_h), p.bp, p.out, p.B, p.IH, p.IW, p.Cin, p.hidP,
             p.Cout, p.OH, p.OW, p.stride, p.dil, p.residual, p.TY, p.TX,
             cdiv(p.OH, p.TY), cdiv(p.OW, p.TX)};
   const int nsub = (p.Cout + 15) / 16, ks = p.CinP / 32;
+  if (!ex) {
+    if (nsub == 1) {
+      if (gpw == 1) launch_ir_tile<1, 1, 1, false>(a, lds, st);
+      else launch_ir_tile<1, 1, 2, false>(a, lds, st);
+      return;
+    }
+    throw std::invalid_argument("fused_ir_tile: unsupported no-expansion Cout");
+  }
 #define IRT(N, K)                                                        \
   if (nsub == N && ks == K) {                                            \
-    if (gpw == 1) launch_ir_tile<N, K, 1>(a, lds, st);                   \
-    else launch_ir_tile<N, K, 2>(a, lds, st);                            \
+    if (gpw == 1) launch_ir_tile<N, K, 1, true>(a, lds, st);             \
+    else launch_ir_tile<N, K, 2, true>(a, lds, st);                      \
     return;                                                              \
   }
   IRT(4, 2) IRT(6, 2) IRT(6, 3) IRT(10, 3) IRT(10, 5) IRT(20, 5) IRT(4, 1) IRT(2, 1)
@@ -443,8 +468,8 @@ void fused_ir_tile(const FusedIRParams& p, hipStream_t st) {
 
 }  // namespace
 
-size_t fused_ir_tile_lds(int CinP, int stride, int dil, int TY, int TX) {
-  return tile_lds_bytes(CinP, stride, dil, TY, TX);
+size_t fused_ir_tile_lds(int CinP, int stride, int dil, int TY, int TX, int expand) {
+  return tile_lds_bytes(CinP, stride, dil, TY, TX, expand != 0);
 }
 
 void fused_inverted_residual(const FusedIRParams& p, hipStream_t st) {

@@ -19,7 +19,7 @@ struct ConvParams {
   int B = 0, IH = 0, IW = 0, Cin = 0, OH = 0, OW = 0, Cout = 0;
   int KH = 1, KW = 1, stride = 1, dil = 1;
   int ldo = 0, co_off = 0, ldr = 0, act = 0;
-  int variant = 0;  // 0 auto, 1 direct (register-fed), 2 LDS-staged
+  int variant = 0;  // 0 auto, 1 direct (register-fed), 2 LDS-staged, 3/4 LDS-DMA 3/2-stage
 };
 void conv_gemm(const ConvParams& p, hipStream_t s);
 
@@ -63,10 +63,15 @@ struct FusedIRParams {
   int stride = 1, residual = 0;
   int dil = 1;         // tile kernel only
   int TY = 0, TX = 0;  // > 0: general 2-D tile kernel (any dilation, CinP <= 160, CoutP <= 320)
+  // tile kernel: fp16 copies of the depthwise weights [9, hidP], bias [hidP] and
+  // projection weights [CoutP, hidP]
+  const void* wd_h = nullptr;
+  const void* bd_h = nullptr;
+  const void* wp_h = nullptr;
 };
 void fused_inverted_residual(const FusedIRParams& p, hipStream_t s);
 // LDS bytes the tile kernel needs for a (TY, TX) tile (0 if the shape is unsupported).
-size_t fused_ir_tile_lds(int CinP, int stride, int dil, int TY, int TX);
+size_t fused_ir_tile_lds(int CinP, int stride, int dil, int TY, int TX, int expand);
 
 // Depthwise 3x3 (+bias, ReLU6) fused with the 1x1 projection (+bias [+ residual]):
 // the depthwise output stays in registers as the projection's MFMA operand.

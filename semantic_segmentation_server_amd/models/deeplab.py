@@ -73,11 +73,16 @@ class DeepLabV3(nn.Module):
 
 def build_model(arch: str = "mnv2", num_classes: int = 21, width_mult: float = 1.0,
                 output_stride: int = 16, aspp: str = "full", seed: int = 0,
-                calibrate_hw: Optional[int] = 129, multi_grid=(1, 2, 4)) -> DeepLabV3:
+                calibrate_hw: Optional[int] = 129, multi_grid=(1, 2, 4),
+                scene_prior: bool = True, calib_input: Optional[torch.Tensor] = None,
+                calib_device: Optional[torch.device] = None) -> DeepLabV3:
     """Random-init DeepLabv3 of the named architecture.
 
     ``calibrate_hw``: side of the synthetic batch used to set BN statistics
-    (None to skip). Calibration is deterministic for a given seed.
+    (None to skip); ``calib_input`` (normalised NCHW) replaces that batch, e.g.
+    letterboxed camera frames at the deployment resolution: BN statistics and the
+    logits prior calibrated on tiny maps do not transfer to 33x33 ones.
+    Calibration is deterministic for a given seed.
     """
     if arch == "mnv2":
         bb = MobileNetV2Backbone(width_mult, output_stride)
@@ -87,11 +92,61 @@ def build_model(arch: str = "mnv2", num_classes: int = 21, width_mult: float = 1
         raise ValueError(f"unknown arch {arch!r}")
     model = DeepLabV3(bb, num_classes, aspp)
     init_random(model, seed)
-    if calibrate_hw:
-        g = torch.Generator().manual_seed(seed + 1)
-        x = synthetic_normalized(2, calibrate_hw, calibrate_hw, g)
+    if calibrate_hw or calib_input is not None:
+        if calib_input is not None:
+            x = calib_input
+        else:
+            g = torch.Generator().manual_seed(seed + 1)
+            x = synthetic_normalized(2, calibrate_hw, calibrate_hw, g)
+        if calib_device is not None:  # fp32 calibration forwards on the GPU, weights back on the host
+            model.to(calib_device)
+            x = x.to(calib_device)
         calibrate_bn(model, x)
+        if scene_prior:
+            calibrate_logits(model, x, scene_class_prior(num_classes).to(x.device))
+        model.cpu()
     return model.eval()
+
+
+def scene_class_prior(num_classes: int) -> torch.Tensor:
+    """Target pixel share per class for the random-init model's label maps.
+
+    A random-init network collapses to one or two classes (>99 % of pixels), so
+    the mask/contour stage would see an empty mask and the benchmark would skip
+    the work a deployed server does. The prior makes the classes that survive
+    the reference's palette->gray>127 mask (``sem_seg_server.py:77-85``; PASCAL:
+    car, person) cover ~35 % of the pixels, background 30 %, the rest evenly.
+    """
+    from ..labels import GRAY_SHIFT, GRAY_W_B, GRAY_W_G, GRAY_W_R, colormap_for
+    cmap = colormap_for("pascal" if num_classes == 21 else "cityscapes")[:num_classes]
+    gray = (cmap[:, 0] * GRAY_W_B + cmap[:, 1] * GRAY_W_G + cmap[:, 2] * GRAY_W_R
+            + (1 << (GRAY_SHIFT - 1))) >> GRAY_SHIFT
+    fg = torch.as_tensor(gray > 127)
+    prior = torch.zeros(num_classes)
+    prior[fg] = 0.35 / max(int(fg.sum()), 1)
+    rest = ~fg
+    rest[0] = False
+    prior[rest] = 0.35 / max(int(rest.sum()), 1)
+    prior[0] += 0.30
+    return prior / prior.sum()
+
+
+@torch.no_grad()
+def calibrate_logits(model: "DeepLabV3", x: torch.Tensor, prior: torch.Tensor,
+                     iters: int = 40) -> None:
+    """Shift the logits-layer bias until the argmax class shares match ``prior``
+    (fixed-point iteration b += 0.5 * log(prior / share) on cached features)."""
+    was_training = model.training
+    model.eval()
+    feats = model.aspp(model.backbone(x))
+    H, W = x.shape[-2:]
+    bias = model.logits.conv.bias
+    for _ in range(iters):
+        up = F.interpolate(model.logits(feats), size=(H, W), mode="bilinear", align_corners=True)
+        share = torch.bincount(up.argmax(1).flatten(), minlength=model.num_classes).float()
+        share = share / share.sum()
+        bias += 0.5 * (torch.log(prior + 1e-6) - torch.log(share + 1e-3)).clamp(-2, 2)
+    model.train(was_training)
 
 
 def synthetic_normalized(n: int, h: int, w: int, g: Optional[torch.Generator] = None) -> torch.Tensor:

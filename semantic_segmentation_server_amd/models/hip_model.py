@@ -51,12 +51,13 @@ def _pack_dw(layer: ConvBNAct, dev) -> Tuple[torch.Tensor, torch.Tensor]:
 _TILES = [(8, 16), (4, 16), (11, 11), (5, 11), (8, 13), (5, 13)]
 
 
-def _tile_candidates(OH: int, OW: int, CinP: int, stride: int, dil: int) -> List[Tuple[int, int]]:
+def _tile_candidates(OH: int, OW: int, CinP: int, stride: int, dil: int,
+                     expand: bool = True) -> List[Tuple[int, int]]:
     """2-D output tiles for the general fused-IR kernel: at most 8 MFMA pixel groups,
     LDS within one CU's 160 KB, and at most 25 % of the tiled area wasted."""
     out = []
     for ty, tx in _TILES:
-        if -(-ty * tx // 16) > 8 or K.fused_ir_tile_lds(CinP, stride, dil, ty, tx) > 160 * 1024:
+        if -(-ty * tx // 16) > 8 or K.fused_ir_tile_lds(CinP, stride, dil, ty, tx, expand) > 160 * 1024:
             continue
         covered = -(-OH // ty) * ty * -(-OW // tx) * tx
         if covered <= 1.25 * OH * OW:
@@ -131,8 +132,10 @@ class HipDeepLab:
                     dw=_pack_dw(blk.dw, dev),
                     project=_pack_dense(blk.project, dev))
                 row_ok = s.dilation == 1 and s.cin <= 64 and s.cout <= 96 and s.cin % 8 == 0
-                tile_ok = (blk.expand is not None and s.cin % 8 == 0 and
-                           (-(-s.cout // 16), -(-s.cin // 32)) in K.FUSED_TILE_SHAPES)
+                shape = (-(-s.cout // 16), -(-s.cin // 32))
+                tile_ok = s.cin % 8 == 0 and (
+                    shape in K.FUSED_TILE_SHAPES if blk.expand is not None
+                    else shape in K.FUSED_TILE_SHAPES_NOEXP and not s.residual)
                 if row_ok or tile_ok:
                     ew = eb = None
                     if blk.expand is not None:
@@ -311,7 +314,8 @@ class HipDeepLab:
                 stride=s.stride, dil=s.dilation, res=res)]))
         if "fused_tile" in blk:
             fp = blk["fused_tile"]
-            for tile in _tile_candidates(OH, OW, fp["CinP"], s.stride, s.dilation):
+            for tile in _tile_candidates(OH, OW, fp["CinP"], s.stride, s.dilation,
+                                         fp["we"] is not None):
                 variants.insert(0, (f"tile{tile[0]}x{tile[1]}", [
                     lambda *_, x=inp, out=out, h=h, w=w, OH=OH, OW=OW, tile=tile: K.fused_ir(
                         x, fp, out, B=B, IH=h, IW=w, OH=OH, OW=OW, tile=tile)]))

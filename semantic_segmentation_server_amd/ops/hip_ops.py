@@ -62,7 +62,7 @@ def conv_gemm(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out: torch.T
               stride: int = 1, dil: int = 1, ldo: Optional[int] = None, co_off: int = 0,
               act=None, res: Optional[torch.Tensor] = None, ldr: Optional[int] = None,
               img_bias: Optional[torch.Tensor] = None, variant: int = 0) -> torch.Tensor:
-    """NHWC implicit-GEMM conv (variant: 0 auto, 1 register-fed, 2 LDS-staged). x: [B,IH,IW,Cin] bf16; w: [Cout,k,k,Cin] bf16;
+    """NHWC implicit-GEMM conv (variant: 0 auto, 1 register-fed, 2 LDS-staged, 3/4 LDS-DMA 3/2-stage). x: [B,IH,IW,Cin] bf16; w: [Cout,k,k,Cin] bf16;
     out: [B,OH,OW,ldo] bf16 written at channel offset co_off."""
     ldo = Cout if ldo is None else ldo
     ldr = Cout if ldr is None else ldr
@@ -106,7 +106,7 @@ def fused_ir(x, packed: dict, out, *, B, IH, IW, OH, OW, tile=None):
     _hip_mod().fused_ir(_ptr(x), _ptr(P["we"]), _ptr(P["be"]), _ptr(P["wd"]), _ptr(P["bd"]),
                         _ptr(P["wp"]), _ptr(P["bp"]), _ptr(out), B, IH, IW, P["Cin"], P["CinP"],
                         P["hidP"], P["Cout"], OH, OW, P["stride"], int(P["residual"]), _stream(),
-                        P.get("dil", 1), TY, TX)
+                        P.get("dil", 1), TY, TX, _ptr(P["wd_h"]), _ptr(P["bd_h"]), _ptr(P["wp_h"]))
     _dbg('fused_ir')
     return out
 
@@ -141,12 +141,14 @@ def pack_project_padded(wp, bp, Cout, hid, device):
     return w.to(torch.bfloat16).contiguous(), b
 
 
-# (Cout/16, CinP/32) shapes the tile kernel is instantiated for (fused_ir.hip)
+# (Cout/16, CinP/32) shapes the tile kernel is instantiated for (fused_ir.hip);
+# blocks without expansion: Cout <= 16 and Cin <= 32
 FUSED_TILE_SHAPES = {(4, 2), (6, 2), (6, 3), (10, 3), (10, 5), (20, 5), (4, 1), (2, 1)}
+FUSED_TILE_SHAPES_NOEXP = {(1, 1)}
 
 
-def fused_ir_tile_lds(CinP, stride, dil, TY, TX) -> int:
-    return int(_hip_mod().fused_ir_tile_lds(CinP, stride, dil, TY, TX))
+def fused_ir_tile_lds(CinP, stride, dil, TY, TX, expand=True) -> int:
+    return int(_hip_mod().fused_ir_tile_lds(CinP, stride, dil, TY, TX, int(expand)))
 
 
 def pack_fused_ir(we, be, wd, bd, wp, bp, *, Cin, hid, Cout, stride, residual, device,
@@ -179,6 +181,9 @@ def pack_fused_ir(we, be, wd, bd, wp, bp, *, Cin, hid, Cout, stride, residual, d
     t = torch.zeros(CoutP, hidP, **f32)
     t[:Cout, :hid] = wp
     out["wp"] = t.to(torch.bfloat16).contiguous()
+    out["wp_h"] = t.to(torch.float16).contiguous()  # tile kernel: fp16 internals
+    out["wd_h"] = out["wd"].to(torch.float16).contiguous()
+    out["bd_h"] = out["bd"].to(torch.float16).contiguous()
     b = torch.zeros(CoutP, **f32)
     b[:Cout] = bp
     out["bp"] = b

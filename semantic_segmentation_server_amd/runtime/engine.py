@@ -42,6 +42,17 @@ log = logging.getLogger(__name__)
 DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32, "int8": torch.bfloat16}
 
 
+def calibration_frames(H: int, W: int, n: int = 2, seed: int = 0) -> torch.Tensor:
+    """Letterboxed synthetic camera frames at the model resolution, normalised:
+    the calibration batch for random-init weights (BN statistics + class prior),
+    drawn from the same distribution the synthetic source serves."""
+    from .sources import SyntheticSource
+    src = SyntheticSource(640, 480, seed=seed + 101, pool=n)
+    frames = torch.from_numpy(np.stack([next(src).image for _ in range(n)]).copy())
+    lx, ly, *_ = R.letterbox_luts(640, 480, W, H)
+    return R.preprocess(frames, torch.from_numpy(lx), torch.from_numpy(ly))
+
+
 def _per_frame(streams, n: int) -> List[int]:
     if isinstance(streams, (int, np.integer)):
         return [int(streams)] * n
@@ -64,8 +75,12 @@ class Engine:
         self.H = self.W = int(cfg.input_size)
         self.min_area = cfg.min_area
         self.palette = np.ascontiguousarray(colormap_for(cfg.dataset), np.int32)
-        self.model = model if model is not None else build_model(
-            cfg.arch, cfg.num_classes, cfg.width_mult, cfg.output_stride, cfg.aspp, cfg.seed)
+        if model is None:
+            calib = None if cfg.model else calibration_frames(self.H, self.W, seed=cfg.seed)
+            model = build_model(cfg.arch, cfg.num_classes, cfg.width_mult, cfg.output_stride,
+                                cfg.aspp, cfg.seed, calib_input=calib,
+                                calib_device=self.device if self.is_cuda else None)
+        self.model = model
         if cfg.model:
             self._load_weights(cfg.model)
         self.model.eval()

@@ -50,7 +50,7 @@ def _nchw(x):
     (2, 65, 65, 144, 32, 1, 1, 1, None, False, 0, 0),
     (1, 33, 33, 1024, 256, 1, 1, 1, "relu", False, 0, 0),
 ])
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4])
 def test_conv_gemm(B, H, W, Cin, Cout, k, stride, dil, act, res, ldo_pad, co_off, variant):
     K = _hip()
     g = torch.Generator(device="cpu").manual_seed(1)
@@ -339,12 +339,13 @@ def test_fused_inverted_residual(cin, cout, t, stride, H):
     (160, 160, 1, 2, 29, (8, 16)),   # partial tiles at the right/bottom edge
     (24, 32, 2, 1, 65, (8, 16)),     # stride 2, CinP 32
     (32, 64, 2, 1, 65, (5, 11)),
+    (32, 16, 1, 1, 37, (8, 16)),     # block 0: no expansion (t = 1)
 ])
 def test_fused_ir_tile(cin, cout, stride, dil, H, tile):
     from semantic_segmentation_server_amd.models.layers import init_random
     from semantic_segmentation_server_amd.models.mobilenetv2 import InvertedResidual, IRSpec
     K = _hip()
-    spec = IRSpec(cin, cout, 6, stride, dil)
+    spec = IRSpec(cin, cout, 1 if cout == 16 else 6, stride, dil)
     blk = InvertedResidual(spec)
     init_random(blk, seed=cin + 3 * cout + dil)
     for m in blk.modules():
@@ -358,10 +359,13 @@ def test_fused_ir_tile(cin, cout, stride, dil, H, tile):
     with torch.no_grad():
         ref = blk(x.float())
     OH, OW = ref.shape[-2:]
-    ew, eb = blk.expand.fold()
+    ew = eb = None
+    if blk.expand is not None:
+        ew, eb = blk.expand.fold()
+        ew = ew[:, :, 0, 0]
     dwf, dbf = blk.dw.fold()
     pwf, pbf = blk.project.fold()
-    packed = K.pack_fused_ir(ew[:, :, 0, 0], eb, dwf[:, 0], dbf, pwf[:, :, 0, 0], pbf, Cin=cin,
+    packed = K.pack_fused_ir(ew, eb, dwf[:, 0], dbf, pwf[:, :, 0, 0], pbf, Cin=cin,
                              hid=spec.hidden, Cout=cout, stride=stride, residual=spec.residual,
                              device=DEV, dil=dil)
     out = torch.full((B, OH, OW, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
