@@ -606,16 +606,20 @@ void conv_gemm(const ConvParams& p, hipStream_t s) {
   const long long M = (long long)p.B * p.OH * p.OW;
   const long long tiles = (M + 127) / 128 * cdiv(p.Cout, 32 * pick_nt(p.Cout));
   const long long K = (long long)p.KH * p.KW * p.Cin;
-  if (p.variant == 3 || p.variant == 4) {
-    // int32 offsets inside the kernel
-    if ((long long)p.B * p.IH * p.IW * p.Cin >= (1LL << 31) || (long long)p.Cout * K >= (1LL << 31))
-      throw std::invalid_argument("conv_gemm glds: tensor too large for 32-bit offsets");
-    if (p.KH * p.KW > 16) throw std::invalid_argument("conv_gemm glds: at most 16 taps");
-    if (p.variant == 3) dispatch_glds<3>(a, s);
+  // auto: LDS-DMA 2-stage for deep K on grids that fill the chip (scripts/bench_conv.py
+  // on MI355X: 1.2-1.9x the register-staged LDS kernel from K = 256 up; shallow-K
+  // layers are output-write-bound and stay on the register-fed kernel)
+  const bool glds_ok = (long long)p.B * p.IH * p.IW * p.Cin < (1LL << 31) &&
+                       (long long)p.Cout * K < (1LL << 31) && p.KH * p.KW <= 16;  // int32 offsets, tap list
+  int variant = p.variant;
+  if (variant == 0) variant = (tiles >= 128 && K >= 256) ? (glds_ok ? 4 : 2) : 1;
+  if (variant == 3 || variant == 4) {
+    if (!glds_ok) throw std::invalid_argument("conv_gemm glds: tensor too large for 32-bit offsets or > 16 taps");
+    if (variant == 3) dispatch_glds<3>(a, s);
     else dispatch_glds<2>(a, s);
     return;
   }
-  if (p.variant == 2 || (p.variant == 0 && tiles >= 256 && K >= 512)) {
+  if (variant == 2) {
     // LDS-staged MFMA path: deep K (ASPP atrous 2880, projections 576-1024) and
     // enough 128-pixel tiles to fill the chip. Shallow-K layers are write-bound
     // and measured faster on the register-fed kernel (rocprof, B=32 MNv2).

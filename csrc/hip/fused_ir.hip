@@ -244,8 +244,9 @@ struct IRTArgs {
   int B, IH, IW, Cin, hidP, Cout, OH, OW, stride, dil, residual, TY, TX, tiles_y, tiles_x;
 };
 
-template <int NSUB, int KS, int GPW, bool EXPAND>
-__global__ __launch_bounds__(256) void fused_ir_tile_kernel(IRTArgs a) {
+template <int NSUB, int KS, int GPW, bool EXPAND, int NW>
+__global__ __launch_bounds__(64 * NW) void fused_ir_tile_kernel(IRTArgs a) {
+  constexpr int NT = 64 * NW;  // threads
   constexpr int CinP = KS * 32;
   constexpr int XS = CinP + 8, ES = 32 + 8;  // +16 B per LDS row: conflict-free ds_read_b128
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -266,7 +267,7 @@ __global__ __launch_bounds__(256) void fused_ir_tile_kernel(IRTArgs a) {
 
   if (EXPAND) {
     constexpr int cpp = CinP / 8;
-    for (int i = tid; i < in_groups * 16 * cpp; i += 256) {
+    for (int i = tid; i < in_groups * 16 * cpp; i += NT) {
       const int ip = i / cpp, c = (i % cpp) * 8;
       const int ty = ip / TIW, tx = ip - ty * TIW;
       const int iy = iy0 + ty, ix = ix0 + tx;
@@ -276,7 +277,7 @@ __global__ __launch_bounds__(256) void fused_ir_tile_kernel(IRTArgs a) {
       st8(X + (size_t)ip * XS + c, v);
     }
   } else {  // depthwise straight on the input: stage it as fp16 (hidP == CinP == 32)
-    for (int i = tid; i < in_groups * 16 * 4; i += 256) {
+    for (int i = tid; i < in_groups * 16 * 4; i += NT) {
       const int ip = i >> 2, c = (i & 3) * 8;
       const int ty = ip / TIW, tx = ip - ty * TIW;
       const int iy = iy0 + ty, ix = ix0 + tx;
@@ -332,7 +333,7 @@ __global__ __launch_bounds__(256) void fused_ir_tile_kernel(IRTArgs a) {
         for (int k = 0; k < KS; ++k) wfr[sub][k] = ld8(wrow + k * 32 + kq * 8);
         bias[sub] = *reinterpret_cast<const f32x4*>(a.be + c0 + sub * 16 + kq * 4);
       }
-      for (int gi = wid; gi < in_groups; gi += 4) {
+      for (int gi = wid; gi < in_groups; gi += NW) {
         const int ip = gi * 16 + r16;
         const int ty = ip / TIW, tx = ip - ty * TIW;
         const int iy = iy0 + ty, ix = ix0 + tx;
@@ -359,17 +360,19 @@ __global__ __launch_bounds__(256) void fused_ir_tile_kernel(IRTArgs a) {
     f16x8 d[GPW];
 #pragma unroll
     for (int g = 0; g < GPW; ++g) d[g] = bdv;
+    // all taps' LDS reads first, then the FMAs: with one or two waves per SIMD a
+    // read-use-read chain exposes the LDS latency on every tap
+    f16x8 v[GPW][9];
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
+    for (int g = 0; g < GPW; ++g)
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int toff = (ky * TIW + kx) * dl;
+      for (int tap = 0; tap < 9; ++tap)
+        v[g][tap] = *reinterpret_cast<const f16x8*>(
+            E + (size_t)(pofs[g] + ((tap / 3) * TIW + tap % 3) * dl) * ES + kq * 8);
 #pragma unroll
-        for (int g = 0; g < GPW; ++g) {
-          const f16x8 v = *reinterpret_cast<const f16x8*>(E + (size_t)(pofs[g] + toff) * ES + kq * 8);
-          d[g] = v * wdv[ky * 3 + kx] + d[g];
-        }
-      }
+    for (int g = 0; g < GPW; ++g)
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) d[g] = v[g][tap] * wdv[tap] + d[g];
 #pragma unroll
     for (int g = 0; g < GPW; ++g) d[g] = __builtin_elementwise_min(__builtin_elementwise_max(d[g], h0), h6);
 
@@ -415,18 +418,26 @@ size_t tile_lds_bytes(int CinP, int stride, int dil, int TY, int TX, bool expand
   return (size_t)((in_px + 15) / 16) * 16 * ((expand ? CinP + 8 : 0) + 40) * 2;
 }
 
-template <int NSUB, int KS, int GPW, bool EX>
-void launch_ir_tile(const IRTArgs& a, size_t lds, hipStream_t st) {
+template <int NSUB, int KS, int GPW, bool EX, int NW>
+void launch_ir_tile_nw(const IRTArgs& a, size_t lds, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
-    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_ir_tile_kernel<NSUB, KS, GPW, EX>),
+    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_ir_tile_kernel<NSUB, KS, GPW, EX, NW>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
           "fused_ir_tile attr");
     attr_set = true;
   }
   const int grid = a.B * a.tiles_y * a.tiles_x;
-  hipLaunchKernelGGL((fused_ir_tile_kernel<NSUB, KS, GPW, EX>), dim3(grid), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((fused_ir_tile_kernel<NSUB, KS, GPW, EX, NW>), dim3(grid), dim3(64 * NW), lds, st, a);
   check_launch("fused_ir_tile");
+}
+
+// groups = ceil(TY*TX / 16) pixel groups: 4 waves x GPW (GPW 1/2)
+template <int NSUB, int KS, bool EX>
+void launch_ir_tile(const IRTArgs& a, int groups, size_t lds, hipStream_t st) {
+  // (8 waves x 1 group measured 1.3-2x slower than 4 x 2 on every 33x33 block)
+  if (groups <= 4) launch_ir_tile_nw<NSUB, KS, 1, EX, 4>(a, lds, st);
+  else launch_ir_tile_nw<NSUB, KS, 2, EX, 4>(a, lds, st);
 }
 
 void fused_ir_tile(const FusedIRParams& p, hipStream_t st) {
@@ -449,16 +460,14 @@ void fused_ir_tile(const FusedIRParams& p, hipStream_t st) {
   const int nsub = (p.Cout + 15) / 16, ks = p.CinP / 32;
   if (!ex) {
     if (nsub == 1) {
-      if (gpw == 1) launch_ir_tile<1, 1, 1, false>(a, lds, st);
-      else launch_ir_tile<1, 1, 2, false>(a, lds, st);
+      launch_ir_tile<1, 1, false>(a, groups, lds, st);
       return;
     }
     throw std::invalid_argument("fused_ir_tile: unsupported no-expansion Cout");
   }
 #define IRT(N, K)                                                        \
   if (nsub == N && ks == K) {                                            \
-    if (gpw == 1) launch_ir_tile<N, K, 1, true>(a, lds, st);             \
-    else launch_ir_tile<N, K, 2, true>(a, lds, st);                      \
+    launch_ir_tile<N, K, true>(a, groups, lds, st);                      \
     return;                                                              \
   }
   IRT(4, 2) IRT(6, 2) IRT(6, 3) IRT(10, 3) IRT(10, 5) IRT(20, 5) IRT(4, 1) IRT(2, 1)

@@ -53,9 +53,92 @@ __global__ __launch_bounds__(256) void dw3x3_kernel(const bf16* __restrict__ in,
   }
 }
 
+// Strip variant: one lane = PX consecutive output pixels of one row x 8 channels,
+// stride / dilation compile-time, so the (PX-1)*S + 2D + 1 input columns of a
+// kernel row are loaded once and shared by the strip's taps (6 loads instead of
+// 12 per row at S1 D1, 9 instead of 12 at S2), weights are loaded once per strip,
+// and all index math is 32-bit (the flat 64-bit div/mod chain above costs more
+// than the arithmetic on the 33x33 maps).
+template <int S, int D, int PX>
+__global__ __launch_bounds__(256) void dw3x3_strip_kernel(const bf16* __restrict__ in,
+                                                          const float* __restrict__ w,
+                                                          const float* __restrict__ bias,
+                                                          bf16* __restrict__ out, int B, int IH,
+                                                          int IW, int C, int OH, int OW, int act) {
+  constexpr int NC = (PX - 1) * S + 2 * D + 1;
+  const int CG = C >> 3;
+  const int SX = (OW + PX - 1) / PX;
+  const int total = B * OH * SX * CG;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int cg = t % CG;
+  int r = t / CG;
+  const int sx = r % SX;
+  r /= SX;
+  const int oy = r % OH, b = r / OH;
+  const int c = cg * 8, ox0 = sx * PX;
+  float acc[PX][8];
+  {
+    const float4 b0 = *reinterpret_cast<const float4*>(bias + c);
+    const float4 b1 = *reinterpret_cast<const float4*>(bias + c + 4);
+#pragma unroll
+    for (int p = 0; p < PX; ++p) {
+      acc[p][0] = b0.x; acc[p][1] = b0.y; acc[p][2] = b0.z; acc[p][3] = b0.w;
+      acc[p][4] = b1.x; acc[p][5] = b1.y; acc[p][6] = b1.z; acc[p][7] = b1.w;
+    }
+  }
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky) {
+    const int iy = oy * S + (ky - 1) * D;
+    if (iy < 0 || iy >= IH) continue;
+    const bf16* row = in + ((size_t)(b * IH + iy) * IW) * C + c;
+    bf16x8 col[NC];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const int ix = ox0 * S - D + j;
+      col[j] = (ix >= 0 && ix < IW) ? ld8(row + (size_t)ix * C) : zero8();
+    }
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const float4 w0 = *reinterpret_cast<const float4*>(w + (ky * 3 + kx) * C + c);
+      const float4 w1 = *reinterpret_cast<const float4*>(w + (ky * 3 + kx) * C + c + 4);
+      const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+      for (int p = 0; p < PX; ++p) {
+        const bf16x8 v = col[p * S + kx * D];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[p][q] += (float)v[q] * wv[q];
+      }
+    }
+  }
+  bf16* op = out + ((size_t)(b * OH + oy) * OW + ox0) * C + c;
+#pragma unroll
+  for (int p = 0; p < PX; ++p) {
+    if (ox0 + p >= OW) break;
+    bf16x8 o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = (bf16)apply_act(acc[p][q], act);
+    st8(op + (size_t)p * C, o);
+  }
+}
+
 void depthwise3x3(const bf16* in, const float* w, const float* bias, bf16* out, int B, int IH,
                   int IW, int C, int OH, int OW, int stride, int dil, int act, hipStream_t s) {
   if (C % 8) throw std::invalid_argument("depthwise3x3: C must be a multiple of 8");
+  constexpr int PX = 4;
+  const long long strip_total = (long long)B * OH * ((OW + PX - 1) / PX) * (C / 8);
+  if (strip_total < (1LL << 31) && (long long)B * IH * IW * C < (1LL << 40)) {
+    const int grid = cdiv(strip_total, 256);
+#define DWS(S_, D_)                                                                              \
+    if (stride == S_ && dil == D_) {                                                             \
+      hipLaunchKernelGGL((dw3x3_strip_kernel<S_, D_, PX>), dim3(grid), dim3(256), 0, s, in, w,   \
+                         bias, out, B, IH, IW, C, OH, OW, act);                                  \
+      check_launch("depthwise3x3 strip");                                                        \
+      return;                                                                                    \
+    }
+    DWS(1, 1) DWS(1, 2) DWS(2, 1) DWS(1, 4)
+#undef DWS
+  }
   const long long total = (long long)B * OH * OW * (C / 8);
   const int grid = (int)std::min<long long>(cdiv(total, 256), 256LL * 32);
   hipLaunchKernelGGL(dw3x3_kernel, dim3(grid), dim3(256), 0, s, in, w, bias, out, B, IH, IW, C,

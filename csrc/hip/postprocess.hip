@@ -148,12 +148,22 @@ __device__ void unite(int32_t* L, int a, int b) {
 }
 
 // ---------------------------------------------------------------- mask + local CCL
-// One 256-thread block = one TW x TH pixel tile. Each thread computes its pixel's
-// mask bit (palette -> 3x3 blur -> gray -> threshold) and the tile's connected
-// components are resolved with union-find on LDS labels; the global label of a
-// pixel is then the raster index (+1) of its tile-local root, which is also the
-// tile-local minimum, so the global min-root invariant is preserved.
-constexpr int TW = 32, TH = 8;
+// One 512-thread block = one TW x TH = 32 x 16 pixel tile, one thread per pixel,
+// half a wave per tile row.
+//  1. mask: the tile's labels + 1-pixel REFLECT_101 halo are staged in LDS, the
+//     palette colours are box-summed separably (horizontal 3-sums in LDS, then
+//     vertical), rounded per channel like cv2.blur, converted with the fixed-point
+//     BGR2GRAY weights and thresholded;
+//  2. runs: each row's mask is one 32-bit ballot; a pixel's initial label is the
+//     start of its horizontal run (foreground and background runs alike), so the
+//     horizontal unions cost nothing;
+//  3. the only unions are between a run and each run of the row above that it
+//     touches (8-neighbourhood for foreground, 4 for background), one union per
+//     touching pair, issued by the pixel where the overlap starts;
+//  4. every root is the minimum tile index of its set (atomicMin linking), so the
+//     global label (raster index + 1 of the tile-local root) keeps the global
+//     min-root invariant the boundary merge relies on.
+constexpr int TW = 32, TH = 16;
 
 __device__ __forceinline__ int lds_ld(const int* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -185,61 +195,88 @@ __device__ void lunite(int* l, int a, int b) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_ccl_local(KArgs a, const int32_t* __restrict__ pal) {
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+__global__ __launch_bounds__(TW * TH) void k_ccl_local(KArgs a, const int32_t* __restrict__ pal) {
+  constexpr int HW2 = TW + 2, HH2 = TH + 2;
   __shared__ int spal[256 * 3];
+  __shared__ uint8_t slab[HH2 * HW2];
+  __shared__ int hs[3][HH2 * TW];
   __shared__ int lbl[TW * TH];
-  __shared__ uint8_t msk[TW * TH];
-  for (int i = threadIdx.x; i < 256 * 3; i += blockDim.x) spal[i] = pal[i];
+  __shared__ unsigned fgrow[TH], bgrow[TH];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 256 * 3; i += TW * TH) spal[i] = pal[i];
   const int b = blockIdx.z;
-  const int tx = threadIdx.x % TW, ty = threadIdx.x / TW;
-  const int x = blockIdx.x * TW + tx, y = blockIdx.y * TH + ty;
+  const int x0 = blockIdx.x * TW, y0 = blockIdx.y * TH;
+  const int tx = tid % TW, ty = tid / TW;
+  const int x = x0 + tx, y = y0 + ty;
   const bool in = x < a.cw && y < a.ch;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) f.L[0] = 0;
-  __syncthreads();
-  uint8_t m = 0;
-  if (in) {
-    const uint8_t* lab = a.labels + (size_t)b * a.H * a.W;
-    int s0 = 0, s1 = 0, s2 = 0;
-#pragma unroll
-    for (int dy = -1; dy <= 1; ++dy) {
-      const int yy = reflect101(y + dy, a.ch);
-#pragma unroll
-      for (int dx = -1; dx <= 1; ++dx) {
-        const int xx = reflect101(x + dx, a.cw);
-        const int l = lab[yy * a.W + xx];
-        s0 += spal[l * 3 + 0];
-        s1 += spal[l * 3 + 1];
-        s2 += spal[l * 3 + 2];
-      }
-    }
-    const int c0 = (s0 * 2 + 9) / 18, c1 = (s1 * 2 + 9) / 18, c2 = (s2 * 2 + 9) / 18;
-    const int g = (c0 * 1868 + c1 * 9617 + c2 * 4899 + (1 << 13)) >> 14;
-    m = g > a.thr ? 1 : 0;
-    f.mask[y * a.cw + x] = m;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) f.L[0] = 0;
+  const uint8_t* lab = a.labels + (size_t)b * a.H * a.W;
+  for (int i = tid; i < HH2 * HW2; i += TW * TH) {
+    const int yy = clampi(reflect101(y0 - 1 + i / HW2, a.ch), 0, a.ch - 1);
+    const int xx = clampi(reflect101(x0 - 1 + i % HW2, a.cw), 0, a.cw - 1);
+    slab[i] = lab[yy * a.W + xx];
   }
-  const int me = threadIdx.x;
-  msk[me] = in ? m : 2;  // 2 = outside the crop (never joins anything)
-  lbl[me] = me;
   __syncthreads();
+  for (int i = tid; i < HH2 * TW; i += TW * TH) {
+    const int r = i / TW, c = i % TW;
+    const uint8_t* sr = slab + r * HW2 + c;
+    const int l0 = sr[0], l1 = sr[1], l2 = sr[2];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) hs[ch][i] = spal[l0 * 3 + ch] + spal[l1 * 3 + ch] + spal[l2 * 3 + ch];
+  }
+  __syncthreads();
+  bool m = false;
   if (in) {
+    int c[3];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      const int sum = hs[ch][ty * TW + tx] + hs[ch][(ty + 1) * TW + tx] + hs[ch][(ty + 2) * TW + tx];
+      c[ch] = (sum * 2 + 9) / 18;
+    }
+    const int g = (c[0] * 1868 + c[1] * 9617 + c[2] * 4899 + (1 << 13)) >> 14;
+    m = g > a.thr;
+    f.mask[y * a.cw + x] = m ? 1 : 0;
+  }
+  // per-row run bitmasks (bit = column); lanes 0-31 / 32-63 of a wave are two rows
+  const unsigned long long bf = __ballot(in && m), bb = __ballot(in && !m);
+  const int half = (tid & 63) >> 5;
+  const unsigned fgm = (unsigned)(bf >> (32 * half)), bgm = (unsigned)(bb >> (32 * half));
+  if ((tid & 31) == 0) {
+    fgrow[ty] = fgm;
+    bgrow[ty] = bgm;
+  }
+  const unsigned mine = m ? fgm : bgm;
+  const int me = tid;
+  int start = me;
+  if (in) {
+    const unsigned starts = mine & ~(mine << 1);
+    start = ty * TW + 31 - __clz(starts & (0xffffffffu >> (31 - tx)));
+  }
+  lbl[me] = start;
+  __syncthreads();
+  if (in && ty > 0) {
+    const unsigned bit = 1u << tx;
+    const int up = me - TW;
     if (m) {
-      if (tx > 0 && msk[me - 1] == 1) lunite(lbl, me, me - 1);
-      if (ty > 0) {
-        const int up = me - TW;
-        if (msk[up] == 1) lunite(lbl, me, up);
-        if (tx > 0 && msk[up - 1] == 1) lunite(lbl, me, up - 1);
-        if (tx + 1 < TW && msk[up + 1] == 1) lunite(lbl, me, up + 1);
-      }
+      const unsigned u = fgrow[ty - 1];
+      const unsigned ends = fgm & ~(fgm >> 1);
+      const bool first = (me == start);
+      const bool last = (ends & bit) != 0;
+      if ((u & bit) && (first || !(u & (bit >> 1)))) lunite(lbl, start, up);
+      if (first && tx > 0 && (u & (bit >> 1)) && !(u & bit)) lunite(lbl, start, up - 1);
+      if (last && tx < 31 && (u & (bit << 1)) && !(u & bit)) lunite(lbl, start, up + 1);
     } else {
-      if (tx > 0 && msk[me - 1] == 0) lunite(lbl, me, me - 1);
-      if (ty > 0 && msk[me - TW] == 0) lunite(lbl, me, me - TW);
+      const unsigned u = bgrow[ty - 1];
+      if ((u & bit) && (me == start || !(u & (bit >> 1)))) lunite(lbl, start, up);
     }
   }
   __syncthreads();
   if (in) {
-    const int r = lfind(lbl, me);
-    const int rx = blockIdx.x * TW + r % TW, ry = blockIdx.y * TH + r / TW;
+    const int r = lfind(lbl, start);
+    const int rx = x0 + r % TW, ry = y0 + r / TW;
     f.L[y * a.cw + x + 1] = ry * a.cw + rx + 1;
   }
 }
@@ -336,17 +373,55 @@ __global__ __launch_bounds__(256) void k_roots(KArgs a) {
   f.t01[p] = 0;
 }
 
-// Wave-aggregated atomic adds: the common case is a whole wave contributing to
-// the same node (interior of a large blob).
-__device__ __forceinline__ void agg_add(FrameWS& f, int node, int d00, long long d10,
+// Per-block privatisation of the component sums. A real scene's mask has a few
+// large components, so every quad of a blob adds into the same three global
+// counters: same-address atomics serialise at one L2 channel (the atomic version
+// of this pass took 127 us per 32 frames on calibrated masks). Each block owns a
+// contiguous strip of quads (a few image rows: few distinct components), sums
+// them in a small LDS open-addressing table keyed by component id, and flushes
+// one global atomic per (block, component). A wave whose 64 lanes hit the same
+// component is reduced by shuffles first; a full table falls back to global
+// atomics, so correctness never depends on the table size.
+constexpr int kHash = 128;
+constexpr int kQuadBlocks = 64;  // blocks per frame for the strip-privatised passes
+
+struct QuadTable {
+  int key[kHash];
+  int s00[kHash];
+  unsigned long long s10[kHash];
+  unsigned long long s01[kHash];
+};
+
+__device__ __forceinline__ void table_add(QuadTable& T, FrameWS& f, int node, int d00,
+                                          long long d10, long long d01) {
+  int h = (int)(((unsigned)node * 2654435761u) >> 25) & (kHash - 1);
+#pragma unroll 1
+  for (int probe = 0; probe < 16; ++probe, h = (h + 1) & (kHash - 1)) {
+    int k = __hip_atomic_load(&T.key[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (k == 0) {
+      k = atomicCAS(&T.key[h], 0, node);
+      if (k == 0) k = node;
+    }
+    if (k == node) {
+      atomicAdd(&T.s00[h], d00);
+      atomicAdd(&T.s10[h], (unsigned long long)d10);
+      atomicAdd(&T.s01[h], (unsigned long long)d01);
+      return;
+    }
+  }
+  atomicAdd(f.a00 + node - 1, d00);
+  atomicAdd(reinterpret_cast<unsigned long long*>(f.a10 + node - 1), (unsigned long long)d10);
+  atomicAdd(reinterpret_cast<unsigned long long*>(f.a01 + node - 1), (unsigned long long)d01);
+}
+
+__device__ __forceinline__ void agg_add(QuadTable& T, FrameWS& f, int node, int d00, long long d10,
                                         long long d01) {
   const bool active = node > 0;
   const unsigned long long act = __ballot(active);
   if (act == 0) return;
   const int leader = __ffsll((long long)act) - 1;
   const int lnode = __shfl(node, leader, 64);
-  const bool same = __all(!active || node == lnode);
-  if (same) {
+  if (__all(!active || node == lnode)) {
     int s00 = active ? d00 : 0;
     long long s10 = active ? d10 : 0, s01 = active ? d01 : 0;
 #pragma unroll
@@ -355,15 +430,9 @@ __device__ __forceinline__ void agg_add(FrameWS& f, int node, int d00, long long
       s10 += __shfl_xor(s10, o, 64);
       s01 += __shfl_xor(s01, o, 64);
     }
-    if ((int)(threadIdx.x & 63) == leader) {
-      atomicAdd(f.a00 + lnode - 1, s00);
-      atomicAdd(reinterpret_cast<unsigned long long*>(f.a10 + lnode - 1), (unsigned long long)s10);
-      atomicAdd(reinterpret_cast<unsigned long long*>(f.a01 + lnode - 1), (unsigned long long)s01);
-    }
+    if ((int)(threadIdx.x & 63) == leader) table_add(T, f, lnode, s00, s10, s01);
   } else if (active) {
-    atomicAdd(f.a00 + node - 1, d00);
-    atomicAdd(reinterpret_cast<unsigned long long*>(f.a10 + node - 1), (unsigned long long)d10);
-    atomicAdd(reinterpret_cast<unsigned long long*>(f.a01 + node - 1), (unsigned long long)d01);
+    table_add(T, f, node, d00, d10, d01);
   }
 }
 
@@ -371,62 +440,80 @@ __device__ __forceinline__ void agg_add(FrameWS& f, int node, int d00, long long
 // Corner order TL, TR, BL, BR. Triangle of corner k = k + its two quad
 // neighbours; sums of its 3 vertices' coordinates = 3x + TX[k], 3y + TY[k].
 __global__ __launch_bounds__(256) void k_quads(KArgs a) {
+  __shared__ QuadTable T;
   const int b = blockIdx.y;
   const int QW = a.cw - 1, QH = a.ch - 1;
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  const int Q = QW > 0 && QH > 0 ? QW * QH : 0;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
-  int fnode = 0, f00 = 0;
-  long long f10 = 0, f01 = 0;
-  int bn[2] = {0, 0}, b00[2] = {0, 0};
-  long long b10[2] = {0, 0}, b01[2] = {0, 0};
-  if (QW > 0 && QH > 0 && q < QW * QH) {
-    const int y = q / QW, x = q - y * QW;
-    const int p0 = y * a.cw + x;
-    const int idx[4] = {p0, p0 + 1, p0 + a.cw, p0 + a.cw + 1};
-    const int TX[4] = {1, 2, 1, 2}, TY[4] = {1, 1, 2, 2};
-    int node[4];
-    bool fg[4];
-    int nf = 0, missing = 0;
+  for (int i = threadIdx.x; i < kHash; i += 256) {
+    T.key[i] = 0; T.s00[i] = 0; T.s10[i] = 0; T.s01[i] = 0;
+  }
+  __syncthreads();
+  const int per = (Q + gridDim.x - 1) / gridDim.x;
+  const int q0 = blockIdx.x * per, q1 = min(Q, q0 + per);
+  for (int qb = q0; qb < q1; qb += 256) {
+    const int q = qb + threadIdx.x;
+    int fnode = 0, f00 = 0;
+    long long f10 = 0, f01 = 0;
+    int bn[2] = {0, 0}, b00[2] = {0, 0};
+    long long b10[2] = {0, 0}, b01[2] = {0, 0};
+    if (q < q1) {
+      const int y = q / QW, x = q - y * QW;
+      const int p0 = y * a.cw + x;
+      const int idx[4] = {p0, p0 + 1, p0 + a.cw, p0 + a.cw + 1};
+      const int TX[4] = {1, 2, 1, 2}, TY[4] = {1, 1, 2, 2};
+      int node[4];
+      bool fg[4];
+      int nf = 0, missing = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      fg[k] = f.mask[idx[k]] != 0;
-      node[k] = f.L[idx[k] + 1];
-      if (fg[k]) { ++nf; fnode = node[k]; } else { missing = k; }
-    }
-    const long long X = x, Y = y;
-    if (nf == 4) {
-      f00 = 2; f10 = 6 * X + 3; f01 = 6 * Y + 3;
-    } else if (nf == 3) {
-      const int o = 3 - missing;  // triangle of the opposite corner
-      f00 = 1; f10 = 3 * X + TX[o]; f01 = 3 * Y + TY[o];
-    } else {
-      fnode = 0;
-    }
-    int nb = 0;
+      for (int k = 0; k < 4; ++k) {
+        fg[k] = f.mask[idx[k]] != 0;
+        node[k] = f.L[idx[k] + 1];
+        if (fg[k]) { ++nf; fnode = node[k]; } else { missing = k; }
+      }
+      const long long X = x, Y = y;
+      if (nf == 4) {
+        f00 = 2; f10 = 6 * X + 3; f01 = 6 * Y + 3;
+      } else if (nf == 3) {
+        const int o = 3 - missing;  // triangle of the opposite corner
+        f00 = 1; f10 = 3 * X + TX[o]; f01 = 3 * Y + TY[o];
+      } else {
+        fnode = 0;
+      }
+      int nb = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (fg[k] || node[k] == 0) continue;
-      bool first = true;
-      int cnt = 0;
+      for (int k = 0; k < 4; ++k) {
+        if (fg[k] || node[k] == 0) continue;
+        bool first = true;
+        int cnt = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (!fg[j] && node[j] == node[k]) {
-          ++cnt;
-          if (j < k) first = false;
+        for (int j = 0; j < 4; ++j) {
+          if (!fg[j] && node[j] == node[k]) {
+            ++cnt;
+            if (j < k) first = false;
+          }
+        }
+        if (!first) continue;
+        if (nb < 2) {
+          bn[nb] = node[k];
+          if (cnt >= 2) { b00[nb] = 2; b10[nb] = 6 * X + 3; b01[nb] = 6 * Y + 3; }
+          else { b00[nb] = 1; b10[nb] = 3 * X + TX[k]; b01[nb] = 3 * Y + TY[k]; }
+          ++nb;
         }
       }
-      if (!first) continue;
-      if (nb < 2) {
-        bn[nb] = node[k];
-        if (cnt >= 2) { b00[nb] = 2; b10[nb] = 6 * X + 3; b01[nb] = 6 * Y + 3; }
-        else { b00[nb] = 1; b10[nb] = 3 * X + TX[k]; b01[nb] = 3 * Y + TY[k]; }
-        ++nb;
-      }
     }
+    agg_add(T, f, fnode, f00, f10, f01);
+    agg_add(T, f, bn[0], b00[0], b10[0], b01[0]);
+    agg_add(T, f, bn[1], b00[1], b10[1], b01[1]);
   }
-  agg_add(f, fnode, f00, f10, f01);
-  agg_add(f, bn[0], b00[0], b10[0], b01[0]);
-  agg_add(f, bn[1], b00[1], b10[1], b01[1]);
+  __syncthreads();
+  for (int i = threadIdx.x; i < kHash; i += 256) {
+    const int node = T.key[i];
+    if (node == 0) continue;
+    atomicAdd(f.a00 + node - 1, T.s00[i]);
+    atomicAdd(reinterpret_cast<unsigned long long*>(f.a10 + node - 1), T.s10[i]);
+    atomicAdd(reinterpret_cast<unsigned long long*>(f.a01 + node - 1), T.s01[i]);
+  }
 }
 
 // ---------------------------------------------------------------- tree sums
@@ -469,66 +556,80 @@ __global__ __launch_bounds__(256) void k_select(KArgs a) {
 }
 
 // ---------------------------------------------------------------- histograms
-__device__ __forceinline__ void hist_add(int32_t* hist, int bins, int slot, int label) {
-  // aggregate identical (slot, label) pairs across the wave
+// Same privatisation: the (slot, class) histogram of a frame is tiny (nslot x bins
+// counters, typically 1-3 slots) and every pixel of a selected contour's fill adds
+// to it, so each block of a frame's strip accumulates in LDS (wave-aggregated
+// first) and flushes its non-zero counters once.
+constexpr int kMaxHist = 256 * 32;
+
+__device__ __forceinline__ void hist_add(int* sh, int bins, int slot, int label) {
   const int key = slot >= 0 ? slot * bins + label : -1;
   const unsigned long long act = __ballot(key >= 0);
   if (act == 0) return;
   const int leader = __ffsll((long long)act) - 1;
   const int lkey = __shfl(key, leader, 64);
   if (__all(key < 0 || key == lkey)) {
-    if ((int)(threadIdx.x & 63) == leader) atomicAdd(hist + lkey, __popcll(act));
+    if ((int)(threadIdx.x & 63) == leader) atomicAdd(sh + lkey, __popcll(act));
   } else if (key >= 0) {
-    atomicAdd(hist + key, 1);
+    atomicAdd(sh + key, 1);
   }
 }
 
 __global__ __launch_bounds__(256) void k_hist(KArgs a) {
+  extern __shared__ int sh[];  // [ns * bins]
   const int b = blockIdx.y;
   const int N = a.ch * a.cw;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
-  if (*f.nslot == 0) return;  // block-uniform early exit: no contour selected
-  int label = 0, n = 0, y = 0, x = 0;
-  bool fgp = false;
-  if (p < N) {
-    y = p / a.cw;
-    x = p - y * a.cw;
-    label = a.labels[(size_t)b * a.H * a.W + y * a.W + x];
-    if (label >= a.bins) label = a.bins - 1;
-    n = f.L[p + 1];
-    fgp = f.mask[p] != 0;
-  }
-  // ancestors (inclusive): the fill of every enclosing contour contains p
-  int depth = 0;
-  while (true) {
-    const int s = (n != 0) ? f.slot[n - 1] : -1;
-    const bool more = __any(n != 0);
-    if (!more) break;
-    hist_add(f.hist, a.bins, s, label);
-    if (n != 0) n = f.parent[n - 1];
-    if (++depth > 65536) break;
-  }
-  // ring: a foreground pixel 4-adjacent to a selected hole of its own component
-  int hs[4] = {-1, -1, -1, -1};
-  if (p < N && fgp) {
-    const int me = f.L[p + 1];
-    const int nb[4] = {x > 0 ? p - 1 : -1, x + 1 < a.cw ? p + 1 : -1, y > 0 ? p - a.cw : -1,
-                       y + 1 < a.ch ? p + a.cw : -1};
-    int seen[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (nb[k] < 0 || f.mask[nb[k]]) continue;
-      const int h = f.L[nb[k] + 1];
-      if (h == 0 || f.parent[h - 1] != me) continue;
-      bool dup = false;
-      for (int j = 0; j < k; ++j) dup |= (seen[j] == h);
-      seen[k] = h;
-      if (!dup) hs[k] = f.slot[h - 1];
+  const int ns = min(*f.nslot, a.K);
+  if (ns == 0) return;  // block-uniform early exit: no contour selected
+  const int nh = ns * a.bins;
+  for (int i = threadIdx.x; i < nh; i += 256) sh[i] = 0;
+  __syncthreads();
+  const int per = (N + gridDim.x - 1) / gridDim.x;
+  const int p0 = blockIdx.x * per, p1 = min(N, p0 + per);
+  for (int pb = p0; pb < p1; pb += 256) {
+    const int p = pb + threadIdx.x;
+    int label = 0, n = 0, y = 0, x = 0;
+    bool fgp = false;
+    if (p < p1) {
+      y = p / a.cw;
+      x = p - y * a.cw;
+      label = a.labels[(size_t)b * a.H * a.W + y * a.W + x];
+      if (label >= a.bins) label = a.bins - 1;
+      n = f.L[p + 1];
+      fgp = f.mask[p] != 0;
     }
-  }
+    // ancestors (inclusive): the fill of every enclosing contour contains p
+    for (int depth = 0; depth <= 65536; ++depth) {
+      if (!__any(n != 0)) break;
+      const int s = (n != 0) ? f.slot[n - 1] : -1;
+      hist_add(sh, a.bins, s, label);
+      if (n != 0) n = f.parent[n - 1];
+    }
+    // ring: a foreground pixel 4-adjacent to a selected hole of its own component
+    int hs[4] = {-1, -1, -1, -1};
+    if (p < p1 && fgp) {
+      const int me = f.L[p + 1];
+      const int nb[4] = {x > 0 ? p - 1 : -1, x + 1 < a.cw ? p + 1 : -1, y > 0 ? p - a.cw : -1,
+                         y + 1 < a.ch ? p + a.cw : -1};
+      int seen[4] = {0, 0, 0, 0};
 #pragma unroll
-  for (int k = 0; k < 4; ++k) hist_add(f.hist, a.bins, hs[k], label);
+      for (int k = 0; k < 4; ++k) {
+        if (nb[k] < 0 || f.mask[nb[k]]) continue;
+        const int h = f.L[nb[k] + 1];
+        if (h == 0 || f.parent[h - 1] != me) continue;
+        bool dup = false;
+        for (int j = 0; j < k; ++j) dup |= (seen[j] == h);
+        seen[k] = h;
+        if (!dup) hs[k] = f.slot[h - 1];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) hist_add(sh, a.bins, hs[k], label);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nh; i += 256)
+    if (sh[i]) atomicAdd(f.hist + i, sh[i]);
 }
 
 // ---------------------------------------------------------------- finalize
@@ -629,6 +730,7 @@ size_t post_workspace_bytes(int B, int H, int W, int K, int num_bins) {
 
 void postprocess(const PostParams& p, hipStream_t s) {
   if (p.K > 256) throw std::invalid_argument("postprocess: K > 256");
+  if ((size_t)p.K * p.num_bins > (size_t)kMaxHist) throw std::invalid_argument("postprocess: K * bins too large");
   if (p.crop_h > p.H || p.crop_w > p.W || p.crop_h <= 0 || p.crop_w <= 0)
     throw std::invalid_argument("postprocess: bad crop");
   KArgs a;
@@ -647,8 +749,6 @@ void postprocess(const PostParams& p, hipStream_t s) {
   const int N = p.crop_h * p.crop_w;
   const dim3 blk(256);
   const dim3 gp(cdiv(N, 256), p.B);
-  const int Q = (p.crop_w - 1) * (p.crop_h - 1);
-  const dim3 gq(cdiv(std::max(Q, 1), 256), p.B);
   // SSA_POST_STAGES=n (debug) launches only the first n stages
   static const int stages = [] {
     const char* e = getenv("SSA_POST_STAGES");
@@ -656,14 +756,16 @@ void postprocess(const PostParams& p, hipStream_t s) {
   }();
   int st = 0;
   const dim3 gt(cdiv(p.crop_w, TW), cdiv(p.crop_h, TH), p.B);
-  if (st++ < stages) hipLaunchKernelGGL(k_ccl_local, gt, blk, 0, s, a, p.palette);
+  if (st++ < stages) hipLaunchKernelGGL(k_ccl_local, gt, dim3(TW * TH), 0, s, a, p.palette);
   if (st++ < stages) hipLaunchKernelGGL(k_ccl_boundary, gp, blk, 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_compress, gp, blk, 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_roots, gp, blk, 0, s, a);
-  if (st++ < stages) hipLaunchKernelGGL(k_quads, gq, blk, 0, s, a);
+  const dim3 gs(kQuadBlocks, p.B);
+  if (st++ < stages) hipLaunchKernelGGL(k_quads, gs, blk, 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_tree, gp, blk, 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_select, gp, blk, 0, s, a);
-  if (st++ < stages) hipLaunchKernelGGL(k_hist, gp, blk, 0, s, a);
+  if (st++ < stages)
+    hipLaunchKernelGGL(k_hist, gs, blk, (size_t)std::min(p.K, 256) * p.num_bins * 4, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_finalize, dim3(p.B), dim3(64), 0, s, a);
   check_launch("postprocess");
 }

@@ -4,11 +4,12 @@ python scripts/bench_conv.py [--reps 20] [--only mnv2|r50]  -> one line per (sha
 time (us), effective TFLOP/s (nominal MACs incl. padding taps), max |diff| vs variant 2.
 """
 import argparse
+import os
 import sys
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from semantic_segmentation_server_amd.ops import hip_ops as K  # noqa: E402
 
 SHAPES = {

@@ -42,7 +42,7 @@ log = logging.getLogger(__name__)
 DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32, "int8": torch.bfloat16}
 
 
-def calibration_frames(H: int, W: int, n: int = 2, seed: int = 0) -> torch.Tensor:
+def calibration_frames(H: int, W: int, n: int = 8, seed: int = 0) -> torch.Tensor:
     """Letterboxed synthetic camera frames at the model resolution, normalised:
     the calibration batch for random-init weights (BN statistics + class prior),
     drawn from the same distribution the synthetic source serves."""
