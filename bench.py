@@ -96,9 +96,10 @@ def main() -> int:
     verbose = os.environ.get("SSA_BENCH_VERBOSE", "0") == "1"
 
     def run_steps(n: int, k0: int = 0) -> None:
+        # double-buffered ingest: the next batch's H2D overlaps this step's compute
+        pipe.prefetch(host_batches[k0 % 2])
         for k in range(n):
-            pipe.prefetch(host_batches[(k0 + k) % 2])
-            pipe.step()
+            pipe.step(next_frames=host_batches[(k0 + k + 1) % 2] if k + 1 < n else None)
             if verbose:
                 print(f"[rank {ctx.rank}] step {k0 + k} ok", file=sys.stderr, flush=True)
 

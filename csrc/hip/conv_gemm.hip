@@ -108,6 +108,9 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   }
 
   // epilogue: lane holds out channels ch0 + j*16 + kq*4 + {0..3} of pixel pix0 + i*16 + r
+  // (8-byte row pieces; staging the tile through LDS for 16-byte stores measured
+  // 1.5x slower on the MobileNetV2 expansions: the extra barrier + LDS round trip
+  // costs more than the partial-line writes, which L2 merges)
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
     const int m = pix0 + i * 16 + r;

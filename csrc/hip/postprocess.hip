@@ -48,11 +48,23 @@ struct FrameWS {
   int32_t* hist;       // [K][bins]
   int32_t* nslot;      // [1] (+ overflow flag at [1])
   int32_t* slot_node;  // [K]
+  int32_t* cidx;       // [N] per tile-local root pixel: its index among the tile's roots
+  int32_t* rootpix;    // [ntiles][kTileRoots] raster index of each tile-local root
+  int32_t* ntroot;     // [ntiles] tile-local roots per tile
+  int32_t* toff;       // [ntiles] compact-id offset of each tile (merge kernel)
+  int32_t* clabel;     // [kMergeCap] final label of each compact node
+  int32_t* flag;       // [4]: [0] = 1 -> frame took the global union-find fallback
+  int32_t* edges;      // [kEdgeCap][2] cross-tile unions (tile-local root pairs, -1 = outside)
 };
+
+constexpr int TW = 32, TH = 16;     // local CCL tile
+constexpr int kTileRoots = TW * TH;  // worst case roots per tile
+constexpr int kMergeCap = 12288;     // compact nodes the per-frame LDS merge handles
+constexpr int kEdgeCap = 1 << 16;    // cross-tile union pairs per frame
 
 // Workspace layout: per frame, fixed stride; counters/hists first (memset region).
 struct Layout {
-  size_t N, K, bins;
+  size_t N, K, bins, ntiles;
   size_t small_bytes;  // nslot(16) + hist + slot_node, per frame (zeroed every call)
   size_t big_bytes;    // per frame
   size_t total(int B) const { return (small_bytes + big_bytes) * (size_t)B; }
@@ -65,8 +77,11 @@ Layout layout(int H, int W, int K, int bins) {
   l.N = (size_t)H * W;
   l.K = K;
   l.bins = bins;
+  l.ntiles = (size_t)((W + TW - 1) / TW) * ((H + TH - 1) / TH);
   l.small_bytes = al(16 + (size_t)K * bins * 4 + (size_t)K * 4);
-  l.big_bytes = al((l.N + 1) * 4) + al(l.N) + 4 * al(l.N * 4) + 4 * al(l.N * 8);
+  l.big_bytes = al((l.N + 1) * 4) + al(l.N) + 4 * al(l.N * 4) + 4 * al(l.N * 8) + al(l.N * 4) +
+                al(l.ntiles * kTileRoots * 4) + 2 * al(l.ntiles * 4) + al(kMergeCap * 4) + al(16) +
+                al((size_t)kEdgeCap * 8);
   return l;
 }
 
@@ -87,6 +102,13 @@ __host__ __device__ inline FrameWS frame_ws(char* ws, const Layout& l, int B, in
   f.a01 = reinterpret_cast<long long*>(p); p += al(l.N * 8);
   f.t10 = reinterpret_cast<long long*>(p); p += al(l.N * 8);
   f.t01 = reinterpret_cast<long long*>(p); p += al(l.N * 8);
+  f.cidx = reinterpret_cast<int32_t*>(p); p += al(l.N * 4);
+  f.rootpix = reinterpret_cast<int32_t*>(p); p += al(l.ntiles * kTileRoots * 4);
+  f.ntroot = reinterpret_cast<int32_t*>(p); p += al(l.ntiles * 4);
+  f.toff = reinterpret_cast<int32_t*>(p); p += al(l.ntiles * 4);
+  f.clabel = reinterpret_cast<int32_t*>(p); p += al(kMergeCap * 4);
+  f.flag = reinterpret_cast<int32_t*>(p); p += al(16);
+  f.edges = reinterpret_cast<int32_t*>(p); p += al((size_t)kEdgeCap * 8);
   return f;
 }
 
@@ -163,8 +185,6 @@ __device__ void unite(int32_t* L, int a, int b) {
 //  4. every root is the minimum tile index of its set (atomicMin linking), so the
 //     global label (raster index + 1 of the tile-local root) keeps the global
 //     min-root invariant the boundary merge relies on.
-constexpr int TW = 32, TH = 16;
-
 __device__ __forceinline__ int lds_ld(const int* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -274,10 +294,208 @@ __global__ __launch_bounds__(TW * TH) void k_ccl_local(KArgs a, const int32_t* _
     }
   }
   __syncthreads();
+  __shared__ int s_nroot;
+  if (tid == 0) s_nroot = 0;
+  __syncthreads();
   if (in) {
     const int r = lfind(lbl, start);
     const int rx = x0 + r % TW, ry = y0 + r / TW;
     f.L[y * a.cw + x + 1] = ry * a.cw + rx + 1;
+    if (r == me) {  // tile-local root: number it for the compact merge
+      const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+      const int c = atomicAdd(&s_nroot, 1);
+      f.cidx[y * a.cw + x] = c;
+      f.rootpix[(size_t)tile * kTileRoots + c] = y * a.cw + x;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) f.ntroot[blockIdx.y * gridDim.x + blockIdx.x] = s_nroot;
+}
+
+// ---------------------------------------------------------------- compact merge
+// Cross-tile merging in two steps.
+// k_ccl_edges: every pixel on a tile edge (or on the image border) emits the
+//   unions it needs as pairs of tile-local roots (-1 = the outside node). Lanes
+//   run along the edge (x for horizontal edges, y for vertical ones), so the
+//   long runs of identical pairs a blob produces collapse to one pair with a
+//   compare against the previous lane; survivors are appended with one atomic
+//   per wave.
+// k_ccl_merge: ONE workgroup per frame numbers the tile-local roots (a few per
+//   tile on real masks) compactly, runs union-find over the pair list on LDS
+//   atomics, and maps every compact node to its component's final label (min
+//   raster index + 1, outside-connected background -> 0).
+// The pre-existing global union-find (k_ccl_boundary: device-coherent pointer
+// chasing from every CU, serialised on the roots of big components) remains the
+// fallback for frames that overflow kMergeCap roots or kEdgeCap pairs.
+__device__ __forceinline__ void emit_pairs(FrameWS& f, int n, const int (&pa)[3], const int (&pb)[3]) {
+  // wave-aggregated append of this lane's n pairs
+  int incl = n;
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  const int total = __shfl(incl, 63, 64);
+  if (total == 0) return;
+  int base = 0;
+  if (lane == 63) base = atomicAdd(f.nslot + 2, total);
+  base = __shfl(base, 63, 64);
+  const int at = base + incl - n;
+  for (int k = 0; k < n; ++k) {
+    if (at + k < kEdgeCap) {
+      f.edges[2 * (at + k)] = pa[k];
+      f.edges[2 * (at + k) + 1] = pb[k];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_ccl_edges(KArgs a) {
+  const int b = blockIdx.z;
+  FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
+  const int tx_n = (a.cw + TW - 1) / TW, ty_n = (a.ch + TH - 1) / TH;
+  // horizontal lines: tile top rows y = k*TH (k >= 1), image rows 0 and ch-1;
+  // vertical lines: tile left columns x = k*TW (k >= 1), right columns x = k*TW-1
+  // (k >= 1, x < cw-1), image columns 0 and cw-1
+  const int nh = (ty_n - 1) + 2, nv = 2 * (tx_n - 1) + 2;
+  const int line = blockIdx.y;
+  const bool horiz = line < nh;
+  int fixed, len;
+  int kind;  // 0 top row, 1 border row, 2 left column, 3 right column, 4 border column
+  if (horiz) {
+    if (line < ty_n - 1) { fixed = (line + 1) * TH; kind = 0; }
+    else { fixed = line == ty_n - 1 ? 0 : a.ch - 1; kind = 1; }
+    len = a.cw;
+  } else {
+    const int l = line - nh;
+    if (l >= nv) return;
+    if (l < tx_n - 1) { fixed = (l + 1) * TW; kind = 2; }
+    else if (l < 2 * (tx_n - 1)) { fixed = (l - (tx_n - 1) + 1) * TW - 1; kind = 3; }
+    else { fixed = l == 2 * (tx_n - 1) ? 0 : a.cw - 1; kind = 4; }
+    len = a.ch;
+  }
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = i < len && fixed >= 0 && (horiz ? fixed < a.ch : fixed < a.cw) &&
+                     !(kind == 3 && fixed + 1 >= a.cw);
+  const int x = horiz ? i : fixed, y = horiz ? fixed : i;
+  const int p = y * a.cw + x;
+  int pa[3] = {0, 0, 0}, pb[3] = {0, 0, 0};
+  int n = 0;
+  if (valid) {
+    const bool m = f.mask[p] != 0;
+    const int me = f.L[p + 1] - 1;
+    auto add = [&](int other) {  // distinct partners only
+      for (int k = 0; k < n; ++k)
+        if (pb[k] == other) return;
+      pa[n] = me;
+      pb[n] = other;
+      ++n;
+    };
+    auto lr = [&](int q) { return f.L[q + 1] - 1; };
+    if (kind == 0) {  // top row of a tile: unions with the row above
+      const int up = p - a.cw;
+      if (m) {
+        if (x > 0 && f.mask[up - 1]) add(lr(up - 1));
+        if (f.mask[up]) add(lr(up));
+        if (x + 1 < a.cw && f.mask[up + 1]) add(lr(up + 1));
+      } else if (!f.mask[up]) {
+        add(lr(up));
+      }
+    } else if (kind == 2) {  // left column of a tile: unions with the column to the left
+      if (m) {
+        if (f.mask[p - 1]) add(lr(p - 1));
+        if (y > 0 && (y % TH) != 0 && f.mask[p - a.cw - 1]) add(lr(p - a.cw - 1));
+      } else if (!f.mask[p - 1]) {
+        add(lr(p - 1));
+      }
+    } else if (kind == 3) {  // right column: up-right diagonal into the next tile
+      if (m && y > 0 && (y % TH) != 0 && f.mask[p - a.cw + 1]) add(lr(p - a.cw + 1));
+    }
+    if ((kind == 1 || kind == 4) && !m) add(-1);  // image-border background -> outside
+  }
+  // drop pairs the previous lane (previous pixel along this line) also emitted
+  const int lane = threadIdx.x & 63;
+  const int qa0 = __shfl_up(pa[0], 1, 64), qb0 = __shfl_up(pb[0], 1, 64);
+  const int qa1 = __shfl_up(pa[1], 1, 64), qb1 = __shfl_up(pb[1], 1, 64);
+  const int qa2 = __shfl_up(pa[2], 1, 64), qb2 = __shfl_up(pb[2], 1, 64);
+  const int qn = __shfl_up(n, 1, 64);
+  int keep = 0;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if (k < n) {
+      bool dup = false;
+      if (lane > 0) {
+        dup |= qn > 0 && qa0 == pa[k] && qb0 == pb[k];
+        dup |= qn > 1 && qa1 == pa[k] && qb1 == pb[k];
+        dup |= qn > 2 && qa2 == pa[k] && qb2 == pb[k];
+      }
+      if (!dup) { pa[keep] = pa[k]; pb[keep] = pb[k]; ++keep; }
+    }
+  }
+  emit_pairs(f, keep, pa, pb);
+}
+
+__global__ __launch_bounds__(1024) void k_ccl_merge(KArgs a) {
+  extern __shared__ int sm[];
+  const int b = blockIdx.x;
+  FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
+  const int tx_n = (a.cw + TW - 1) / TW, ty_n = (a.ch + TH - 1) / TH;
+  const int nt = tx_n * ty_n;
+  const int tid = threadIdx.x;
+  int* toff = sm;                   // [nt + 1]
+  int* part = sm + nt + 1;          // [1024] scan partials
+  int* par = part + 1024;           // [kMergeCap + 1] (last = outside)
+  int* minr = par + kMergeCap + 1;  // [kMergeCap + 1]
+  // exclusive scan of the per-tile root counts
+  const int per = (nt + 1023) / 1024;
+  const int t0 = tid * per, t1 = min(nt, t0 + per);
+  int sum = 0;
+  for (int t = t0; t < t1; ++t) sum += f.ntroot[t];
+  part[tid] = sum;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int v = tid >= o ? part[tid - o] : 0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  int acc = part[tid] - sum;
+  for (int t = t0; t < t1; ++t) {
+    toff[t] = acc;
+    acc += f.ntroot[t];
+  }
+  if (tid == 1023) toff[nt] = part[1023];
+  __syncthreads();
+  const int R = toff[nt];
+  const int E = f.nslot[2];
+  if (tid == 0) f.flag[0] = (R > kMergeCap || E > kEdgeCap) ? 1 : 0;
+  if (R > kMergeCap || E > kEdgeCap) return;  // fallback: k_ccl_boundary + k_compress
+  const int OUT = R;
+  for (int i = tid; i <= R; i += 1024) {
+    par[i] = i;
+    minr[i] = 0x7fffffff;
+  }
+  for (int t = tid; t < nt; t += 1024) f.toff[t] = toff[t];
+  __syncthreads();
+  auto compact = [&](int r) {
+    const int ly = r / a.cw, lx = r - ly * a.cw;
+    return toff[(ly / TH) * tx_n + lx / TW] + f.cidx[r];
+  };
+  for (int e = tid; e < E; e += 1024) {
+    const int ra = f.edges[2 * e], rb = f.edges[2 * e + 1];
+    lunite(par, compact(ra), rb < 0 ? OUT : compact(rb));
+  }
+  __syncthreads();
+  for (int t = tid; t < nt; t += 1024) {
+    const int n = f.ntroot[t];
+    for (int c = 0; c < n; ++c)
+      atomicMin(&minr[lfind(par, toff[t] + c)], f.rootpix[(size_t)t * kTileRoots + c]);
+  }
+  __syncthreads();
+  const int outroot = lfind(par, OUT);
+  for (int i = tid; i < R; i += 1024) {
+    const int r = lfind(par, i);
+    f.clabel[i] = r == outroot ? 0 : minr[r] + 1;
   }
 }
 
@@ -288,6 +506,7 @@ __global__ __launch_bounds__(256) void k_ccl_boundary(KArgs a) {
   const int N = a.ch * a.cw;
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= N) return;
+  if (frame_ws(a.ws, a.lay, a.B, b).flag[0] == 0) return;  // merged in LDS
   const int y = p / a.cw, x = p - y * a.cw;
   const bool left = x > 0 && (x % TW) == 0;
   const bool top = y > 0 && (y % TH) == 0;
@@ -345,6 +564,14 @@ __global__ __launch_bounds__(256) void k_compress(KArgs a) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= N) return;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
+  if (f.flag[0] == 0) {  // compact merge: pixel -> its tile-local root -> final label
+    const int lr = f.L[p + 1] - 1;
+    const int ly = lr / a.cw, lx = lr - ly * a.cw;
+    const int tx_n = (a.cw + TW - 1) / TW;
+    const int t = (ly / TH) * tx_n + lx / TW;
+    f.L[p + 1] = f.clabel[f.toff[t] + f.cidx[lr]];
+    return;
+  }
   // Read-only traversal: a path-halving store here could overwrite another
   // thread's final root store with a stale grandparent (observed: 1 pixel in ~1M
   // left pointing at a non-root). Every concurrent store below writes a root, so
@@ -757,6 +984,23 @@ void postprocess(const PostParams& p, hipStream_t s) {
   int st = 0;
   const dim3 gt(cdiv(p.crop_w, TW), cdiv(p.crop_h, TH), p.B);
   if (st++ < stages) hipLaunchKernelGGL(k_ccl_local, gt, dim3(TW * TH), 0, s, a, p.palette);
+  {
+    const int tx_n = cdiv(p.crop_w, TW), ty_n = cdiv(p.crop_h, TH);
+    const int nt = tx_n * ty_n;
+    const size_t lds = (size_t)(nt + 1 + 1024 + 2 * (kMergeCap + 1)) * 4;
+    const int lines = (ty_n - 1) + 2 + 2 * (tx_n - 1) + 2;
+    if (st++ < stages)
+      hipLaunchKernelGGL(k_ccl_edges, dim3(cdiv(std::max(p.crop_w, p.crop_h), 256), lines, p.B), blk, 0, s, a);
+    if (lds > 160 * 1024) throw std::invalid_argument("postprocess: crop too large for the LDS merge");
+    static bool attr = false;
+    if (!attr) {
+      check(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ccl_merge),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
+            "k_ccl_merge attr");
+      attr = true;
+    }
+    if (st++ < stages) hipLaunchKernelGGL(k_ccl_merge, dim3(p.B), dim3(1024), lds, s, a);
+  }
   if (st++ < stages) hipLaunchKernelGGL(k_ccl_boundary, gp, blk, 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_compress, gp, blk, 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_roots, gp, blk, 0, s, a);

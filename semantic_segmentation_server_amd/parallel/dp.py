@@ -90,6 +90,7 @@ class DataParallelPipeline:
                                     pin_memory=self.cuda)
         self.frames_done = 0
         self.records_out = 0
+        self._prev_done = None  # compute-done event of the previous step
 
     # ---------------------------------------------------------------- ingest
     def prefetch(self, host_frames: torch.Tensor) -> None:
@@ -121,12 +122,15 @@ class DataParallelPipeline:
         return self.staging[s]
 
     # ---------------------------------------------------------------- step
-    def step(self, frame_ids=None, ts=None, streams=None) -> np.ndarray:
+    def step(self, frame_ids=None, ts=None, streams=None, next_frames=None) -> np.ndarray:
         """Run one step on the prefetched frames; returns rank-0 records (else empty).
 
         ``frame_ids``/``ts``/``streams`` describe this rank's B frames (defaults:
         running counters, 0.0, rank * S + i % S). They travel with the records
         through the gather so rank 0 can tag every record with its origin.
+        ``next_frames`` (pinned host batch): its H2D starts on the copy stream as
+        soon as this step's compute is enqueued, so ingest overlaps compute
+        (double-buffered staging) instead of preceding it.
         """
         B = self.B
         fids = list(frame_ids) if frame_ids is not None else \
@@ -136,6 +140,14 @@ class DataParallelPipeline:
             [self.ctx.rank * self.S + i % self.S for i in range(B)]
         frames = self._frames_for_step()
         labels, packed = self.engine.run_device(frames)
+        if next_frames is not None:
+            if self.cuda:  # the staging slot being refilled was last read one step ago
+                self.copy_stream.wait_stream(torch.cuda.current_stream(self.dev)) \
+                    if self._prev_done is None else self.copy_stream.wait_event(self._prev_done)
+            self.prefetch(next_frames)
+        if self.cuda:
+            self._prev_done = torch.cuda.Event()
+            self._prev_done.record(torch.cuda.current_stream(self.dev))
         if packed is None:  # host post-processing path (torch backend / exact mode)
             self.frames_done += B * self.ctx.world
             return self.engine.records_from_labels(labels, fids, tss, strm)

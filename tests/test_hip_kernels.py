@@ -211,6 +211,40 @@ def test_device_postprocess_matches_spec(seed, h, w, min_area):
             assert got[j, 4] == np.float32(min(1.0, cy / H))
 
 
+@pytest.mark.parametrize("block,period,min_area", [(3, 4, 100.0), (4, 5, 100.0), (4, 5, 3000.0)])
+def test_device_postprocess_many_components(block, period, min_area):
+    """Lattice masks with 10-16k components per frame (plus a few large blobs,
+    the only contours above min_area): the 3x3 / period-4 lattice overflows the
+    per-frame LDS merge (global union-find fallback), the others stay on the
+    compact merge."""
+    from semantic_segmentation_server_amd.labels import pascal_colormap
+    from semantic_segmentation_server_amd.postprocess.components import component_segments
+    from semantic_segmentation_server_amd.postprocess.device import DevicePostprocess
+    h = w = 513
+    lab = np.zeros((h, w), np.uint8)
+    for y in range(0, h - block + 1, period):
+        for x in range(0, w - block + 1, period):
+            lab[y:y + block, x:x + block] = 15 if (x // period + y // period) % 3 else 7
+    lab[40:200, 30:150] = 15
+    lab[80:120, 60:100] = 0      # hole
+    lab[300:480, 250:500] = 7
+    lab[350:420, 300:330] = 15   # island of another class
+    maps = np.stack([lab, lab[:, ::-1].copy()])
+    post = DevicePostprocess(torch.device(DEV), h, w, pascal_colormap(), K=64)
+    rec = post.run(torch.from_numpy(maps).to(DEV), w, h, min_area).cpu().numpy()
+    for i in range(2):
+        exp = component_segments(maps[i], min_area)
+        n = int(rec[i, 0])
+        assert n == min(len(exp), 64), (n, len(exp))
+        got = rec[i, 1:1 + 5 * n].reshape(n, 5)
+        for j in range(n):
+            lab_, score, area, cx, cy = exp[j][:5]
+            assert int(got[j, 0]) == lab_ and abs(got[j, 1] - score) < 1e-6
+            assert got[j, 2] == np.float32(min(1.0, area / (w * h)))
+            assert got[j, 3] == np.float32(min(1.0, cx / w))
+            assert got[j, 4] == np.float32(min(1.0, cy / h))
+
+
 def _small_cfg(**kw):
     from semantic_segmentation_server_amd import config as C
     base = dict(input_size=129, batch=2, backend="hip", graph=False)
