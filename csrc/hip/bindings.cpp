@@ -41,7 +41,7 @@ PYBIND11_MODULE(_hip, m) {
         [](uintptr_t in, uintptr_t we, uintptr_t be, uintptr_t wd, uintptr_t bd, uintptr_t wp,
            uintptr_t bp, uintptr_t out, int B, int IH, int IW, int Cin, int CinP, int hidP,
            int Cout, int OH, int OW, int stride, int residual, uintptr_t stream, int dil, int TY,
-           int TX, uintptr_t wd_h, uintptr_t bd_h, uintptr_t wp_h) {
+           int TX, uintptr_t wd_h, uintptr_t bd_h, uintptr_t wp_h, uintptr_t trace) {
           FusedIRParams p;
           p.in = P<const bf16>(in); p.we = P<const bf16>(we); p.be = P<const float>(be);
           p.wd = P<const float>(wd); p.bd = P<const float>(bd); p.wp = P<const bf16>(wp);
@@ -50,6 +50,7 @@ PYBIND11_MODULE(_hip, m) {
           p.OH = OH; p.OW = OW; p.stride = stride; p.residual = residual;
           p.dil = dil; p.TY = TY; p.TX = TX;
           p.wd_h = P<const void>(wd_h); p.bd_h = P<const void>(bd_h); p.wp_h = P<const void>(wp_h);
+          p.trace = P<long long>(trace);
           fused_inverted_residual(p, S(stream));
         },
         py::arg("in"), py::arg("we"), py::arg("be"), py::arg("wd"), py::arg("bd"), py::arg("wp"),
@@ -57,7 +58,7 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("CinP"), py::arg("hidP"), py::arg("Cout"), py::arg("OH"), py::arg("OW"),
         py::arg("stride"), py::arg("residual"), py::arg("stream"), py::arg("dil") = 1,
         py::arg("TY") = 0, py::arg("TX") = 0, py::arg("wd_h") = 0, py::arg("bd_h") = 0,
-        py::arg("wp_h") = 0);
+        py::arg("wp_h") = 0, py::arg("trace") = 0);
   m.def("fused_ir_tile_lds", &fused_ir_tile_lds);
 
   m.def("dw_project",

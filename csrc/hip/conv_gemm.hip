@@ -363,10 +363,12 @@ __device__ __attribute__((aligned(16))) int4 g_zero_page[8];
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-template <int MT, int NT, int ST>
-__global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs a) {
-  constexpr int BM = 32 * MT, BN = 32 * NT, ROWB = 128;  // BK = 64 bf16 per stage row
-  constexpr int GA = BM / 32, GB = BN / 32;              // glds per thread per stage
+template <int MT, int NT, int ST, int WM = 2, int WN = 2>
+__global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(ConvArgs a) {
+  constexpr int NW = WM * WN;                            // waves: WM (pixels) x WN (channels)
+  constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN, ROWB = 128;  // BK = 64 bf16 per stage row
+  constexpr int GA = BM / (8 * NW), GB = BN / (8 * NW);  // glds per thread per stage
+  static_assert(GA * 8 * NW == BM && GB * 8 * NW == BN, "tile rows must split over the waves");
   constexpr int SB = (BM + BN) * ROWB;
   constexpr int VM_INFLIGHT = (ST - 2) * (GA + GB);
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -374,7 +376,7 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WN, wn = wid % WN;
   const int r16 = lane & 15, kq = lane >> 4;
   const int M = a.B * a.OH * a.OW;
   const int tiles_m = cdiv_dev(M, BM), tiles_n = cdiv_dev(a.Cout, BN);
@@ -390,7 +392,7 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs a) {
   int tapbits = 0;
 #pragma unroll
   for (int i = 0; i < GA; ++i) {
-    const int m = m0 + wid * (BM / 4) + i * 8 + grow;
+    const int m = m0 + wid * (BM / NW) + i * 8 + grow;
     av[i] = m < M;
     const int mm = av[i] ? m : 0;
     const int b = mm / (a.OH * a.OW);
@@ -409,7 +411,7 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs a) {
   bool bv[GB];
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
-    const int n = n0 + wid * (BN / 4) + j * 8 + grow;
+    const int n = n0 + wid * (BN / NW) + j * 8 + grow;
     bv[j] = n < a.Cout;
     boff[j] = (bv[j] ? n : 0) * taps * a.Cin;
   }
@@ -438,14 +440,14 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs a) {
       const int iy = ay[i] + dy, ix = ax[i] + dx;
       const bool ok = av[i] && cok && iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW;
       const void* src = ok ? (const void*)(a.in + aoff[i] + doff) : (const void*)g_zero_page;
-      __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(sA + (wid * (BM / 4) + i * 8) * ROWB), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(sA + (wid * (BM / NW) + i * 8) * ROWB), 16, 0, 0);
     }
     char* sB = sA + BM * ROWB;
     const int wofs = t * a.Cin + c;
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
       const void* src = (bv[j] && cok) ? (const void*)(a.w + boff[j] + wofs) : (const void*)g_zero_page;
-      __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(sB + (wid * (BN / 4) + j * 8) * ROWB), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(sB + (wid * (BN / NW) + j * 8) * ROWB), 16, 0, 0);
     }
     if (++is_c == cch) { is_c = 0; ++is_tap; }
   };
@@ -532,19 +534,20 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs a) {
   }
 }
 
-template <int MT, int NT, int ST>
+template <int MT, int NT, int ST, int WM = 2, int WN = 2>
 static void launch_conv_glds(const ConvArgs& a, hipStream_t s) {
+  constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN;
   const int M = a.B * a.OH * a.OW;
-  const int grid = cdiv(M, 32 * MT) * cdiv(a.Cout, 32 * NT);
-  const size_t lds = (size_t)ST * (32 * MT + 32 * NT) * 128 + 16;
+  const int grid = cdiv(M, BM) * cdiv(a.Cout, BN);
+  const size_t lds = (size_t)ST * (BM + BN) * 128 + 16;
   static bool attr_set = false;
   if (!attr_set) {
-    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_glds_kernel<MT, NT, ST>),
+    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_glds_kernel<MT, NT, ST, WM, WN>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
           "conv_glds attr");
     attr_set = true;
   }
-  hipLaunchKernelGGL((conv_glds_kernel<MT, NT, ST>), dim3(grid), dim3(256), lds, s, a);
+  hipLaunchKernelGGL((conv_glds_kernel<MT, NT, ST, WM, WN>), dim3(grid), dim3(64 * WM * WN), lds, s, a);
   check_launch("conv_glds");
 }
 
@@ -620,6 +623,15 @@ void conv_gemm(const ConvParams& p, hipStream_t s) {
     if (!glds_ok) throw std::invalid_argument("conv_gemm glds: tensor too large for 32-bit offsets or > 16 taps");
     if (variant == 3) dispatch_glds<3>(a, s);
     else dispatch_glds<2>(a, s);
+    return;
+  }
+  if (variant == 5 || variant == 6) {
+    // wide tiles, 8 waves (2 x 4): 128 x 256 (5) / 256 x 256 (6) -- the A (pixel)
+    // tile is fetched once for all 256 output channels of the ASPP-class layers,
+    // fewer L2->LDS bytes per MAC where per-CU fill bandwidth is the limit
+    if (!glds_ok) throw std::invalid_argument("conv_gemm glds: tensor too large for 32-bit offsets or > 16 taps");
+    if (variant == 5) launch_conv_glds<4, 4, 2, 2, 4>(a, s);
+    else launch_conv_glds<8, 4, 2, 2, 4>(a, s);
     return;
   }
   if (variant == 2) {

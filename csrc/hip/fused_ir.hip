@@ -242,7 +242,13 @@ struct IRTArgs {
   const bf16* in; const bf16* we; const float* be; const f16* wd; const f16* bd;
   const f16* wp; const float* bp; bf16* out;
   int B, IH, IW, Cin, hidP, Cout, OH, OW, stride, dil, residual, TY, TX, tiles_y, tiles_x;
+  long long* trace;  // debug: s_memtime stamps of workgroup 0 / wave 0 (null = off)
 };
+
+#define IR_STAMP(k)                                                                 \
+  do {                                                                              \
+    if (a.trace && blockIdx.x == 0 && threadIdx.x == 0) a.trace[k] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 
 template <int NSUB, int KS, int GPW, bool EXPAND, int NW>
 __global__ __launch_bounds__(64 * NW) void fused_ir_tile_kernel(IRTArgs a) {
@@ -264,6 +270,22 @@ __global__ __launch_bounds__(64 * NW) void fused_ir_tile_kernel(IRTArgs a) {
   const int iy0 = oy0 * s - dl, ix0 = ox0 * s - dl;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int r16 = lane & 15, kq = lane >> 4;
+  IR_STAMP(0);
+  // expansion weights are software-pipelined one chunk ahead: s_memtime timelines
+  // showed every chunk's expansion stalled ~2.5k cycles on these loads (L2 under
+  // load), longer than the chunk's MFMA + depthwise work
+  bf16x8 wfr_n[2][KS];
+  f32x4 bias_n[2];
+  auto load_expand_w = [&](int c) {
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const bf16* wrow = a.we + (size_t)(c + sub * 16 + r16) * CinP;
+#pragma unroll
+      for (int k = 0; k < KS; ++k) wfr_n[sub][k] = ld8(wrow + k * 32 + kq * 8);
+      bias_n[sub] = *reinterpret_cast<const f32x4*>(a.be + c + sub * 16 + kq * 4);
+    }
+  };
+  if (EXPAND) load_expand_w(0);  // overlaps the input-tile staging
 
   if (EXPAND) {
     constexpr int cpp = CinP / 8;
@@ -304,12 +326,14 @@ __global__ __launch_bounds__(64 * NW) void fused_ir_tile_kernel(IRTArgs a) {
   }
   __syncthreads();
 
+  IR_STAMP(1);
   f32x4 acc[GPW][NSUB];
 #pragma unroll
   for (int g = 0; g < GPW; ++g)
 #pragma unroll
     for (int n = 0; n < NSUB; ++n) acc[g][n] = f32x4{0.f, 0.f, 0.f, 0.f};
   const f16x8 h0 = {0, 0, 0, 0, 0, 0, 0, 0}, h6 = {6, 6, 6, 6, 6, 6, 6, 6};
+
 
   for (int c0 = 0; c0 < a.hidP; c0 += 32) {
     // this chunk's depthwise / projection weights: issued first, in flight under the expansion
@@ -328,10 +352,9 @@ __global__ __launch_bounds__(64 * NW) void fused_ir_tile_kernel(IRTArgs a) {
       f32x4 bias[2];
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
-        const bf16* wrow = a.we + (size_t)(c0 + sub * 16 + r16) * CinP;
 #pragma unroll
-        for (int k = 0; k < KS; ++k) wfr[sub][k] = ld8(wrow + k * 32 + kq * 8);
-        bias[sub] = *reinterpret_cast<const f32x4*>(a.be + c0 + sub * 16 + kq * 4);
+        for (int k = 0; k < KS; ++k) wfr[sub][k] = wfr_n[sub][k];
+        bias[sub] = bias_n[sub];
       }
       for (int gi = wid; gi < in_groups; gi += NW) {
         const int ip = gi * 16 + r16;
@@ -353,7 +376,10 @@ __global__ __launch_bounds__(64 * NW) void fused_ir_tile_kernel(IRTArgs a) {
           *reinterpret_cast<f16x4*>(E + (size_t)ip * ES + sub * 16 + kq * 4) = o;
         }
       }
+      IR_STAMP(2 + 4 * (c0 / 32));
       __syncthreads();
+      IR_STAMP(3 + 4 * (c0 / 32));
+      if (c0 + 32 < a.hidP) load_expand_w(c0 + 32);  // in flight under depthwise + projection
     }
 
     // ---- depthwise (packed fp16): lane -> 8 channels (kq*8..) of its pixel in each group
@@ -376,14 +402,17 @@ __global__ __launch_bounds__(64 * NW) void fused_ir_tile_kernel(IRTArgs a) {
 #pragma unroll
     for (int g = 0; g < GPW; ++g) d[g] = __builtin_elementwise_min(__builtin_elementwise_max(d[g], h0), h6);
 
+    IR_STAMP(4 + 4 * (c0 / 32));
     // ---- project chunk (fp16 MFMA, fp32 accumulate)
 #pragma unroll
     for (int n = 0; n < NSUB; ++n)
 #pragma unroll
       for (int g = 0; g < GPW; ++g)
         acc[g][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[n], d[g], acc[g][n], 0, 0, 0);
+    IR_STAMP(5 + 4 * (c0 / 32));
     if (EXPAND) __syncthreads();  // E is rewritten by the next chunk
   }
+  IR_STAMP(126);
 
 #pragma unroll
   for (int g = 0; g < GPW; ++g) {
@@ -456,7 +485,7 @@ void fused_ir_tile(const FusedIRParams& p, hipStream_t st) {
   IRTArgs a{p.in, p.we, p.be, reinterpret_cast<const f16*>(p.wd_h), reinterpret_cast<const f16*>(p.bd_h),
             reinterpret_cast<const f16*>(p.wp_h), p.bp, p.out, p.B, p.IH, p.IW, p.Cin, p.hidP,
             p.Cout, p.OH, p.OW, p.stride, p.dil, p.residual, p.TY, p.TX,
-            cdiv(p.OH, p.TY), cdiv(p.OW, p.TX)};
+            cdiv(p.OH, p.TY), cdiv(p.OW, p.TX), p.trace};
   const int nsub = (p.Cout + 15) / 16, ks = p.CinP / 32;
   if (!ex) {
     if (nsub == 1) {

@@ -19,7 +19,7 @@ struct ConvParams {
   int B = 0, IH = 0, IW = 0, Cin = 0, OH = 0, OW = 0, Cout = 0;
   int KH = 1, KW = 1, stride = 1, dil = 1;
   int ldo = 0, co_off = 0, ldr = 0, act = 0;
-  int variant = 0;  // 0 auto, 1 direct (register-fed), 2 LDS-staged, 3/4 LDS-DMA 3/2-stage
+  int variant = 0;  // 0 auto, 1 direct, 2 LDS-staged, 3/4 LDS-DMA 3/2-stage, 5/6 LDS-DMA 128x256/256x256
 };
 void conv_gemm(const ConvParams& p, hipStream_t s);
 
@@ -68,6 +68,7 @@ struct FusedIRParams {
   const void* wd_h = nullptr;
   const void* bd_h = nullptr;
   const void* wp_h = nullptr;
+  long long* trace = nullptr;  // debug timeline (128 slots), tile kernel only
 };
 void fused_inverted_residual(const FusedIRParams& p, hipStream_t s);
 // LDS bytes the tile kernel needs for a (TY, TX) tile (0 if the shape is unsupported).

@@ -46,7 +46,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default=None)
-    ap.add_argument("--variants", default="1,2,3,4")
+    ap.add_argument("--variants", default="1,4,5,6")
     a = ap.parse_args()
     dev = torch.device("cuda")
     variants = [int(v) for v in a.variants.split(",")]

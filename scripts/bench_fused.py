@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--tiles", default="5x11,11x11,8x16")
+    ap.add_argument("--trace", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda")
     _, specs = mnv2_block_specs(1.0, 16)
@@ -60,6 +61,14 @@ def main():
         en.record()
         torch.cuda.synchronize()
         print(f"  tile {t}: {st.elapsed_time(en) * 1e3 / a.reps:8.1f} us", flush=True)
+        if a.trace:
+            tr = torch.zeros(128, dtype=torch.int64, device=dev)
+            K.fused_ir(x, P, out, B=B, IH=H, IW=H, OH=OH, OW=OH, tile=(ty, tx), trace=tr)
+            torch.cuda.synchronize()
+            v = tr.cpu().numpy()
+            t0 = v[0]
+            marks = [(i, int(v[i] - t0)) for i in range(128) if v[i]]
+            print("    timeline (s_memtime ticks since start):", marks[:40])
 
 
 if __name__ == "__main__":

@@ -138,9 +138,36 @@ def v2_file_descriptor() -> descriptor_pb2.FileDescriptorProto:
     return fd
 
 
+HEALTH_SERVICE = "grpc.health.v1.Health"
+
+
+def health_file_descriptor() -> descriptor_pb2.FileDescriptorProto:
+    """The standard gRPC health-checking protocol (grpc/health/v1/health.proto),
+    so stock probes (grpc_health_probe, load balancers, k8s) can query the server
+    without grpcio-health-checking installed."""
+    fd = descriptor_pb2.FileDescriptorProto()
+    fd.name = "grpc/health/v1/health.proto"
+    fd.package = "grpc.health.v1"
+    fd.syntax = "proto3"
+    m = fd.message_type.add(); m.name = "HealthCheckRequest"
+    _field(m, "service", 1, F.TYPE_STRING)
+    m = fd.message_type.add(); m.name = "HealthCheckResponse"
+    e = m.enum_type.add(); e.name = "ServingStatus"
+    for i, n in enumerate(["UNKNOWN", "SERVING", "NOT_SERVING", "SERVICE_UNKNOWN"]):
+        v = e.value.add(); v.name = n; v.number = i
+    _field(m, "status", 1, F.TYPE_ENUM,
+           type_name=".grpc.health.v1.HealthCheckResponse.ServingStatus")
+    svc = fd.service.add(); svc.name = "Health"
+    _method(svc, "Check", ".grpc.health.v1.HealthCheckRequest", ".grpc.health.v1.HealthCheckResponse")
+    w = _method(svc, "Watch", ".grpc.health.v1.HealthCheckRequest", ".grpc.health.v1.HealthCheckResponse")
+    w.server_streaming = True
+    return fd
+
+
 POOL = descriptor_pool.DescriptorPool()
 _V1_FD = POOL.Add(v1_file_descriptor())
 _V2_FD = POOL.Add(v2_file_descriptor())
+_HEALTH_FD = POOL.Add(health_file_descriptor())
 
 
 def _cls(full_name: str):
@@ -163,6 +190,10 @@ StreamList = _cls("sem_seg_server.v2.StreamList")
 Stats = _cls("sem_seg_server.v2.Stats")
 HealthStatus = _cls("sem_seg_server.v2.HealthStatus")
 
+# ---- grpc.health.v1 ---------------------------------------------------------
+HealthCheckRequest = _cls("grpc.health.v1.HealthCheckRequest")
+HealthCheckResponse = _cls("grpc.health.v1.HealthCheckResponse")
+
 V1_METHODS = {
     "GetSegmentedObjects": (Empty, SegmentedObjectData),
     "GetCameraResolution": (Empty, CameraResolution),
@@ -180,4 +211,5 @@ def file_descriptor_set_bytes() -> bytes:
     s = descriptor_pb2.FileDescriptorSet()
     s.file.add().CopyFrom(v1_file_descriptor())
     s.file.add().CopyFrom(v2_file_descriptor())
+    s.file.add().CopyFrom(health_file_descriptor())
     return s.SerializeToString()

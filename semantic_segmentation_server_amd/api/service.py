@@ -122,6 +122,64 @@ def add_v2_servicer(servicer, server) -> None:
         (grpc.method_handlers_generic_handler(P.V2_SERVICE, _handlers(servicer, P.V2_METHODS)),))
 
 
+class HealthServicer:
+    """grpc.health.v1.Health. ``status_fn(service) -> bool | None`` (None = unknown
+    service); "" and the two segmentation services are known. Watch streams the
+    status whenever it changes (polled every ``watch_period`` s) until cancelled."""
+
+    KNOWN = ("", P.V1_SERVICE, P.V2_SERVICE)
+
+    def __init__(self, status_fn: Optional[Callable[[str], Optional[bool]]] = None,
+                 watch_period: float = 0.5):
+        self.status_fn = status_fn or (lambda service: True)
+        self.watch_period = watch_period
+
+    def _status(self, service: str) -> int:
+        R = P.HealthCheckResponse
+        if service not in self.KNOWN:
+            return R.SERVICE_UNKNOWN
+        ok = self.status_fn(service)
+        return R.UNKNOWN if ok is None else (R.SERVING if ok else R.NOT_SERVING)
+
+    def Check(self, request, context):
+        st = self._status(request.service)
+        if st == P.HealthCheckResponse.SERVICE_UNKNOWN:
+            context.set_code(grpc.StatusCode.NOT_FOUND)
+            context.set_details(f"unknown service {request.service!r}")
+        return P.HealthCheckResponse(status=st)
+
+    def Watch(self, request, context):
+        last = None
+        while context.is_active():
+            st = self._status(request.service)
+            if st != last:
+                yield P.HealthCheckResponse(status=st)
+                last = st
+            time.sleep(self.watch_period)
+
+
+def add_health_servicer(servicer: HealthServicer, server) -> None:
+    handlers = {
+        "Check": grpc.unary_unary_rpc_method_handler(
+            servicer.Check, request_deserializer=P.HealthCheckRequest.FromString,
+            response_serializer=P.HealthCheckResponse.SerializeToString),
+        "Watch": grpc.unary_stream_rpc_method_handler(
+            servicer.Watch, request_deserializer=P.HealthCheckRequest.FromString,
+            response_serializer=P.HealthCheckResponse.SerializeToString),
+    }
+    server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(P.HEALTH_SERVICE, handlers),))
+
+
+class HealthStub:
+    def __init__(self, channel):
+        self.Check = channel.unary_unary(
+            f"/{P.HEALTH_SERVICE}/Check", request_serializer=P.HealthCheckRequest.SerializeToString,
+            response_deserializer=P.HealthCheckResponse.FromString)
+        self.Watch = channel.unary_stream(
+            f"/{P.HEALTH_SERVICE}/Watch", request_serializer=P.HealthCheckRequest.SerializeToString,
+            response_deserializer=P.HealthCheckResponse.FromString)
+
+
 class _Stub:
     def __init__(self, channel, service: str, methods: Dict[str, tuple]):
         for name, (req, resp) in methods.items():

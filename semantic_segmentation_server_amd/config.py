@@ -64,6 +64,10 @@ class Config:
     metrics_dump: Optional[str] = None
     log_level: str = "INFO"
     inject_fault: Optional[str] = None     # "rank:step" fault injection for tests
+    rank_timeout: float = 300.0            # process-group collective timeout (s)
+    degrade: bool = True                   # rank 0 keeps serving alone when a peer rank is lost
+    debug_dump: Optional[str] = None       # directory for annotated PNG frames (reference :196-205)
+    debug_every: int = 0                   # dump every N-th frame (0 = off)
 
     @property
     def min_area(self) -> float:
@@ -125,6 +129,12 @@ def add_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--metrics_dump", default=d.metrics_dump)
     p.add_argument("--log_level", default=d.log_level)
     p.add_argument("--inject_fault", default=d.inject_fault)
+    p.add_argument("--rank_timeout", type=float, default=d.rank_timeout)
+    p.add_argument("--no_degrade", dest="degrade", action="store_false",
+                   help="exit instead of serving from rank 0 alone when a peer rank is lost")
+    p.add_argument("--debug_dump", default=d.debug_dump,
+                   help="write annotated PNG frames here (contours, centroids, labels)")
+    p.add_argument("--debug_every", type=int, default=d.debug_every)
     return p
 
 

@@ -85,7 +85,7 @@ def conv_gemm(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out: torch.T
     return out
 
 
-def fused_ir(x, packed: dict, out, *, B, IH, IW, OH, OW, tile=None):
+def fused_ir(x, packed: dict, out, *, B, IH, IW, OH, OW, tile=None, trace=None):
     """Fused inverted residual. ``packed`` from ``pack_fused_ir``.
 
     ``tile=(TY, TX)`` selects the general 2-D tile kernel (any dilation, Cin <= 160,
@@ -106,7 +106,8 @@ def fused_ir(x, packed: dict, out, *, B, IH, IW, OH, OW, tile=None):
     _hip_mod().fused_ir(_ptr(x), _ptr(P["we"]), _ptr(P["be"]), _ptr(P["wd"]), _ptr(P["bd"]),
                         _ptr(P["wp"]), _ptr(P["bp"]), _ptr(out), B, IH, IW, P["Cin"], P["CinP"],
                         P["hidP"], P["Cout"], OH, OW, P["stride"], int(P["residual"]), _stream(),
-                        P.get("dil", 1), TY, TX, _ptr(P["wd_h"]), _ptr(P["bd_h"]), _ptr(P["wp_h"]))
+                        P.get("dil", 1), TY, TX, _ptr(P["wd_h"]), _ptr(P["bd_h"]), _ptr(P["wp_h"]),
+                        _ptr(trace))
     _dbg('fused_ir')
     return out
 

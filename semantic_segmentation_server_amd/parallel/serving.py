@@ -10,11 +10,14 @@ metadata are RCCL-gathered to rank 0, which pushes them into the per-stream
 result hub behind the v1/v2 services. With ``--ingest scatter`` rank 0 owns the
 sources for the whole node and RCCL-scatters frames instead.
 
-Failure handling: every step ends with a tiny all-reduce that
-carries the stop flag and a liveness heartbeat; a rank whose source fails keeps
-stepping on its last good batch (logged) so collectives never hang; a process
-group timeout (``--rank_timeout``) surfaces as an exception, after which rank 0
-keeps serving the results it has and reports ``serving=False`` through Health.
+Failure handling: every step starts with a tiny all-reduce that
+carries the stop flag; a rank whose source fails keeps stepping on its last good
+batch (logged) so collectives never hang. When a peer rank is lost, the next
+collective fails (peer connection closed, or the ``--rank_timeout`` process-group
+timeout) and rank 0 switches to degraded mode: it drops the process group,
+re-shards onto itself (its own streams, local ingest) and keeps producing and
+serving; Health/grpc.health report ``ranks_alive = 1`` and the cause
+(``--no_degrade`` exits instead). A non-root rank that loses rank 0 exits.
 ``--inject_fault rank:step`` raises on that rank/step (used by tests).
 """
 from __future__ import annotations
@@ -45,7 +48,9 @@ class DistributedServer:
     def __init__(self, cfg: Config, ctx: Optional[D.DistContext] = None,
                  max_steps: Optional[int] = None):
         self.cfg = cfg
-        self.ctx = ctx or D.init()
+        self.ctx = ctx or D.init(timeout_s=cfg.rank_timeout)
+        self.run_ctx = self.ctx  # == ctx until degraded to rank 0 alone
+        self.degraded = False
         self.max_steps = max_steps
         self.metrics = Metrics()
         S_ = max(1, cfg.streams)
@@ -66,6 +71,7 @@ class DistributedServer:
         self.grpc_server = None
         self.port = None
         self._last = None
+        self._ingest = cfg.ingest
         self.fault = None
         if cfg.inject_fault:
             r, st = cfg.inject_fault.split(":")
@@ -85,10 +91,31 @@ class DistributedServer:
                    for r in range(self.ctx.world) for s in range(self.S)]
         S.add_v2_servicer(S.SemanticSegmentationV2Servicer(
             self.hub, labels, self.cfg.num_detections, streams, self.metrics,
-            lambda: (self.alive, self.ctx.world if self.alive else 0, self.ctx.world,
-                     self.error or "ok")), self.grpc_server)
+            self._health), self.grpc_server)
+        S.add_health_servicer(S.HealthServicer(lambda service: self.alive), self.grpc_server)
         self.grpc_server.start()
         log.info("rank 0 serving gRPC on port %d for %d ranks", self.port, self.ctx.world)
+
+    def _health(self):
+        alive = self.run_ctx.world if self.alive else 0
+        return self.alive, alive, self.ctx.world, self.error or "ok"
+
+    # ------------------------------------------------------------- degrade
+    def _degrade(self, err: BaseException) -> None:
+        """Peer lost: continue on rank 0 alone (local ingest, no collectives)."""
+        log.error("rank 0 lost a peer (%r): degrading to single-rank serving", err)
+        self.degraded = True
+        self.error = f"degraded to rank 0 alone after: {err!r}"
+        self.metrics.inc("degrade_events")
+        try:
+            D.destroy(self.ctx)
+        except Exception:  # the group may already be broken
+            pass
+        self.run_ctx = D.DistContext(0, 1, self.ctx.local_rank, self.ctx.device, None)
+        res = self.camera_res
+        self.pipe = DataParallelPipeline(self.run_ctx, self.engine, res[0], res[1], self.cfg.batch,
+                                         "local", self.hub, self.S)
+        self._ingest = "local"
 
     # ----------------------------------------------------------------- step
     def _gather_local(self):
@@ -96,8 +123,8 @@ class DistributedServer:
             return None, None, None, None
         per = [self.cfg.batch // self.S + (1 if s < self.cfg.batch % self.S else 0)
                for s in range(self.S)]
-        if self.cfg.ingest == "scatter":
-            per = [p * self.ctx.world for p in per]
+        if self._ingest == "scatter":
+            per = [p * self.run_ctx.world for p in per]
         imgs, ids, ts, strm = [], [], [], []
         for src, n in zip(self.sources, per):
             if n == 0:
@@ -130,17 +157,17 @@ class DistributedServer:
             frames, ids, ts, strm = self._gather_local()
         except StopIteration:
             stop, frames = 1.0, None
-        if D.allreduce_max(self.ctx, stop) > 0:
+        if D.allreduce_max(self.run_ctx, stop) > 0:
             return False
         if frames is not None:
             host = torch.from_numpy(np.ascontiguousarray(frames))
             if self.engine.is_cuda:
                 host = host.pin_memory()
             self.pipe.prefetch(host)
-        local_ids = ids if self.cfg.ingest == "local" else None
+        local_ids = ids if self._ingest == "local" else None
         recs = self.pipe.step(local_ids, ts if local_ids else None, strm if local_ids else None)
         dt = (time.perf_counter() - t0) * 1e3
-        n = self.cfg.batch * self.ctx.world
+        n = self.cfg.batch * self.run_ctx.world
         self.metrics.inc("frames", n)
         self.metrics.inc("objects", len(recs))
         self.metrics.observe("step_ms", dt)
@@ -150,18 +177,24 @@ class DistributedServer:
 
     def run(self, stop_event: Optional[threading.Event] = None) -> None:
         self.start_rpc()
-        try:
-            while True:
-                if stop_event is not None and stop_event.is_set():
-                    if D.allreduce_max(self.ctx, 1.0) > 0:
-                        break
-                if not self.step():
-                    break
-        except Exception as e:
-            self.alive = False
-            self.error = repr(e)
-            log.exception("rank %d stopped", self.ctx.rank)
-            raise
+        while True:
+            try:
+                while True:
+                    if stop_event is not None and stop_event.is_set():
+                        if D.allreduce_max(self.run_ctx, 1.0) > 0:
+                            return
+                    if not self.step():
+                        return
+            except Exception as e:
+                injected_here = self.fault is not None and self.fault[0] == self.ctx.rank
+                if (self.ctx.is_root and self.run_ctx.world > 1 and self.cfg.degrade
+                        and not injected_here):
+                    self._degrade(e)
+                    continue  # keep stepping on rank 0 alone
+                self.alive = False
+                self.error = repr(e)
+                log.exception("rank %d stopped", self.ctx.rank)
+                raise
 
     def stop(self) -> None:
         if self.grpc_server is not None:

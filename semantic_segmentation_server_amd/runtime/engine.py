@@ -50,7 +50,7 @@ def calibration_frames(H: int, W: int, n: int = 8, seed: int = 0) -> torch.Tenso
     src = SyntheticSource(640, 480, seed=seed + 101, pool=n)
     frames = torch.from_numpy(np.stack([next(src).image for _ in range(n)]).copy())
     lx, ly, *_ = R.letterbox_luts(640, 480, W, H)
-    return R.preprocess(frames, torch.from_numpy(lx), torch.from_numpy(ly))
+    return R.preprocess(frames, torch.from_numpy(np.array(lx)), torch.from_numpy(np.array(ly)))
 
 
 def _per_frame(streams, n: int) -> List[int]:
@@ -70,6 +70,14 @@ class Engine:
     def __init__(self, cfg: Config, device: Optional[torch.device] = None,
                  model: Optional[torch.nn.Module] = None):
         self.cfg = cfg
+        from ..utils.tracing import NULL_TRACER
+        self.tracer = NULL_TRACER  # Server / bench install a live one with --profile
+        self.debug = None
+        if cfg.debug_dump and cfg.debug_every > 0:
+            from ..utils.debug_dump import DebugDumper
+            self.debug = DebugDumper(cfg.debug_dump, cfg.debug_every, colormap_for(cfg.dataset),
+                                     load_labels(cfg.labels),
+                                     cfg.min_area_ratio * cfg.input_size * cfg.input_size)
         self.device = device or resolve_device(cfg.device)
         self.is_cuda = self.device.type == "cuda"
         self.H = self.W = int(cfg.input_size)
@@ -248,17 +256,28 @@ class Engine:
             frames = torch.from_numpy(np.ascontiguousarray(frames_host))
             with torch.no_grad():
                 labels = self._infer_eager(frames)
+            if self.debug is not None and self.debug.want():
+                self.debug.dump(frames_host[0], labels[0].numpy(), self.crop_w, self.crop_h,
+                                _per_frame(streams, len(frame_ids))[0], int(frame_ids[0]))
             return self.records_from_labels(labels, frame_ids, ts, streams)
+        tr = self.tracer
         with torch.cuda.stream(self.stream):
-            frames = torch.from_numpy(np.ascontiguousarray(frames_host)).pin_memory() \
-                .to(self.device, non_blocking=True)
-            labels, post = self.run_device(frames)
+            with tr.stage("h2d", self.stream):
+                frames = torch.from_numpy(np.ascontiguousarray(frames_host)).pin_memory() \
+                    .to(self.device, non_blocking=True)
+            with tr.stage("model+post", self.stream):
+                labels, post = self.run_device(frames)
             if post is not None:
-                recs = self._hip_post.fetch(post, frame_ids, ts, _per_frame(streams, len(frame_ids)),
-                                            self.W, self.H)
+                with tr.stage("d2h+records", self.stream):
+                    recs = self._hip_post.fetch(post, frame_ids, ts,
+                                                _per_frame(streams, len(frame_ids)), self.W, self.H)
             else:
                 recs = None
         self.stream.synchronize()
+        if self.debug is not None and self.debug.want():
+            self.debug.dump(frames_host[0], labels[0].cpu().numpy(), self.crop_w, self.crop_h,
+                            _per_frame(streams, len(frame_ids))[0], int(frame_ids[0]))
         if recs is None:
-            recs = self.records_from_labels(labels, frame_ids, ts, streams)
+            with tr.stage("host_post"):
+                recs = self.records_from_labels(labels, frame_ids, ts, streams)
         return recs

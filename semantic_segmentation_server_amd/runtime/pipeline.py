@@ -71,9 +71,16 @@ class Producer(threading.Thread):
                 break
             try:
                 t0 = time.perf_counter()
-                frames, ids, ts, streams = self._gather()
+                tr = getattr(self.engine, "tracer", None)
+                if tr is None:
+                    from ..utils.tracing import NULL_TRACER as tr
+                with tr.stage("capture"):
+                    frames, ids, ts, streams = self._gather()
                 recs = self.engine.step(frames, ids, ts, streams)
-                self.hub.push_records(recs)
+                with tr.stage("publish"):
+                    self.hub.push_records(recs)
+                self.metrics.observe("objects_per_frame", len(recs) / max(1, len(ids)))
+                self.metrics.observe("buffer_depth", self.hub.depth)
                 dt = (time.perf_counter() - t0) * 1e3
                 self.metrics.observe("frame_ms", dt / len(ids))
                 self.metrics.observe("step_ms", dt)

@@ -43,6 +43,9 @@ class Server:
         self.camera_res = probe_resolution(cfg.source, cfg.camera_idx, cfg.camera_width,
                                            cfg.camera_height, cfg.source_path)
         self.engine = engine or Engine(cfg)
+        from .utils.tracing import Tracer
+        self.tracer = Tracer(self.metrics, enabled=cfg.profile)
+        self.engine.tracer = self.tracer
         self.sources = [make_source(cfg.source, s, cfg.camera_idx, cfg.camera_width,
                                     cfg.camera_height, cfg.source_path, fps=cfg.fps_limit,
                                     seed=cfg.seed) for s in range(cfg.streams)]
@@ -57,6 +60,7 @@ class Server:
                                                    streams, self.metrics, self._health)
         S.add_v1_servicer(self.v1, self.grpc_server)
         S.add_v2_servicer(self.v2, self.grpc_server)
+        S.add_health_servicer(S.HealthServicer(lambda service: self._health()[0]), self.grpc_server)
 
     def _health(self):
         alive = self.producer.is_alive() and (time.time() - self.producer.alive_ts) < 30

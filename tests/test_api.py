@@ -145,3 +145,34 @@ def test_grpc_loopback_v1_and_v2():
             assert v2.GetStats(P.Empty()).buffer_depth == 0
     finally:
         server.stop(0)
+
+
+def test_grpc_health_v1():
+    state = {"ok": True}
+    server, port = S.make_server(4, 0, "127.0.0.1")
+    S.add_health_servicer(S.HealthServicer(lambda service: state["ok"], watch_period=0.05), server)
+    server.start()
+    try:
+        with grpc.insecure_channel(f"127.0.0.1:{port}") as ch:
+            h = S.HealthStub(ch)
+            R = P.HealthCheckResponse
+            assert h.Check(P.HealthCheckRequest(service="")).status == R.SERVING
+            assert h.Check(P.HealthCheckRequest(service=P.V1_SERVICE)).status == R.SERVING
+            with pytest.raises(grpc.RpcError) as ei:
+                h.Check(P.HealthCheckRequest(service="nope"))
+            assert ei.value.code() == grpc.StatusCode.NOT_FOUND
+            state["ok"] = False
+            assert h.Check(P.HealthCheckRequest()).status == R.NOT_SERVING
+            it = h.Watch(P.HealthCheckRequest())
+            assert next(it).status == R.NOT_SERVING
+            state["ok"] = True
+            assert next(it).status == R.SERVING
+            it.cancel()
+    finally:
+        server.stop(0)
+
+
+def test_health_descriptor_matches_standard_wire_format():
+    # grpc.health.v1.HealthCheckResponse{status = SERVING(1)} -> 08 01
+    assert P.HealthCheckResponse(status=1).SerializeToString() == b"\x08\x01"
+    assert P.HealthCheckRequest(service="x").SerializeToString() == b"\x0a\x01x"

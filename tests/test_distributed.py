@@ -144,3 +144,48 @@ def test_distributed_server_cpu():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert n == 3 and streams == [0, 1, 2, 3] and world == 2 and steps == 3 and frames == 12
+
+
+def _degrade_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import grpc
+    from semantic_segmentation_server_amd import config as C
+    from semantic_segmentation_server_amd.api import proto as P
+    from semantic_segmentation_server_amd.api.service import HealthStub, SemanticSegmentationV2Stub
+    from semantic_segmentation_server_amd.parallel import dist as D
+    from semantic_segmentation_server_amd.parallel.serving import DistributedServer
+    ctx = D.init("gloo", timeout_s=60)
+    cfg = C.parse(["--port", "0", "--host", "127.0.0.1", "--device", "cpu", "--input_size", "65",
+                   "--batch", "2", "--streams", "1", "--gpus", str(world),
+                   "--inject_fault", "1:2", "--rank_timeout", "60"])
+    srv = DistributedServer(cfg, ctx, max_steps=6)
+    try:
+        srv.run()
+    except RuntimeError:
+        if rank == 1:
+            os._exit(0)  # the lost rank: drop its connections abruptly
+        raise
+    with grpc.insecure_channel(f"127.0.0.1:{srv.port}") as ch:
+        h = SemanticSegmentationV2Stub(ch).Health(P.Empty())
+        g = HealthStub(ch).Check(P.HealthCheckRequest())
+    q.put((srv.steps, srv.degraded, h.ranks_alive, h.world_size, h.detail, g.status,
+           srv.metrics.snapshot()["frames"]))
+    srv.stop()
+
+
+def test_rank_loss_degrades_to_rank0():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_degrade_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    steps, degraded, alive, world, detail, status, frames = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert degraded and steps == 6 and alive == 1 and world == 2 and "degraded" in detail
+    assert status == 1  # SERVING
+    # 2 lock-step steps on 2 ranks (4 frames each), then 4 steps on rank 0 alone (2 frames each)
+    assert frames == 2 * 4 + 4 * 2

@@ -50,7 +50,7 @@ def _nchw(x):
     (2, 65, 65, 144, 32, 1, 1, 1, None, False, 0, 0),
     (1, 33, 33, 1024, 256, 1, 1, 1, "relu", False, 0, 0),
 ])
-@pytest.mark.parametrize("variant", [1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6])
 def test_conv_gemm(B, H, W, Cin, Cout, k, stride, dil, act, res, ldo_pad, co_off, variant):
     K = _hip()
     g = torch.Generator(device="cpu").manual_seed(1)

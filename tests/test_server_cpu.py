@@ -67,3 +67,29 @@ def test_exact_and_fast_contour_modes_agree_cpu():
     a = e_fast.step(f, [0], [0.0], 0)
     b = e_exact.step(f, [0], [0.0], 0)
     assert a.tolist() == b.tolist() and len(a) == 2
+
+
+def test_debug_dump_writes_annotated_png(tmp_path):
+    from PIL import Image
+    from semantic_segmentation_server_amd import config as C
+    from semantic_segmentation_server_amd.labels import load_labels, pascal_colormap
+    from semantic_segmentation_server_amd.utils.debug_dump import render
+    lab = np.zeros((129, 129), np.uint8)
+    lab[20:80, 30:100] = 15
+    lab[40:60, 50:70] = 0
+    frame = np.full((96, 128, 3), 90, np.uint8)
+    im = render(frame, lab, 129, 96, pascal_colormap(), load_labels(), min_area=50.0)
+    assert im.size == (129, 96)
+    a = np.asarray(im)
+    assert (a == [0, 255, 0]).all(-1).sum() > 100      # contour outlines drawn
+    assert (a == [255, 0, 0]).all(-1).sum() > 4        # centroid marker
+    # engine hook: --debug_dump / --debug_every on the CPU path
+    import torch
+    from semantic_segmentation_server_amd.runtime.engine import Engine
+    cfg = C.parse(["--device", "cpu", "--input_size", "65", "--debug_dump", str(tmp_path),
+                   "--debug_every", "1"])
+    e = Engine(cfg, torch.device("cpu"))
+    e.step(np.full((1, 48, 64, 3), 128, np.uint8), [7], [0.0], 3)
+    files = sorted(p.name for p in tmp_path.iterdir())
+    assert files == ["s003_f00000007.png"]
+    assert Image.open(tmp_path / files[0]).size[0] > 0
