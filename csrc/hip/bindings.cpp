@@ -60,6 +60,18 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("TY") = 0, py::arg("TX") = 0, py::arg("wd_h") = 0, py::arg("bd_h") = 0,
         py::arg("wp_h") = 0, py::arg("trace") = 0);
   m.def("fused_ir_tile_lds", &fused_ir_tile_lds);
+  m.def("stem_block0",
+        [](uintptr_t frames, uintptr_t lx, uintptr_t ly, uintptr_t ws, uintptr_t bs, uintptr_t wd,
+           uintptr_t bd, uintptr_t wp, uintptr_t bp, uintptr_t out, int B, int Hc, int Wc, int H,
+           int W, int SH, int SW, int Cout, int TY, int TX, uintptr_t stream) {
+          StemBlock0Params p;
+          p.frames = P<const uint8_t>(frames); p.lut_x = P<const int32_t>(lx); p.lut_y = P<const int32_t>(ly);
+          p.ws = P<const bf16>(ws); p.bs = P<const float>(bs); p.wd = P<const void>(wd);
+          p.bd = P<const void>(bd); p.wp = P<const void>(wp); p.bp = P<const float>(bp); p.out = P<bf16>(out);
+          p.B = B; p.Hc = Hc; p.Wc = Wc; p.H = H; p.W = W; p.SH = SH; p.SW = SW; p.Cout = Cout;
+          p.TY = TY; p.TX = TX;
+          stem_block0(p, S(stream));
+        });
 
   m.def("dw_project",
         [](uintptr_t hid_in, uintptr_t wd, uintptr_t bd, uintptr_t wp, uintptr_t bp, uintptr_t res,

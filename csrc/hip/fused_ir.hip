@@ -442,6 +442,135 @@ __global__ __launch_bounds__(64 * NW) void fused_ir_tile_kernel(IRTArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Stem + first inverted residual in one kernel (MobileNetV2 blocks 0: no
+// expansion, dw 3x3 on the 32 stem channels, project 32 -> 16). The 257^2 x 32
+// stem activation (135 MB per 32 frames) is the largest tensor of the network and
+// this fusion never writes it: per TY x TX output tile, the letterboxed camera
+// pixels under the tile's receptive field are gathered through the LUTs into LDS
+// (normalised, bf16), the stem conv runs on MFMA (K = 3x3x3 = 27 padded to 32:
+// one v_mfma_f32_16x16x32_bf16 per 16 pixels x 16 channels) over the tile plus its
+// 1-pixel halo, relu6 in fp16 into LDS, then the tile kernel's packed-fp16
+// depthwise and fp16-MFMA projection.
+struct SB0Args {
+  const uint8_t* frames; const int32_t* lut_x; const int32_t* lut_y;
+  const bf16* ws;  // stem weights [32 out][32 K] bf16, K = (ky*3 + kx)*3 + c (RGB), zero-padded
+  const float* bs; // stem bias [32]
+  const f16* wd; const f16* bd;  // depthwise [9][32], [32] fp16
+  const f16* wp;   // projection [16][32] fp16
+  const float* bp; // [16]
+  bf16* out;       // [B, SH, SW, Cout]
+  int B, Hc, Wc, H, W, SH, SW, Cout, TY, TX, tiles_y, tiles_x;
+};
+
+template <int GPW>
+__global__ __launch_bounds__(256) void stem_block0_kernel(SB0Args a) {
+  constexpr int ES = 32 + 8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int SHT = a.TY + 2, SWT = a.TX + 2;        // stem tile incl. halo
+  const int IHT = 2 * SHT + 1, IWT = 2 * SWT + 1;  // model-input region
+  const int s_px = SHT * SWT, s_groups = (s_px + 15) / 16;
+  bf16* IN = reinterpret_cast<bf16*>(smem);                                   // [IHT*IWT][4]
+  f16* E = reinterpret_cast<f16*>(smem + ((size_t)IHT * IWT * 8 + 15) / 16 * 16);  // [s_groups*16][ES]
+  const int ntile = a.tiles_y * a.tiles_x;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = bid / ntile, t = bid % ntile;
+  const int oy0 = (t / a.tiles_x) * a.TY, ox0 = (t % a.tiles_x) * a.TX;
+  const int sy0 = oy0 - 1, sx0 = ox0 - 1;           // stem tile origin
+  const int iy0 = 2 * sy0 - 1, ix0 = 2 * sx0 - 1;   // input region origin
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+
+  const uint8_t* fb = a.frames + (size_t)b * a.Hc * a.Wc * 3;
+  for (int i = tid; i < IHT * IWT; i += 256) {
+    const int y = iy0 + i / IWT, x = ix0 + i % IWT;
+    float rgb[3] = {0.f, 0.f, 0.f};  // conv zero padding outside the model input
+    if (y >= 0 && y < a.H && x >= 0 && x < a.W) {
+      const int sy = a.lut_y[y], sx = a.lut_x[x];
+      if (sy >= 0 && sx >= 0) {
+        const uint8_t* px = fb + ((size_t)sy * a.Wc + sx) * 3;
+        rgb[0] = px[2] * (1.f / 127.5f) - 1.f;  // BGR -> RGB
+        rgb[1] = px[1] * (1.f / 127.5f) - 1.f;
+        rgb[2] = px[0] * (1.f / 127.5f) - 1.f;
+      } else {
+        rgb[0] = rgb[1] = rgb[2] = -1.f;  // letterbox padding: uint8 0 -> -1
+      }
+    }
+    bf16x4 v = {(bf16)rgb[0], (bf16)rgb[1], (bf16)rgb[2], (bf16)0.f};
+    *reinterpret_cast<bf16x4*>(IN + (size_t)i * 4) = v;
+  }
+  // stem weights (A operand): rows = out channels sub*16 + r16, K = kq*8 .. +7
+  bf16x8 wst[2];
+  f32x4 bst[2];
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub) {
+    wst[sub] = ld8(a.ws + (size_t)(sub * 16 + r16) * 32 + kq * 8);
+    bst[sub] = *reinterpret_cast<const f32x4*>(a.bs + sub * 16 + kq * 4);
+  }
+  // per-lane K gather offsets into IN (relative to the stem pixel's window origin)
+  int koff[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = kq * 8 + e;
+    const int tap = k / 3, c = k % 3;
+    koff[e] = k < 27 ? (((tap / 3) * IWT + (tap % 3)) * 4 + c) : -1;
+  }
+  __syncthreads();
+  const f16x4 z4 = {0, 0, 0, 0}, s4 = {6, 6, 6, 6};
+  for (int gi = wid; gi < s_groups; gi += 4) {
+    const int sp = gi * 16 + r16;
+    const int ty = sp / SWT, tx = sp - ty * SWT;
+    const int sy = sy0 + ty, sx = sx0 + tx;
+    const bool inside = sp < s_px && sy >= 0 && sy < a.SH && sx >= 0 && sx < a.SW;
+    const int base = sp < s_px ? ((2 * ty) * IWT + 2 * tx) * 4 : 0;
+    bf16x8 xf;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) xf[e] = koff[e] >= 0 ? IN[base + koff[e]] : (bf16)0.f;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      f32x4 e4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wst[sub], xf, bst[sub], 0, 0, 0);
+      f16x4 o = {(f16)e4[0], (f16)e4[1], (f16)e4[2], (f16)e4[3]};
+      o = __builtin_elementwise_min(__builtin_elementwise_max(o, z4), s4);
+      if (!inside) o = z4;  // depthwise zero padding outside the stem image
+      *reinterpret_cast<f16x4*>(E + (size_t)sp * ES + sub * 16 + kq * 4) = o;
+    }
+  }
+  // depthwise / projection weights
+  f16x8 wdv[9];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) wdv[tap] = *reinterpret_cast<const f16x8*>(a.wd + tap * 32 + kq * 8);
+  const f16x8 bdv = *reinterpret_cast<const f16x8*>(a.bd + kq * 8);
+  const f16x8 af = *reinterpret_cast<const f16x8*>(a.wp + (size_t)r16 * 32 + kq * 8);
+  __syncthreads();
+  const f16x8 h0 = {0, 0, 0, 0, 0, 0, 0, 0}, h6 = {6, 6, 6, 6, 6, 6, 6, 6};
+#pragma unroll
+  for (int g = 0; g < GPW; ++g) {
+    const int p = (wid * GPW + g) * 16 + r16;
+    const int py = p / a.TX, px = p - py * a.TX;
+    const int oy = oy0 + py, ox = ox0 + px;
+    const bool valid = p < a.TY * a.TX && oy < a.SH && ox < a.SW;
+    const int pofs = valid ? py * SWT + px : 0;
+    f16x8 v[9];
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+      v[tap] = *reinterpret_cast<const f16x8*>(E + (size_t)(pofs + (tap / 3) * SWT + tap % 3) * ES + kq * 8);
+    f16x8 d = bdv;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) d = v[tap] * wdv[tap] + d;
+    d = __builtin_elementwise_min(__builtin_elementwise_max(d, h0), h6);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, d, acc, 0, 0, 0);
+    if (!valid) continue;
+    const int co = kq * 4;
+    if (co >= a.Cout) continue;
+    bf16* op = a.out + (((size_t)b * a.SH + oy) * a.SW + ox) * a.Cout + co;
+    bf16x4 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = (bf16)(acc[q] + a.bp[co + q]);
+    *reinterpret_cast<bf16x4*>(op) = o;
+  }
+}
+
 size_t tile_lds_bytes(int CinP, int stride, int dil, int TY, int TX, bool expand = true) {
   const int in_px = ((TY - 1) * stride + 2 * dil + 1) * ((TX - 1) * stride + 2 * dil + 1);
   return (size_t)((in_px + 15) / 16) * 16 * ((expand ? CinP + 8 : 0) + 40) * 2;
@@ -505,6 +634,25 @@ void fused_ir_tile(const FusedIRParams& p, hipStream_t st) {
 }
 
 }  // namespace
+
+void stem_block0(const StemBlock0Params& p, hipStream_t st) {
+  if (p.Cout != 16) throw std::invalid_argument("stem_block0: block 0 must project to 16 channels");
+  if (p.TY < 1 || p.TX < 1 || (p.TY * p.TX + 15) / 16 > 8) throw std::invalid_argument("stem_block0: bad tile");
+  if (p.SH != (p.H - 1) / 2 + 1 || p.SW != (p.W - 1) / 2 + 1) throw std::invalid_argument("stem_block0: bad stem size");
+  SB0Args a{p.frames, p.lut_x, p.lut_y, p.ws, p.bs, reinterpret_cast<const f16*>(p.wd),
+            reinterpret_cast<const f16*>(p.bd), reinterpret_cast<const f16*>(p.wp), p.bp, p.out,
+            p.B, p.Hc, p.Wc, p.H, p.W, p.SH, p.SW, p.Cout, p.TY, p.TX, cdiv(p.SH, p.TY), cdiv(p.SW, p.TX)};
+  const int SHT = p.TY + 2, SWT = p.TX + 2;
+  const size_t lds = ((size_t)(2 * SHT + 1) * (2 * SWT + 1) * 8 + 15) / 16 * 16 +
+                     (size_t)((SHT * SWT + 15) / 16) * 16 * 40 * 2;
+  const int grid = p.B * a.tiles_y * a.tiles_x;
+  const int groups = (p.TY * p.TX + 15) / 16;
+  if (groups <= 4)
+    hipLaunchKernelGGL(stem_block0_kernel<1>, dim3(grid), dim3(256), lds, st, a);
+  else
+    hipLaunchKernelGGL(stem_block0_kernel<2>, dim3(grid), dim3(256), lds, st, a);
+  check_launch("stem_block0");
+}
 
 size_t fused_ir_tile_lds(int CinP, int stride, int dil, int TY, int TX, int expand) {
   return tile_lds_bytes(CinP, stride, dil, TY, TX, expand != 0);

@@ -71,6 +71,17 @@ struct FusedIRParams {
   long long* trace = nullptr;  // debug timeline (128 slots), tile kernel only
 };
 void fused_inverted_residual(const FusedIRParams& p, hipStream_t s);
+// Fused stem (3x3 s2, 3 -> 32, relu6, letterbox gather) + MobileNetV2 block 0
+// (dw 3x3 on 32 ch + relu6, project 32 -> 16); weights: ws [32][32] bf16 with
+// K = (ky*3+kx)*3 + c (RGB), bs [32] f32, wd [9][32] f16, bd [32] f16, wp [16][32] f16, bp [16].
+struct StemBlock0Params {
+  const uint8_t* frames = nullptr; const int32_t* lut_x = nullptr; const int32_t* lut_y = nullptr;
+  const bf16* ws = nullptr; const float* bs = nullptr;
+  const void* wd = nullptr; const void* bd = nullptr; const void* wp = nullptr;
+  const float* bp = nullptr; bf16* out = nullptr;
+  int B = 0, Hc = 0, Wc = 0, H = 0, W = 0, SH = 0, SW = 0, Cout = 16, TY = 8, TX = 16;
+};
+void stem_block0(const StemBlock0Params& p, hipStream_t s);
 // LDS bytes the tile kernel needs for a (TY, TX) tile (0 if the shape is unsupported).
 size_t fused_ir_tile_lds(int CinP, int stride, int dil, int TY, int TX, int expand);
 

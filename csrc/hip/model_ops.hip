@@ -421,9 +421,88 @@ __global__ __launch_bounds__(256) void upsample_argmax_kernel(const bf16* __rest
   }
 }
 
+// Separable interval variant (upsampling, K <= 32, ldk % 8 == 0): one lane = one
+// output row x one source interval [j, j+1], i.e. every output pixel X of the row
+// whose left source column (int)(sw * X) is j (16 of them at 33 -> 513). The lane
+// vertically interpolates its two source columns once (16-byte bf16 loads) into
+// fp32 registers (and their difference), after which each output pixel costs one
+// FMA + compare per class: no per-pixel gathers and no register selects (PMC on
+// the direct kernel: 4 x K scalar bf16 loads per pixel made it issue-bound).
+// Interpolant v = v_j + lx1 * (v_{j+1} - v_j) with v_c = ly0 * L[y0][c] + ly1 * L[y1][c]:
+// the same bilinear value as torch's align_corners=True in another rounding order
+// (the tests check argmax agreement).
+template <int KP, int PXMAX>
+__global__ __launch_bounds__(256) void upsample_argmax_interval_kernel(
+    const bf16* __restrict__ logits, uint8_t* __restrict__ labels, int B, int h, int w, int K,
+    int ldk, int H, int W) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B * H * w) return;
+  const int j = t % w;
+  const int Y = (t / w) % H;
+  const int b = t / (w * H);
+  const float sh = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
+  const float sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
+  const float fy = sh * (float)Y;
+  const int y0 = (int)fy;
+  const int yp = y0 < h - 1 ? 1 : 0;
+  const float ly1 = fy - (float)y0, ly0 = 1.f - ly1;
+  // first output column whose left source column is j (exact fp32 formula, then fix-up)
+  int xs = sw > 0.f ? (int)((float)j / sw) - 1 : 0;
+  if (xs < 0) xs = 0;
+  while (xs > 0 && (int)(sw * (float)xs) >= j) --xs;
+  while (xs < W && (int)(sw * (float)xs) < j) ++xs;
+  const int j1 = j < w - 1 ? j + 1 : j;
+  const bf16* r0 = logits + ((size_t)(b * h + y0) * w) * ldk;
+  const bf16* r1 = r0 + (size_t)yp * w * ldk;
+  float v0[KP], dv[KP];
+#pragma unroll
+  for (int k8 = 0; k8 < KP; k8 += 8) {
+    const bf16x8 a0 = ld8(r0 + (size_t)j * ldk + k8), a1 = ld8(r1 + (size_t)j * ldk + k8);
+    const bf16x8 c0 = ld8(r0 + (size_t)j1 * ldk + k8), c1 = ld8(r1 + (size_t)j1 * ldk + k8);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float u = ly0 * (float)a0[q] + ly1 * (float)a1[q];
+      const float v = ly0 * (float)c0[q] + ly1 * (float)c1[q];
+      v0[k8 + q] = u;
+      dv[k8 + q] = v - u;
+    }
+  }
+  uint8_t* op = labels + ((size_t)b * H + Y) * W;
+#pragma unroll
+  for (int e = 0; e < PXMAX; ++e) {
+    const int X = xs + e;
+    if (X >= W) break;
+    const float fx = sw * (float)X;
+    if ((int)fx != j) break;
+    const float lx1 = j < w - 1 ? fx - (float)j : 0.f;
+    float best = -3.0e38f;
+    int arg = 0;
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+      const float v = v0[k] + lx1 * dv[k];
+      if (k < K && v > best) { best = v; arg = k; }
+    }
+    op[X] = (uint8_t)arg;
+  }
+}
+
 void upsample_argmax(const bf16* logits, uint8_t* labels, int B, int h, int w, int K, int ldk,
                      int H, int W, hipStream_t s) {
   if (K > 256) throw std::invalid_argument("upsample_argmax: K > 256");
+  // interval path: at most PXMAX output pixels share a left source column
+  const float sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
+  if (K <= 32 && ldk % 8 == 0 && ldk >= ((K + 7) / 8) * 8 && w >= 2 && W > 1 && sw > 0.f &&
+      1.f / sw <= 30.f && (long long)B * H * w < (1LL << 31)) {
+    const long long total = (long long)B * H * w;
+    if (K <= 24)
+      hipLaunchKernelGGL((upsample_argmax_interval_kernel<24, 32>), dim3(cdiv(total, 256)), dim3(256),
+                         0, s, logits, labels, B, h, w, K, ldk, H, W);
+    else
+      hipLaunchKernelGGL((upsample_argmax_interval_kernel<32, 32>), dim3(cdiv(total, 256)), dim3(256),
+                         0, s, logits, labels, B, h, w, K, ldk, H, W);
+    check_launch("upsample_argmax interval");
+    return;
+  }
   const long long total = (long long)B * H * ((W + 3) / 4);
   hipLaunchKernelGGL(upsample_argmax_kernel<256>, dim3(cdiv(total, 256)), dim3(256), 0, s, logits,
                      labels, B, h, w, K, ldk, H, W);

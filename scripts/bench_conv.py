@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default=None)
     ap.add_argument("--variants", default="1,4,5,6")
+    ap.add_argument("--shape", default=None, help="only this shape name (e.g. b15_exp)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     variants = [int(v) for v in a.variants.split(",")]
@@ -54,6 +55,8 @@ def main():
         if a.only and fam != a.only:
             continue
         for name, B, H, W, Cin, Cout, k, stride, dil in shapes:
+            if a.shape and name != a.shape:
+                continue
             OH, OW = (H - 1) // stride + 1, (W - 1) // stride + 1
             x = (torch.randn(B, H, W, Cin, device=dev) * 0.5).to(torch.bfloat16)
             w = (torch.randn(Cout, k, k, Cin, device=dev) / (Cin * k * k) ** 0.5).to(torch.bfloat16)

@@ -83,7 +83,15 @@ class Choice:
         if mode in ("0", "1"):
             want = "unfused" if mode == "0" else "fused"
             self.pick = next((i for i, (n, _) in enumerate(self.variants) if n == want), 0)
+            for _, ops in self.variants:
+                for op in ops:
+                    if isinstance(op, Choice):
+                        op.autotune(args, reps)
             return
+        for _, ops in self.variants:  # nested choices first (e.g. block 0 inside stem+block0)
+            for op in ops:
+                if isinstance(op, Choice):
+                    op.autotune(args, reps)
         if len(self.variants) < 2:
             return
         times = []
@@ -123,6 +131,7 @@ class HipDeepLab:
         self.kind = "mnv2" if isinstance(bb, MobileNetV2Backbone) else "resnet50"
         self.stem = _pack_stem(bb.stem, dev) + (bb.stem.k, bb.stem.stride, bb.stem.act, bb.stem.cout)
         self.blocks: List[dict] = []
+        self.stem_block0 = None
         if self.kind == "mnv2":
             for blk in bb.blocks:
                 s = blk.spec
@@ -155,6 +164,14 @@ class HipDeepLab:
                     pwf, pbf = blk.project.fold()
                     d["dwproj"] = K.pack_project_padded(pwf[:, :, 0, 0], pbf, s.cout, s.hidden, dev)
                 self.blocks.append(d)
+            b0 = bb.blocks[0]
+            s0 = b0.spec
+            if (b0.expand is None and s0.stride == 1 and s0.dilation == 1 and s0.cin == 32 and
+                    s0.cout == 16 and bb.stem.cout == 32 and bb.stem.k == 3 and bb.stem.stride == 2
+                    and bb.stem.act == "relu6"):
+                dwf, dbf = b0.dw.fold()
+                pwf, pbf = b0.project.fold()
+                self.stem_block0 = K.pack_stem_block0(bb.stem, dwf[:, 0], dbf, pwf[:, :, 0, 0], pbf, dev)
         else:
             for blk in bb.blocks:
                 self.blocks.append(dict(
@@ -207,6 +224,7 @@ class HipDeepLab:
             K.stem_conv(frames, lx, ly, sw, sb, x, H=H, W=W, OH=OH, OW=OW, Cout=sc, k=sk,
                         stride=ss, act=sact)
         ops.append(stem_op)
+        stem_at = len(ops) - 1
         h, w, c = OH, OW, sc
         if self.kind == "resnet50":
             PH, PW = conv_out_hw(h, w, 3, 2, 1)
@@ -219,6 +237,15 @@ class HipDeepLab:
         else:
             for i, blk in enumerate(self.blocks):
                 x, h, w, c = self._mnv2_block(ops, buf, i, blk, x, B, h, w, c)
+                if i == 0 and self.stem_block0 is not None:
+                    # stem + block 0 as one kernel (the 257^2 x 32 stem tensor never hits HBM)
+                    sbp, out0 = self.stem_block0, x
+                    fused = [(f"stem_block0_{ty}x{tx}", [
+                        lambda frames, lx, ly, out0=out0, ty=ty, tx=tx, sbp=sbp: K.stem_block0(
+                            frames, lx, ly, sbp, out0, H=H, W=W, tile=(ty, tx))])
+                        for ty, tx in ((8, 16), (4, 16), (8, 8))]
+                    sep = ("separate", [ops[stem_at], ops[stem_at + 1]])
+                    ops[stem_at:stem_at + 2] = [Choice("stem+block0", fused + [sep])]
         # ---- ASPP
         A = self.aspp_c
         cat = buf("aspp_cat", B, h, w, self.cat_c)

@@ -191,6 +191,38 @@ def pack_fused_ir(we, be, wd, bd, wp, bp, *, Cin, hid, Cout, stride, residual, d
     return out
 
 
+def pack_stem_block0(stem, wd, bd, wp, bp, device) -> dict:
+    """Weights of the fused stem + block-0 kernel. stem: ConvBNAct (3x3 s2, 3 -> 32);
+    wd [32, 3, 3], bd [32], wp [16, 32], bp [16] (BN folded)."""
+    w, b = stem.fold()                                   # [32, 3, 3, 3] (RGB in)
+    ws = torch.zeros(32, 32, dtype=torch.float32)
+    ws[:, :27] = w.permute(0, 2, 3, 1).reshape(32, 27)   # K = (ky*3 + kx)*3 + c
+    f32 = dict(dtype=torch.float32, device=device)
+    return dict(
+        ws=ws.to(device=device, dtype=torch.bfloat16).contiguous(), bs=b.to(**f32).contiguous(),
+        wd_h=wd.reshape(32, 9).t().contiguous().to(device=device, dtype=torch.float16),
+        bd_h=bd.to(device=device, dtype=torch.float16).contiguous(),
+        wp_h=wp.to(device=device, dtype=torch.float16).contiguous(),
+        bp=bp.to(**f32).contiguous(), Cout=int(wp.shape[0]))
+
+
+def stem_block0(frames, lut_x, lut_y, packed: dict, out, *, H, W, tile=(8, 16)):
+    """Fused stem + MobileNetV2 block 0. frames [B, Hc, Wc, 3] u8 BGR; out [B, SH, SW, 16] bf16."""
+    B, Hc, Wc, _ = frames.shape
+    SH, SW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    _chk(frames, torch.uint8, "frames", B * Hc * Wc * 3)
+    _chk(out, torch.bfloat16, "out", B * SH * SW * packed["Cout"])
+    _chk(lut_x, torch.int32, "lut_x", W)
+    _chk(lut_y, torch.int32, "lut_y", H)
+    P = packed
+    _hip_mod().stem_block0(_ptr(frames), _ptr(lut_x), _ptr(lut_y), _ptr(P["ws"]), _ptr(P["bs"]),
+                           _ptr(P["wd_h"]), _ptr(P["bd_h"]), _ptr(P["wp_h"]), _ptr(P["bp"]),
+                           _ptr(out), B, Hc, Wc, H, W, SH, SW, P["Cout"], tile[0], tile[1],
+                           _stream())
+    _dbg("stem_block0")
+    return out
+
+
 def depthwise3x3(x, w, bias, out, *, B, IH, IW, C, OH, OW, stride=1, dil=1, act="relu6"):
     """x: [B,IH,IW,C] bf16; w: [9, C] fp32; out: [B,OH,OW,C] bf16."""
     _chk(x, torch.bfloat16, "x", B * IH * IW * C)

@@ -50,7 +50,7 @@ def _nchw(x):
     (2, 65, 65, 144, 32, 1, 1, 1, None, False, 0, 0),
     (1, 33, 33, 1024, 256, 1, 1, 1, "relu", False, 0, 0),
 ])
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7])
 def test_conv_gemm(B, H, W, Cin, Cout, k, stride, dil, act, res, ldo_pad, co_off, variant):
     K = _hip()
     g = torch.Generator(device="cpu").manual_seed(1)
@@ -360,6 +360,41 @@ def test_fused_inverted_residual(cin, cout, t, stride, H):
     out = torch.empty(B, OH, OW, cout, dtype=torch.bfloat16, device=DEV)
     K.fused_ir(_nhwc(x).to(DEV), packed, out, B=B, IH=H, IW=W, OH=OH, OW=OW)
     torch.cuda.synchronize()
+    assert _rel(_nchw(out).cpu(), ref) < 2e-2
+
+
+@pytest.mark.parametrize("cam,H,tile", [((640, 480), 513, (8, 16)), ((200, 150), 129, (4, 16)),
+                                        ((97, 131), 65, (8, 8))])
+def test_stem_block0_fused(cam, H, tile):
+    from semantic_segmentation_server_amd.models.layers import ConvBNAct, init_random
+    from semantic_segmentation_server_amd.models.mobilenetv2 import InvertedResidual, IRSpec
+    from semantic_segmentation_server_amd.ops import reference_ops as R
+    K = _hip()
+    stem = ConvBNAct(3, 32, 3, 2, act="relu6")
+    blk = InvertedResidual(IRSpec(32, 16, 1, 1, 1))
+    init_random(stem, seed=5)
+    init_random(blk, seed=6)
+    for m in list(stem.modules()) + list(blk.modules()):
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.uniform_(-0.2, 0.2)
+            m.running_var.uniform_(0.5, 2.0)
+    stem.eval(); blk.eval()
+    Wc, Hc = cam
+    g = torch.Generator().manual_seed(3)
+    frames = torch.randint(0, 256, (2, Hc, Wc, 3), generator=g, dtype=torch.uint8)
+    lx, ly, *_ = R.letterbox_luts(Wc, Hc, H, H)
+    x = R.preprocess(frames, torch.from_numpy(np.array(lx)), torch.from_numpy(np.array(ly)))
+    with torch.no_grad():
+        ref = blk(stem(x))
+    dwf, dbf = blk.dw.fold()
+    pwf, pbf = blk.project.fold()
+    P = K.pack_stem_block0(stem, dwf[:, 0], dbf, pwf[:, :, 0, 0], pbf, DEV)
+    SH = (H - 1) // 2 + 1
+    out = torch.full((2, SH, SH, 16), float("nan"), dtype=torch.bfloat16, device=DEV)
+    K.stem_block0(frames.to(DEV), torch.tensor(np.array(lx), dtype=torch.int32, device=DEV),
+                  torch.tensor(np.array(ly), dtype=torch.int32, device=DEV), P, out, H=H, W=H, tile=tile)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
     assert _rel(_nchw(out).cpu(), ref) < 2e-2
 
 
