@@ -106,6 +106,19 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("OH"), py::arg("OW"), py::arg("Cout"), py::arg("K"), py::arg("stride"),
         py::arg("act"), py::arg("stream"), py::arg("out_inv_scale") = 0.f);
 
+  m.def("pw_conv",
+        [](uintptr_t in, uintptr_t w, uintptr_t img_bias, uintptr_t res,
+           uintptr_t out, int M, int K, int N, int HW, int ldo, int co_off, int ldr, int act,
+           int mt, int nch, uintptr_t stream) {
+          PwConvParams p;
+          p.in = P<const bf16>(in); p.w = P<const bf16>(w);
+          p.img_bias = P<const float>(img_bias); p.res = P<const bf16>(res); p.out = P<bf16>(out);
+          p.M = M; p.K = K; p.N = N; p.HW = HW; p.ldo = ldo; p.co_off = co_off; p.ldr = ldr;
+          p.act = act; p.mt = mt; p.nch = nch;
+          pw_conv(p, S(stream));
+        });
+  m.def("pw_conv_supported_ks", &pw_conv_supported_ks);
+
   m.def("conv_i8",
         [](uintptr_t in, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t img_bias,
            uintptr_t res, float res_scale, uintptr_t out, float inv_out_scale, int out_mode, int B,

@@ -23,6 +23,22 @@ struct ConvParams {
 };
 void conv_gemm(const ConvParams& p, hipStream_t s);
 
+// Pointwise conv, weight-streamed (pw_conv.hip). w is host-packed per 64-channel
+// chunk: weights in MFMA fragment order [4][ceil(K/32)][64 lanes][8] bf16 followed by
+// 1 KiB holding the chunk's 64 fp32 biases, zero-padded (hip_ops.pack_pw_weights).
+struct PwConvParams {
+  const bf16* in = nullptr;        // [M, K]
+  const bf16* w = nullptr;         // packed weights + biases
+  const float* img_bias = nullptr; // optional [M / HW, N]
+  const bf16* res = nullptr;       // optional [M, ldr]
+  bf16* out = nullptr;             // [M, ldo] at channel offset co_off
+  int M = 0, K = 0, N = 0, HW = 1, ldo = 0, co_off = 0, ldr = 0, act = 0;
+  int mt = 2;   // 16*mt pixels per wave (2 or 4)
+  int nch = 1;  // 64-channel chunks per workgroup
+};
+void pw_conv(const PwConvParams& p, hipStream_t s);
+int pw_conv_supported_ks(int K);  // 0 if K has no instantiation
+
 // int8 implicit-GEMM conv (int8 MFMA, int32 accumulate). scale[n] = in_scale *
 // w_scale[n]; out_mode 0 -> int8 out (round(v * inv_out_scale), clamp +-127),
 // 1 -> bf16 out. res (optional) is int8 [M, Cout] with res_scale.

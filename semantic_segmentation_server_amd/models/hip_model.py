@@ -117,6 +117,31 @@ def _pack_stem(layer: ConvBNAct, dev) -> Tuple[torch.Tensor, torch.Tensor]:
             b.contiguous().to(dev, torch.float32))
 
 
+_PW_CONFIGS = [(2, 1), (2, 2), (2, 3), (4, 3), (4, 5)]
+
+
+def pw_choice(name: str, gemm_op: Callable, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor,
+              out: torch.Tensor, *, M: int, Cin: int, Cout: int, ldo: Optional[int] = None,
+              co_off: int = 0, act=None, N_out: Optional[int] = None) -> Callable:
+    """A 1x1 conv step: the generic implicit GEMM (``gemm_op``) or the weight-streamed
+    pw_conv kernel in a few (pixels-per-wave, chunks-per-workgroup) shapes, picked by
+    the plan autotuner on the real buffers. Falls back to ``gemm_op`` alone when
+    pw_conv has no instantiation for (Cin, Cout)."""
+    Np = max(Cout, N_out or Cout)
+    if not K.pw_supported(Cin, Np) or (ldo or Np) % 8 or co_off % 8:
+        return gemm_op
+    wpk = K.pack_pw_weights(w, b, N_out=Np)
+    variants = [("gemm", [gemm_op])]
+    NC = -(-Np // 64)
+    for mt, nch in _PW_CONFIGS:
+        if nch > NC:
+            continue
+        variants.append((f"pw{mt}x{nch}", [
+            lambda *_, mt=mt, nch=nch: K.pw_conv(x, wpk, out, M=M, K=Cin, N=Np, ldo=ldo,
+                                                  co_off=co_off, act=act, mt=mt, nch=nch)]))
+    return Choice(name, variants)
+
+
 class HipDeepLab:
     def __init__(self, model: DeepLabV3, device: torch.device, cfg=None):
         if device.type != "cuda":
@@ -250,8 +275,9 @@ class HipDeepLab:
         A = self.aspp_c
         cat = buf("aspp_cat", B, h, w, self.cat_c)
         b0w, b0b = self.aspp_b0
-        ops.append(lambda *_, x=x, h=h, w=w, c=c: K.conv_gemm(
+        ops.append(pw_choice("aspp.b0", lambda *_, x=x, h=h, w=w, c=c: K.conv_gemm(
             x, b0w, b0b, cat, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w, Cout=A, k=1, ldo=self.cat_c,
+            co_off=0, act="relu"), x, b0w, b0b, cat, M=B * h * w, Cin=c, Cout=A, ldo=self.cat_c,
             co_off=0, act="relu"))
         for j, ((aw, ab), rate) in enumerate(self.aspp_atrous):
             ops.append(lambda *_, x=x, h=h, w=w, c=c, aw=aw, ab=ab, rate=rate, j=j: K.conv_gemm(
@@ -274,9 +300,11 @@ class HipDeepLab:
             cat, self.proj_w, self.proj_b, proj, B=B, IH=h, IW=w, Cin=self.cat_c, OH=h, OW=w,
             Cout=A, k=1, act="relu", img_bias=img_bias))
         logits = buf("logits", B, h, w, self.ldk)
-        ops.append(lambda *_, h=h, w=w: K.conv_gemm(
+        ops.append(pw_choice("logits", lambda *_, h=h, w=w: K.conv_gemm(
             proj, self.logit_w, self.logit_b, logits, B=B, IH=h, IW=w, Cin=A, OH=h, OW=w,
-            Cout=self.num_classes, k=1, ldo=self.ldk, act=None))
+            Cout=self.num_classes, k=1, ldo=self.ldk, act=None), proj, self.logit_w,
+            self.logit_b, logits, M=B * h * w, Cin=A, Cout=self.num_classes, ldo=self.ldk, act=None,
+            N_out=self.ldk))
         labels = buf("labels", B, H, W, dtype=torch.uint8)
         ops.append(lambda *_, h=h, w=w: K.upsample_argmax(
             logits, labels, B=B, h=h, w=w, K=self.num_classes, ldk=self.ldk, H=H, W=W))
@@ -315,8 +343,9 @@ class HipDeepLab:
         if blk["expand"] is not None:
             ew, eb = blk["expand"]
             e = buf(f"b{i}_exp", B, h, w, hid)
-            ops.append(lambda *_, x=x, e=e, h=h, w=w, c=c: K.conv_gemm(
-                x, ew, eb, e, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w, Cout=hid, k=1, act="relu6"))
+            ops.append(pw_choice(f"block{i}.expand", lambda *_, x=x, e=e, h=h, w=w, c=c: K.conv_gemm(
+                x, ew, eb, e, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w, Cout=hid, k=1, act="relu6"),
+                x, ew, eb, e, M=B * h * w, Cin=c, Cout=hid, act="relu6"))
             x = e
         unfused_expand_out = x
         OH, OW = conv_out_hw(h, w, 3, s.stride, s.dilation)

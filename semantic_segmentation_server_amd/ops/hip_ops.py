@@ -85,6 +85,61 @@ def conv_gemm(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out: torch.T
     return out
 
 
+def pw_supported(K: int, N: int) -> bool:
+    """True if pw_conv has an instantiation for this (K = Cin, N = Cout) pair."""
+    ks = (K + 31) // 32
+    return K % 8 == 0 and N % 8 == 0 and (ks <= 5 or ks in (8, 10))
+
+
+def pack_pw_weights(w: torch.Tensor, bias: torch.Tensor, N_out: Optional[int] = None) -> torch.Tensor:
+    """[N, K] (or [N, 1, 1, K]) weights + [N] fp32 bias -> pw_conv's packed operand.
+
+    Per 64-output-channel chunk c: the weights in MFMA fragment order
+    [4 subtiles][ceil(K/32)][64 lanes][8] bf16, element (j, k, lane, e) =
+    W[c*64 + j*16 + lane%16][k*32 + (lane//16)*8 + e], then 1 KiB holding the
+    chunk's 64 fp32 biases (zero-padded). ``N_out`` pads the channel count (e.g. 21
+    logits written as 24)."""
+    w = w.reshape(w.shape[0], -1).float()
+    N, Kd = w.shape
+    Np = max(N, N_out or N)
+    NC, KS = -(-Np // 64), -(-Kd // 32)
+    full = torch.zeros(NC * 64, KS * 32, dtype=torch.float32, device=w.device)
+    full[:N, :Kd] = w
+    # [c, j, r, k, kq, e] -> [c, j, k, kq, r, e]  (lane = kq*16 + r)
+    wt = full.reshape(NC, 4, 16, KS, 4, 8).permute(0, 1, 3, 4, 2, 5).reshape(NC, -1)
+    bt = torch.zeros(NC, 256, dtype=torch.float32, device=w.device)
+    bflat = torch.zeros(NC * 64, dtype=torch.float32, device=w.device)
+    bflat[:N] = bias.float().to(w.device)
+    bt[:, :64] = bflat.reshape(NC, 64)
+    return torch.cat([wt.to(torch.bfloat16), bt.view(torch.bfloat16)], dim=1).contiguous()
+
+
+def pw_conv(x, wpk, out, *, M, K, N, ldo=None, co_off=0, act=None, res=None, ldr=None,
+            img_bias=None, HW=1, mt=2, nch=1) -> torch.Tensor:
+    """Weight-streamed 1x1 conv (pw_conv.hip). x: [M, K] bf16 (NHWC pixels), wpk from
+    ``pack_pw_weights`` (weights + bias), out [M, ldo] bf16 at channel offset co_off."""
+    ldo = N if ldo is None else ldo
+    ldr = N if ldr is None else ldr
+    if not pw_supported(K, N) or ldo % 8 or co_off % 8 or (res is not None and ldr % 8):
+        raise ValueError(f"pw_conv: unsupported K={K} N={N} ldo={ldo} co_off={co_off}")
+    if co_off + N > ldo or mt not in (2, 4) or nch < 1:
+        raise ValueError("pw_conv: bad co_off / mt / nch")
+    NC, KS = -(-N // 64), -(-K // 32)
+    _chk(x, torch.bfloat16, "x", M * K)
+    _chk(wpk, torch.bfloat16, "wpk", NC * (4 * KS + 1) * 512)
+    _chk(out, torch.bfloat16, "out", M * ldo)
+    if res is not None:
+        _chk(res, torch.bfloat16, "res", M * ldr)
+    if img_bias is not None:
+        _chk(img_bias, torch.float32, "img_bias", (M // HW) * N)
+        if M % HW:
+            raise ValueError("pw_conv: M must be a multiple of HW with img_bias")
+    _hip_mod().pw_conv(_ptr(x), _ptr(wpk), _ptr(img_bias), _ptr(res), _ptr(out), M, K, N, HW, ldo,
+                       co_off, ldr, ACT[act], mt, nch, _stream())
+    _dbg('pw_conv')
+    return out
+
+
 def fused_ir(x, packed: dict, out, *, B, IH, IW, OH, OW, tile=None, trace=None):
     """Fused inverted residual. ``packed`` from ``pack_fused_ir``.
 

@@ -99,6 +99,53 @@ def test_conv_gemm_img_bias():
     assert _rel(_nchw(out).cpu(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("M,Cin,Cout,act,res,img,ldo_pad,co_off,n_out", [
+    (2 * 33 * 33, 160, 960, "relu6", False, False, 0, 0, None),   # b14-16 expansion
+    (1000, 96, 576, "relu6", False, False, 0, 0, None),           # M tail (not a multiple of 128/256)
+    (777, 24, 144, "relu6", False, False, 0, 0, None),            # K = 24 (< one 32-deep step)
+    (1089, 320, 256, "relu", False, False, 1024, 256, None),      # ASPP b0 into a concat slice
+    (1089, 256, 21, None, False, False, 0, 0, 24),                # logits, N padded 21 -> 24
+    (999, 64, 96, None, True, False, 0, 0, None),                 # residual
+    (4 * 121, 128, 80, "relu", False, True, 0, 0, None),          # per-image bias, N % 64 != 0
+])
+@pytest.mark.parametrize("mt,nch", [(2, 1), (2, 3), (4, 2)])
+def test_pw_conv(M, Cin, Cout, act, res, img, ldo_pad, co_off, n_out, mt, nch):
+    K = _hip()
+    g = torch.Generator().manual_seed(3)
+    x = (torch.randn(M, Cin, generator=g) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(Cout, Cin, generator=g) / Cin ** 0.5).to(torch.bfloat16)
+    b = torch.randn(Cout, generator=g)
+    ref = x.float() @ w.float().t() + b
+    N = n_out or Cout
+    r = ib = None
+    HW = 121 if img else 1
+    if res:
+        r = torch.randn(M, N, generator=g).to(torch.bfloat16)
+        ref = ref + r.float()[:, :Cout]
+    if img:
+        ib = torch.randn(M // HW, N, generator=g)
+        ref = ref + ib.repeat_interleave(HW, 0)[:, :Cout]
+    if act == "relu":
+        ref = F.relu(ref)
+    elif act == "relu6":
+        ref = F.relu6(ref)
+    ldo = co_off + N + ldo_pad
+    out = torch.full((M, ldo), 7.0, dtype=torch.bfloat16, device=DEV)
+    wpk = K.pack_pw_weights(w.to(DEV), b.to(DEV), N_out=N)
+    K.pw_conv(x.to(DEV), wpk, out, M=M, K=Cin, N=N, ldo=ldo, co_off=co_off, act=act,
+              res=None if r is None else r.to(DEV), img_bias=None if ib is None else ib.to(DEV),
+              HW=HW, mt=mt, nch=nch)
+    torch.cuda.synchronize()
+    got = out[:, co_off:co_off + Cout].float().cpu()
+    assert _rel(got, ref) < 1e-2
+    if N > Cout and not res and not img:  # padded channels: zero weights and bias -> act(0)
+        assert torch.all(out[:, co_off + Cout:co_off + N].float() == 0)
+    if co_off:
+        assert torch.all(out[:, :co_off] == 7.0)
+    if ldo_pad:
+        assert torch.all(out[:, co_off + N:] == 7.0)
+
+
 @pytest.mark.parametrize("B,H,W,C,stride,dil", [
     (2, 33, 35, 96, 1, 1), (2, 33, 35, 96, 2, 1), (1, 33, 33, 960, 1, 2), (2, 257, 257, 32, 1, 1),
     (1, 65, 65, 144, 2, 1)])

@@ -1,0 +1,37 @@
+"""CPU check of pw_conv's host-side weight packing: unpacking the packed tensor with
+the kernel's own index formula (pw_conv.hip) must give back W and the bias."""
+import pytest
+import torch
+
+from semantic_segmentation_server_amd.ops import hip_ops as K
+
+
+@pytest.mark.parametrize("N,Kd,n_out", [(96, 160, None), (21, 256, 24), (576, 96, None), (144, 24, None)])
+def test_pack_pw_roundtrip(N, Kd, n_out):
+    g = torch.Generator().manual_seed(0)
+    w = torch.randn(N, Kd, generator=g)
+    b = torch.randn(N, generator=g)
+    p = K.pack_pw_weights(w, b, N_out=n_out)
+    Np = max(N, n_out or N)
+    NC, KS = -(-Np // 64), -(-Kd // 32)
+    assert p.dtype == torch.bfloat16 and p.numel() == NC * (4 * KS + 1) * 512
+    chunks = p.reshape(NC, (4 * KS + 1) * 512)
+    wrec = torch.zeros(NC * 64, KS * 32)
+    brec = torch.zeros(NC * 64)
+    for c in range(NC):
+        wt = chunks[c, : 4 * KS * 512].float().reshape(4, KS, 64, 8)
+        for j in range(4):
+            for k in range(KS):
+                for lane in range(64):
+                    r, kq = lane % 16, lane // 16
+                    wrec[c * 64 + j * 16 + r, k * 32 + kq * 8: k * 32 + kq * 8 + 8] = wt[j, k, lane]
+        brec[c * 64:(c + 1) * 64] = chunks[c, 4 * KS * 512:].contiguous().view(torch.float32)[:64]
+    assert torch.equal(wrec[:N, :Kd], w.to(torch.bfloat16).float())
+    assert wrec[N:].abs().sum() == 0 and wrec[:, Kd:].abs().sum() == 0
+    assert torch.equal(brec[:N], b) and brec[N:].abs().sum() == 0
+
+
+def test_pw_supported():
+    assert K.pw_supported(160, 960) and K.pw_supported(24, 144) and K.pw_supported(320, 256)
+    assert not K.pw_supported(960, 160)  # deep K: the generic implicit GEMM handles it
+    assert not K.pw_supported(256, 21)   # N must be padded to a multiple of 8
