@@ -22,8 +22,10 @@ PYBIND11_MODULE(_hip, m) {
   m.def("conv_gemm",
         [](uintptr_t in, uintptr_t w, uintptr_t bias, uintptr_t img_bias, uintptr_t res,
            uintptr_t out, int B, int IH, int IW, int Cin, int OH, int OW, int Cout, int KH, int KW,
-           int stride, int dil, int ldo, int co_off, int ldr, int act, uintptr_t stream, int variant) {
+           int stride, int dil, int ldo, int co_off, int ldr, int act, uintptr_t stream, int variant,
+           uintptr_t perm, int Mp) {
           ConvParams p;
+          p.perm = P<const int>(perm); p.Mp = Mp;
           p.in = P<const bf16>(in); p.w = P<const bf16>(w); p.bias = P<const float>(bias);
           p.img_bias = P<const float>(img_bias); p.res = P<const bf16>(res); p.out = P<bf16>(out);
           p.B = B; p.IH = IH; p.IW = IW; p.Cin = Cin; p.OH = OH; p.OW = OW; p.Cout = Cout;
@@ -35,13 +37,13 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("out"), py::arg("B"), py::arg("IH"), py::arg("IW"), py::arg("Cin"), py::arg("OH"),
         py::arg("OW"), py::arg("Cout"), py::arg("KH"), py::arg("KW"), py::arg("stride"),
         py::arg("dil"), py::arg("ldo"), py::arg("co_off"), py::arg("ldr"), py::arg("act"),
-        py::arg("stream"), py::arg("variant") = 0);
+        py::arg("stream"), py::arg("variant") = 0, py::arg("perm") = 0, py::arg("Mp") = 0);
 
   m.def("fused_ir",
         [](uintptr_t in, uintptr_t we, uintptr_t be, uintptr_t wd, uintptr_t bd, uintptr_t wp,
            uintptr_t bp, uintptr_t out, int B, int IH, int IW, int Cin, int CinP, int hidP,
            int Cout, int OH, int OW, int stride, int residual, uintptr_t stream, int dil, int TY,
-           int TX, uintptr_t wd_h, uintptr_t bd_h, uintptr_t wp_h, uintptr_t trace) {
+           int TX, uintptr_t wd_h, uintptr_t bd_h, uintptr_t wp_h, uintptr_t trace, int persist) {
           FusedIRParams p;
           p.in = P<const bf16>(in); p.we = P<const bf16>(we); p.be = P<const float>(be);
           p.wd = P<const float>(wd); p.bd = P<const float>(bd); p.wp = P<const bf16>(wp);
@@ -51,15 +53,17 @@ PYBIND11_MODULE(_hip, m) {
           p.dil = dil; p.TY = TY; p.TX = TX;
           p.wd_h = P<const void>(wd_h); p.bd_h = P<const void>(bd_h); p.wp_h = P<const void>(wp_h);
           p.trace = P<long long>(trace);
-          fused_inverted_residual(p, S(stream));
+          if (persist) fused_ir_persist(p, S(stream));
+          else fused_inverted_residual(p, S(stream));
         },
         py::arg("in"), py::arg("we"), py::arg("be"), py::arg("wd"), py::arg("bd"), py::arg("wp"),
         py::arg("bp"), py::arg("out"), py::arg("B"), py::arg("IH"), py::arg("IW"), py::arg("Cin"),
         py::arg("CinP"), py::arg("hidP"), py::arg("Cout"), py::arg("OH"), py::arg("OW"),
         py::arg("stride"), py::arg("residual"), py::arg("stream"), py::arg("dil") = 1,
         py::arg("TY") = 0, py::arg("TX") = 0, py::arg("wd_h") = 0, py::arg("bd_h") = 0,
-        py::arg("wp_h") = 0, py::arg("trace") = 0);
+        py::arg("wp_h") = 0, py::arg("trace") = 0, py::arg("persist") = 0);
   m.def("fused_ir_tile_lds", &fused_ir_tile_lds);
+  m.def("fused_ir_persist_lds", &fused_ir_persist_lds);
   m.def("stem_block0",
         [](uintptr_t frames, uintptr_t lx, uintptr_t ly, uintptr_t ws, uintptr_t bs, uintptr_t wd,
            uintptr_t bd, uintptr_t wp, uintptr_t bp, uintptr_t out, int B, int Hc, int Wc, int H,
@@ -118,6 +122,18 @@ PYBIND11_MODULE(_hip, m) {
           pw_conv(p, S(stream));
         });
   m.def("pw_conv_supported_ks", &pw_conv_supported_ks);
+  m.def("tap_conv",
+        [](uintptr_t in, uintptr_t w, uintptr_t bias, uintptr_t out, uintptr_t perm, int Mp, int B,
+           int H, int W, int Cin, int Cout, int KH, int KW, int dil, int ldo, int co_off, int act,
+           uintptr_t stream) {
+          TapConvParams p;
+          p.in = P<const bf16>(in); p.w = P<const bf16>(w); p.bias = P<const float>(bias);
+          p.out = P<bf16>(out); p.perm = P<const int>(perm); p.Mp = Mp;
+          p.B = B; p.H = H; p.W = W; p.Cin = Cin; p.Cout = Cout; p.KH = KH; p.KW = KW;
+          p.dil = dil; p.ldo = ldo; p.co_off = co_off; p.act = act;
+          tap_conv(p, S(stream));
+        });
+  m.def("tap_conv_group_channels", &tap_conv_group_channels);
 
   m.def("conv_i8",
         [](uintptr_t in, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t img_bias,

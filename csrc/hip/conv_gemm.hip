@@ -32,6 +32,8 @@ struct ConvArgs {
   int B, IH, IW, Cin, OH, OW, Cout;
   int KH, KW, stride, dil;
   int ldo, co_off, ldr, act;
+  const int* perm;  // LDS-DMA kernel only: GEMM row -> output pixel (-1: padding), or null
+  int Mp;           // rows of the permuted GEMM (perm != null)
 };
 
 template <int MT, int NT>
@@ -483,7 +485,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(ConvArgs a) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
   const int r16 = lane & 15, kq = lane >> 4;
-  const int M = a.B * a.OH * a.OW;
+  // GEMM rows: output pixels, optionally through a permutation that groups pixels
+  // of equal tap validity into whole tiles (dilated ASPP branches: the tile tap
+  // mask below then skips every all-padding tap, not only the row-uniform ones)
+  const int M = a.perm ? a.Mp : a.B * a.OH * a.OW;
   const int tiles_m = cdiv_dev(M, BM), tiles_n = cdiv_dev(a.Cout, BN);
   const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
   const int tn = bid % tiles_n, tm = bid / tiles_n;
@@ -498,8 +503,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(ConvArgs a) {
 #pragma unroll
   for (int i = 0; i < GA; ++i) {
     const int m = m0 + wid * (BM / NW) + i * 8 + grow;
-    av[i] = m < M;
-    const int mm = av[i] ? m : 0;
+    const int pm = m < M ? (a.perm ? a.perm[m] : m) : -1;
+    av[i] = pm >= 0;
+    const int mm = av[i] ? pm : 0;
     const int b = mm / (a.OH * a.OW);
     const int rem = mm - b * a.OH * a.OW;
     ay[i] = (rem / a.OW) * a.stride;
@@ -599,8 +605,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(ConvArgs a) {
 
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
-    const int m = m0 + wm * 16 * MT + i * 16 + r16;
-    if (m >= M) continue;
+    const int mg = m0 + wm * 16 * MT + i * 16 + r16;
+    if (mg >= M) continue;
+    const int m = a.perm ? a.perm[mg] : mg;
+    if (m < 0) continue;
     const int b = m / (a.OH * a.OW);
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
@@ -642,7 +650,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(ConvArgs a) {
 template <int MT, int NT, int ST, int WM = 2, int WN = 2>
 static void launch_conv_glds(const ConvArgs& a, hipStream_t s) {
   constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN;
-  const int M = a.B * a.OH * a.OW;
+  const int M = a.perm ? a.Mp : a.B * a.OH * a.OW;
   const int grid = cdiv(M, BM) * cdiv(a.Cout, BN);
   const size_t lds = (size_t)ST * (BM + BN) * 128 + 16;
   static bool attr_set = false;
@@ -713,7 +721,7 @@ void conv_gemm(const ConvParams& p, hipStream_t s) {
   if (p.co_off % 1 != 0 || p.ldo < p.co_off + p.Cout) throw std::invalid_argument("conv_gemm: bad ldo/co_off");
   if (p.res && p.ldr < p.Cout) throw std::invalid_argument("conv_gemm: bad ldr");
   ConvArgs a{p.in, p.w, p.bias, p.img_bias, p.res, p.out, p.B, p.IH, p.IW, p.Cin, p.OH, p.OW,
-             p.Cout, p.KH, p.KW, p.stride, p.dil, p.ldo, p.co_off, p.ldr, p.act};
+             p.Cout, p.KH, p.KW, p.stride, p.dil, p.ldo, p.co_off, p.ldr, p.act, p.perm, p.Mp};
   const long long M = (long long)p.B * p.OH * p.OW;
   const long long tiles = (M + 127) / 128 * cdiv(p.Cout, 32 * pick_nt(p.Cout));
   const long long K = (long long)p.KH * p.KW * p.Cin;
@@ -724,10 +732,30 @@ void conv_gemm(const ConvParams& p, hipStream_t s) {
                        (long long)p.Cout * K < (1LL << 31) && p.KH * p.KW <= 16;  // int32 offsets, tap list
   int variant = p.variant;
   if (variant == 0) variant = (tiles >= 128 && K >= 256) ? (glds_ok ? 4 : 2) : 1;
+  if (p.perm && (variant < 3 || variant == 7 || variant > 10 || !glds_ok))
+    throw std::invalid_argument("conv_gemm: a pixel permutation needs an LDS-DMA variant (3-6)");
   if (variant == 3 || variant == 4) {
     if (!glds_ok) throw std::invalid_argument("conv_gemm glds: tensor too large for 32-bit offsets or > 16 taps");
     if (variant == 3) dispatch_glds<3>(a, s);
     else dispatch_glds<2>(a, s);
+    return;
+  }
+  if (variant >= 8 && variant <= 10) {
+    // deeper rings (ST = 3/4 stages, 2-3 K-steps in flight) at one workgroup per CU:
+    // 8: 128 x 256, 8 waves (2 per SIMD), ST 3 -- ASPP-class N = 256
+    // 9: 64 x (32*nt), 4 waves, ST 4 -- the 33x33 projections (N = 96..320)
+    // 10: 128 x 128, 4 waves, ST 4
+    if (!glds_ok) throw std::invalid_argument("conv_gemm glds: tensor too large for 32-bit offsets or > 16 taps");
+    if (variant == 8) launch_conv_glds<4, 4, 3, 2, 4>(a, s);
+    else if (variant == 10) launch_conv_glds<4, 4, 4, 2, 2>(a, s);
+    else switch (pick_nt(p.Cout)) {
+      case 1: launch_conv_glds<2, 1, 4, 2, 2>(a, s); break;
+      case 2: launch_conv_glds<2, 2, 4, 2, 2>(a, s); break;
+      case 3: launch_conv_glds<2, 3, 4, 2, 2>(a, s); break;
+      case 4: launch_conv_glds<2, 4, 4, 2, 2>(a, s); break;
+      case 5: launch_conv_glds<2, 5, 4, 2, 2>(a, s); break;
+      default: launch_conv_glds<2, 6, 4, 2, 2>(a, s); break;
+    }
     return;
   }
   if (variant == 5 || variant == 6) {

@@ -20,6 +20,10 @@ struct ConvParams {
   int KH = 1, KW = 1, stride = 1, dil = 1;
   int ldo = 0, co_off = 0, ldr = 0, act = 0;
   int variant = 0;  // 0 auto, 1 direct, 2 LDS-staged, 3/4 LDS-DMA 3/2-stage, 5/6 LDS-DMA 128x256/256x256
+  // optional GEMM-row -> output-pixel permutation (-1 = padding row) of Mp rows;
+  // LDS-DMA variants only (tap-validity-grouped tiles for dilated convs)
+  const int* perm = nullptr;
+  int Mp = 0;
 };
 void conv_gemm(const ConvParams& p, hipStream_t s);
 
@@ -37,6 +41,21 @@ struct PwConvParams {
   int nch = 1;  // 64-channel chunks per workgroup
 };
 void pw_conv(const PwConvParams& p, hipStream_t s);
+
+// Dilated KxK stride-1 conv as a tap loop of weight-streamed MFMA GEMMs
+// (tap_conv.hip; the ASPP atrous branches). w is host-packed (hip_ops.pack_tap_weights):
+// [tap][ceil(Cout/128)][8 subtiles][ceil(Cin/32)][64 lanes][8] bf16, zero-padded.
+struct TapConvParams {
+  const bf16* in = nullptr;     // [B, H, W, Cin]
+  const bf16* w = nullptr;      // packed
+  const float* bias = nullptr;  // [ceil(Cout/128)*128] (zero-padded)
+  bf16* out = nullptr;          // [B, H, W, ldo] at channel offset co_off
+  const int* perm = nullptr;    // optional row -> pixel permutation (tap_group_perm), Mp rows
+  int Mp = 0;
+  int B = 0, H = 0, W = 0, Cin = 0, Cout = 0, KH = 3, KW = 3, dil = 1, ldo = 0, co_off = 0, act = 0;
+};
+void tap_conv(const TapConvParams& p, hipStream_t s);
+int tap_conv_group_channels();  // output channels per workgroup (packing granule)
 int pw_conv_supported_ks(int K);  // 0 if K has no instantiation
 
 // int8 implicit-GEMM conv (int8 MFMA, int32 accumulate). scale[n] = in_scale *
@@ -87,6 +106,11 @@ struct FusedIRParams {
   long long* trace = nullptr;  // debug timeline (128 slots), tile kernel only
 };
 void fused_inverted_residual(const FusedIRParams& p, hipStream_t s);
+// Persistent variant of the tile kernel (fused_ir_persist.hip): block weights staged
+// in LDS once per workgroup, next input tile prefetched; same params (TY/TX > 0).
+void fused_ir_persist(const FusedIRParams& p, hipStream_t s);
+// LDS bytes it needs (0: tile too large for the input-tile prefetch registers).
+size_t fused_ir_persist_lds(int CinP, int hidP, int Cout, int stride, int dil, int TY, int TX);
 // Fused stem (3x3 s2, 3 -> 32, relu6, letterbox gather) + MobileNetV2 block 0
 // (dw 3x3 on 32 ch + relu6, project 32 -> 16); weights: ws [32][32] bf16 with
 // K = (ky*3+kx)*3 + c (RGB), bs [32] f32, wd [9][32] f16, bd [32] f16, wp [16][32] f16, bp [16].

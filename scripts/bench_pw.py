@@ -86,3 +86,36 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def bench_tap(reps=20):
+    """ASPP atrous branches: conv_gemm (LDS-DMA, raster / tap-grouped) vs tap_conv."""
+    dev = torch.device("cuda")
+    B, H, W, Cin, Cout = 32, 33, 33, 320, 256
+    x = (torch.randn(B, H, W, Cin, device=dev) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(Cout, 3, 3, Cin, device=dev) / (9 * Cin) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(Cout, device=dev)
+    out = torch.empty(B, H, W, 1024, dtype=torch.bfloat16, device=dev)
+    wpk, bp = K.pack_tap_weights(w, b)
+    for rate in (6, 12, 18):
+        ref = out.clone()
+        K.conv_gemm(x, w, b, ref, B=B, IH=H, IW=W, Cin=Cin, OH=H, OW=W, Cout=Cout, k=3, dil=rate,
+                    ldo=1024, co_off=256, act="relu")
+        line = [f"aspp_r{rate}"]
+        pg = K.tap_group_perm(B, H, W, 3, rate, 128, dev)
+        us = timeit(lambda: K.conv_gemm(x, w, b, out, B=B, IH=H, IW=W, Cin=Cin, OH=H, OW=W, Cout=Cout,
+                                        k=3, dil=rate, ldo=1024, co_off=256, act="relu", variant=4,
+                                        perm=pg), reps)
+        line.append(f"gemm_v4g={us:6.1f}")
+        for grouped in (False, True):
+            perm = K.tap_group_perm(B, H, W, 3, rate, 256, dev) if grouped else None
+            out.zero_()
+            us = timeit(lambda: K.tap_conv(x, wpk, bp, out, B=B, H=H, W=W, Cin=Cin, Cout=Cout, k=3,
+                                           dil=rate, ldo=1024, co_off=256, act="relu", perm=perm), reps)
+            err = (out[..., 256:512].float() - ref[..., 256:512].float()).abs().max().item()
+            line.append(f"tap{'g' if grouped else ''}={us:6.1f}({err:.2g})")
+        print("  ".join(line), flush=True)
+
+
+if __name__ == "__main__" and os.environ.get("SSA_BENCH_TAP", "1") == "1":
+    bench_tap()

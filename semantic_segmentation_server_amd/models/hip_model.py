@@ -280,9 +280,27 @@ class HipDeepLab:
             co_off=0, act="relu"), x, b0w, b0b, cat, M=B * h * w, Cin=c, Cout=A, ldo=self.cat_c,
             co_off=0, act="relu"))
         for j, ((aw, ab), rate) in enumerate(self.aspp_atrous):
-            ops.append(lambda *_, x=x, h=h, w=w, c=c, aw=aw, ab=ab, rate=rate, j=j: K.conv_gemm(
-                x, aw, ab, cat, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w, Cout=A, k=3, dil=rate,
-                ldo=self.cat_c, co_off=(j + 1) * A, act="relu"))
+            # atrous branch: raster-order tiles, or tiles grouped by tap validity
+            # (tap_group_perm) so the kernel skips every all-padding tap
+            variants = []
+            if c in K.TAP_CIN and A % 8 == 0:
+                twp, tbp = K.pack_tap_weights(aw, ab)
+                for name, grouped in (("tap", False), ("tapg", True)):
+                    perm = K.tap_group_perm(B, h, w, 3, rate, 256, dev) if grouped else None
+                    variants.append((name, [
+                        lambda *_, x=x, h=h, w=w, c=c, twp=twp, tbp=tbp, rate=rate, j=j, perm=perm:
+                        K.tap_conv(x, twp, tbp, cat, B=B, H=h, W=w, Cin=c, Cout=A, k=3, dil=rate,
+                                   ldo=self.cat_c, co_off=(j + 1) * A, act="relu", perm=perm)]))
+            for name, variant, bm in (("v4", 4, 0), ("v4g", 4, 128), ("v5g", 5, 128),
+                                      ("v6g", 6, 256)):
+                perm = K.tap_group_perm(B, h, w, 3, rate, bm, dev) if bm else None
+                variants.append((name, [
+                    lambda *_, x=x, h=h, w=w, c=c, aw=aw, ab=ab, rate=rate, j=j, variant=variant,
+                    perm=perm: K.conv_gemm(
+                        x, aw, ab, cat, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w, Cout=A, k=3, dil=rate,
+                        ldo=self.cat_c, co_off=(j + 1) * A, act="relu", variant=variant,
+                        perm=perm)]))
+            ops.append(Choice(f"aspp.rate{rate}", variants))
         img_bias = None
         if self.has_pool:
             gap = buf("gap", B, c, dtype=torch.float32)
@@ -296,9 +314,10 @@ class HipDeepLab:
                                                 K=c, act="relu"))
             ops.append(lambda *_: K.matvec(pooled, self.proj_pool_w, None, img_bias, B=B, N=A, K=A))
         proj = buf("aspp_proj", B, h, w, A)
-        ops.append(lambda *_, h=h, w=w: K.conv_gemm(
-            cat, self.proj_w, self.proj_b, proj, B=B, IH=h, IW=w, Cin=self.cat_c, OH=h, OW=w,
-            Cout=A, k=1, act="relu", img_bias=img_bias))
+        ops.append(Choice("aspp.proj", [(f"v{v}", [
+            lambda *_, h=h, w=w, v=v: K.conv_gemm(
+                cat, self.proj_w, self.proj_b, proj, B=B, IH=h, IW=w, Cin=self.cat_c, OH=h, OW=w,
+                Cout=A, k=1, act="relu", img_bias=img_bias, variant=v)]) for v in (4, 3, 5, 6)]))
         logits = buf("logits", B, h, w, self.ldk)
         ops.append(pw_choice("logits", lambda *_, h=h, w=w: K.conv_gemm(
             proj, self.logit_w, self.logit_b, logits, B=B, IH=h, IW=w, Cin=A, OH=h, OW=w,
@@ -375,6 +394,18 @@ class HipDeepLab:
                 variants.insert(0, (f"tile{tile[0]}x{tile[1]}", [
                     lambda *_, x=inp, out=out, h=h, w=w, OH=OH, OW=OW, tile=tile: K.fused_ir(
                         x, fp, out, B=B, IH=h, IW=w, OH=OH, OW=OW, tile=tile)]))
+            shape = (-(-s.cout // 16), fp["CinP"] // 32)
+            if fp["we"] is not None and shape in K.FUSED_PERSIST_SHAPES:
+                for tile in _TILES:
+                    lds = K.fused_ir_persist_lds(fp["CinP"], fp["hidP"], s.cout, s.stride,
+                                                 s.dilation, *tile)
+                    covered = -(-OH // tile[0]) * tile[0] * -(-OW // tile[1]) * tile[1]
+                    if (0 < lds <= 80 * 1024 and -(-tile[0] * tile[1] // 16) <= 8
+                            and covered <= 1.25 * OH * OW):
+                        variants.insert(0, (f"persist{tile[0]}x{tile[1]}", [
+                            lambda *_, x=inp, out=out, h=h, w=w, OH=OH, OW=OW, tile=tile: K.fused_ir(
+                                x, fp, out, B=B, IH=h, IW=w, OH=OH, OW=OW, tile=tile,
+                                persist=True)]))
         if "fused" in blk:
             fp = blk["fused"]
             variants.insert(0, ("fused", [lambda *_, x=inp, out=out, h=h, w=w, OH=OH, OW=OW:

@@ -83,6 +83,54 @@ def test_conv_gemm(B, H, W, Cin, Cout, k, stride, dil, act, res, ldo_pad, co_off
         assert torch.all(out[..., co_off + Cout:] == 7.0)
 
 
+@pytest.mark.parametrize("B,H,W,rate", [(3, 33, 33, 6), (2, 33, 33, 12), (2, 33, 33, 18),
+                                         (2, 17, 21, 24)])
+@pytest.mark.parametrize("variant,bm", [(3, 128), (4, 128), (5, 128), (6, 256)])
+def test_conv_gemm_tap_grouped(B, H, W, rate, variant, bm):
+    """Dilated 3x3 through the tap-validity permutation: same result as raster order,
+    channel-slice write, padding rows (-1) write nothing."""
+    K = _hip()
+    Cin, Cout, co_off, ldo = 64, 96, 32, 160
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(B, Cin, H, W, generator=g).to(torch.bfloat16)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / (Cin * 9) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(Cout, generator=g)
+    ref = F.relu(F.conv2d(x.float(), w.float(), b, 1, rate, rate))
+    perm = K.tap_group_perm(B, H, W, 3, rate, bm, DEV)
+    assert perm.numel() % bm == 0
+    out = torch.full((B, H, W, ldo), 7.0, dtype=torch.bfloat16, device=DEV)
+    K.conv_gemm(_nhwc(x).to(DEV), w.permute(0, 2, 3, 1).contiguous().to(DEV), b.to(DEV), out,
+                B=B, IH=H, IW=W, Cin=Cin, OH=H, OW=W, Cout=Cout, k=3, dil=rate, ldo=ldo,
+                co_off=co_off, act="relu", variant=variant, perm=perm)
+    torch.cuda.synchronize()
+    assert _rel(_nchw(out[..., co_off:co_off + Cout]).cpu(), ref) < 1e-2
+    assert torch.all(out[..., :co_off] == 7.0) and torch.all(out[..., co_off + Cout:] == 7.0)
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,rate,grouped", [
+    (3, 33, 33, 320, 256, 6, True), (2, 33, 33, 320, 256, 12, False), (2, 33, 33, 320, 256, 18, True),
+    (2, 17, 21, 160, 96, 24, True), (1, 9, 11, 64, 200, 1, False), (2, 20, 20, 256, 136, 2, True)])
+def test_tap_conv(B, H, W, Cin, Cout, rate, grouped):
+    """tap_conv vs F.conv2d: raster or tap-grouped rows, channel-slice write, partial
+    128-channel group (Cout % 128 != 0)."""
+    K = _hip()
+    co_off, extra = 8, 16
+    ldo = co_off + Cout + extra
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(B, Cin, H, W, generator=g).to(torch.bfloat16)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / (Cin * 9) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(Cout, generator=g)
+    ref = F.relu(F.conv2d(x.float(), w.float(), b, 1, rate, rate))
+    wpk, bp = K.pack_tap_weights(w.permute(0, 2, 3, 1).contiguous().to(DEV), b.to(DEV))
+    perm = K.tap_group_perm(B, H, W, 3, rate, 256, DEV) if grouped else None
+    out = torch.full((B, H, W, ldo), 7.0, dtype=torch.bfloat16, device=DEV)
+    K.tap_conv(_nhwc(x).to(DEV), wpk, bp, out, B=B, H=H, W=W, Cin=Cin, Cout=Cout, k=3, dil=rate,
+               ldo=ldo, co_off=co_off, act="relu", perm=perm)
+    torch.cuda.synchronize()
+    assert _rel(_nchw(out[..., co_off:co_off + Cout]).cpu(), ref) < 1e-2
+    assert torch.all(out[..., :co_off] == 7.0) and torch.all(out[..., co_off + Cout:] == 7.0)
+
+
 def test_conv_gemm_img_bias():
     K = _hip()
     B, H, W, Cin, Cout = 3, 5, 7, 64, 48
@@ -455,9 +503,13 @@ def test_stem_block0_fused(cam, H, tile):
     (160, 160, 1, 2, 29, (8, 16)),   # partial tiles at the right/bottom edge
     (24, 32, 2, 1, 65, (8, 16)),     # stride 2, CinP 32
     (32, 64, 2, 1, 65, (5, 11)),
+    (16, 24, 2, 1, 67, (5, 11)),     # block 1 shape (CinP 32 from Cin 16)
+    (24, 24, 1, 1, 41, (11, 11)),    # block 2 shape: residual, Cin 24 -> CinP 32
+    (32, 32, 1, 1, 30, (8, 13)),     # blocks 4/5, partial edge tiles
     (32, 16, 1, 1, 37, (8, 16)),     # block 0: no expansion (t = 1)
 ])
-def test_fused_ir_tile(cin, cout, stride, dil, H, tile):
+@pytest.mark.parametrize("persist", [False, True])
+def test_fused_ir_tile(cin, cout, stride, dil, H, tile, persist):
     from semantic_segmentation_server_amd.models.layers import init_random
     from semantic_segmentation_server_amd.models.mobilenetv2 import InvertedResidual, IRSpec
     K = _hip()
@@ -484,8 +536,14 @@ def test_fused_ir_tile(cin, cout, stride, dil, H, tile):
     packed = K.pack_fused_ir(ew, eb, dwf[:, 0], dbf, pwf[:, :, 0, 0], pbf, Cin=cin,
                              hid=spec.hidden, Cout=cout, stride=stride, residual=spec.residual,
                              device=DEV, dil=dil)
+    if persist:
+        shape = (-(-cout // 16), packed["CinP"] // 32)
+        lds = K.fused_ir_persist_lds(packed["CinP"], packed["hidP"], cout, stride, dil, *tile)
+        if ew is None or shape not in K.FUSED_PERSIST_SHAPES or not 0 < lds <= 160 * 1024:
+            pytest.skip("no persistent instantiation for this block shape")
     out = torch.full((B, OH, OW, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
-    K.fused_ir(_nhwc(x).to(DEV), packed, out, B=B, IH=H, IW=W, OH=OH, OW=OW, tile=tile)
+    K.fused_ir(_nhwc(x).to(DEV), packed, out, B=B, IH=H, IW=W, OH=OH, OW=OW, tile=tile,
+               persist=persist)
     torch.cuda.synchronize()
     assert torch.isfinite(out).all()
     assert _rel(_nchw(out).cpu(), ref) < 2e-2

@@ -35,3 +35,39 @@ def test_pw_supported():
     assert K.pw_supported(160, 960) and K.pw_supported(24, 144) and K.pw_supported(320, 256)
     assert not K.pw_supported(960, 160)  # deep K: the generic implicit GEMM handles it
     assert not K.pw_supported(256, 21)   # N must be padded to a multiple of 8
+
+
+@pytest.mark.parametrize("B,H,W,dil,bm", [(2, 33, 33, 18, 128), (3, 33, 33, 6, 256), (1, 9, 7, 12, 128)])
+def test_tap_group_perm_is_tap_uniform(B, H, W, dil, bm):
+    """Every BM-row tile of the permutation holds pixels with one tap-validity pattern."""
+    p = K.tap_group_perm(B, H, W, 3, dil, bm)
+    assert p.numel() % bm == 0
+    v = p[p >= 0]
+    assert torch.equal(torch.sort(v).values, torch.arange(B * H * W, dtype=torch.int32))
+    for t in range(p.numel() // bm):
+        rows = p[t * bm:(t + 1) * bm]
+        rows = rows[rows >= 0].long() % (H * W)
+        if rows.numel() == 0:
+            continue
+        y, x = rows // W, rows % W
+        pat = torch.stack([(y - dil >= 0), (y + dil < H), (x - dil >= 0), (x + dil < W)], 1)
+        assert torch.all(pat == pat[0]), f"tile {t} mixes tap patterns"
+
+
+def test_pack_tap_roundtrip():
+    g = torch.Generator().manual_seed(1)
+    Cout, Cin = 200, 160
+    w = torch.randn(Cout, 3, 3, Cin, generator=g)
+    b = torch.randn(Cout, generator=g)
+    p, bp = K.pack_tap_weights(w, b)
+    G, KS = 2, 5
+    t5 = p.float().reshape(9, G, 8, KS, 64, 8)
+    rec = torch.zeros(9, G * 128, KS * 32)
+    for lane in range(64):
+        r, kq = lane % 16, lane // 16
+        for j in range(8):
+            for k in range(KS):
+                rec[:, j * 16 + r::128][:, :G, k * 32 + kq * 8:k * 32 + kq * 8 + 8] = t5[:, :, j, k, lane]
+    want = w.to(torch.bfloat16).float().reshape(Cout, 9, Cin).permute(1, 0, 2)
+    assert torch.equal(rec[:, :Cout, :Cin], want) and rec[:, Cout:].abs().sum() == 0
+    assert torch.equal(bp[:Cout], b) and bp[Cout:].abs().sum() == 0
