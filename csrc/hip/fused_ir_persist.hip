@@ -33,6 +33,7 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kPNW = 4;      // waves per workgroup
 constexpr int kPXPF = 8;     // max 16-byte input-tile loads per thread held for the prefetch
+constexpr int kPMaxG = 4;    // max expansion pixel groups per wave (halo tile <= 256 pixels)
 
 struct PIRArgs {
   const bf16* in; const bf16* we; const float* be; const f16* wd; const f16* bd;
@@ -136,6 +137,33 @@ __global__ __launch_bounds__(64 * kPNW) void fused_ir_persist_kernel(PIRArgs a) 
   store_x();
   __syncthreads();
 
+  // Tile-invariant per-lane geometry, computed once (the PMC profile of the first
+  // version showed ~38 VALU instructions per MFMA, mostly the integer divisions
+  // and address math of the halo pixels redone for every tile and every chunk):
+  //  * expansion groups of this wave: halo pixel (ty, tx), X / E element offsets;
+  //  * output groups: tile-local (py, px) and the depthwise base offset in E.
+  constexpr int MAXG = kPMaxG;  // expansion groups per wave
+  int gip[MAXG], gyx[MAXG];    // halo pixel index; (ty << 16 | tx), ty = 0x7fff for padding lanes
+#pragma unroll
+  for (int k = 0; k < MAXG; ++k) {
+    const int ip = (wid + k * kPNW) * 16 + r16;
+    const int ty = ip / TIW;
+    gip[k] = ip;
+    gyx[k] = ((ip < in_px ? ty : 0x7fff) << 16) | (ip - ty * TIW);
+  }
+  const int ngroups_w = (in_groups - wid + kPNW - 1) / kPNW;  // expansion groups this wave owns
+  int pofs[GPW], opy[GPW], opx[GPW];
+  bool pin[GPW];
+#pragma unroll
+  for (int g = 0; g < GPW; ++g) {
+    const int p = (wid * GPW + g) * 16 + r16;
+    opy[g] = p / a.TX;
+    opx[g] = p - opy[g] * a.TX;
+    pin[g] = p < a.TY * a.TX;
+    pofs[g] = pin[g] ? (opy[g] * s * TIW + opx[g] * s) * ES : 0;
+  }
+  const int dw_row = TIW * dl * ES, dw_col = dl * ES;  // tap strides in E (elements)
+
   const f16x8 h0 = {0, 0, 0, 0, 0, 0, 0, 0}, h6 = {6, 6, 6, 6, 6, 6, 6, 6};
   for (; tile < a.ntiles; tile += gridDim.x) {
     const int b = tile / ntile_img, t = tile - b * ntile_img;
@@ -144,17 +172,15 @@ __global__ __launch_bounds__(64 * kPNW) void fused_ir_persist_kernel(PIRArgs a) 
     const int next = tile + gridDim.x;
     if (next < a.ntiles) load_x(next);  // in flight under this tile's chunks
 
-    int pofs[GPW], oyv[GPW], oxv[GPW];
+    // this tile's image-border masks
+    unsigned inside = 0;
+#pragma unroll
+    for (int k = 0; k < MAXG; ++k)
+      if ((unsigned)(iy0 + (gyx[k] >> 16)) < (unsigned)a.IH && (unsigned)(ix0 + (gyx[k] & 0xffff)) < (unsigned)a.IW)
+        inside |= 1u << k;
     bool pval[GPW];
 #pragma unroll
-    for (int g = 0; g < GPW; ++g) {
-      const int p = (wid * GPW + g) * 16 + r16;
-      const int py = p / a.TX, px = p - py * a.TX;
-      oyv[g] = oy0 + py;
-      oxv[g] = ox0 + px;
-      pval[g] = p < a.TY * a.TX && oyv[g] < a.OH && oxv[g] < a.OW;
-      pofs[g] = pval[g] ? (py * s) * TIW + px * s : 0;
-    }
+    for (int g = 0; g < GPW; ++g) pval[g] = pin[g] && oy0 + opy[g] < a.OH && ox0 + opx[g] < a.OW;
     f32x4 acc[GPW][NSUB];
 #pragma unroll
     for (int g = 0; g < GPW; ++g)
@@ -171,14 +197,13 @@ __global__ __launch_bounds__(64 * kPNW) void fused_ir_persist_kernel(PIRArgs a) 
         for (int k = 0; k < KS; ++k) wfr[sub][k] = ld8(sWe + (c0 + sub * 16 + r16) * WES + k * 32 + kq * 8);
         bias[sub] = *reinterpret_cast<const f32x4*>(sBe + c0 + sub * 16 + kq * 4);
       }
-      for (int gi = wid; gi < in_groups; gi += kPNW) {
-        const int ip = gi * 16 + r16;
-        const int ty = ip / TIW, tx = ip - ty * TIW;
-        const int iy = iy0 + ty, ix = ix0 + tx;
-        const bool inside = ip < in_px && iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW;
+#pragma unroll
+      for (int kg = 0; kg < MAXG; ++kg) {
+        if (kg >= ngroups_w) break;
         bf16x8 xf[KS];
 #pragma unroll
-        for (int k = 0; k < KS; ++k) xf[k] = ld8(X + (size_t)ip * XS + k * 32 + kq * 8);
+        for (int k = 0; k < KS; ++k) xf[k] = ld8(X + gip[kg] * XS + k * 32 + kq * 8);
+        const bool in_img = (inside >> kg) & 1u;
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub) {
           f32x4 e = bias[sub];
@@ -186,8 +211,8 @@ __global__ __launch_bounds__(64 * kPNW) void fused_ir_persist_kernel(PIRArgs a) 
           for (int k = 0; k < KS; ++k) e = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[sub][k], xf[k], e, 0, 0, 0);
           f16x4 o = {(f16)e[0], (f16)e[1], (f16)e[2], (f16)e[3]};
           o = __builtin_elementwise_min(__builtin_elementwise_max(o, h0.lo), h6.lo);
-          if (!inside) o = h0.lo;  // zero padding applies to the expanded tensor
-          *reinterpret_cast<f16x4*>(E + (size_t)ip * ES + sub * 16 + kq * 4) = o;
+          if (!in_img) o = h0.lo;  // zero padding applies to the expanded tensor
+          *reinterpret_cast<f16x4*>(E + gip[kg] * ES + sub * 16 + kq * 4) = o;
         }
       }
       __syncthreads();
@@ -207,7 +232,7 @@ __global__ __launch_bounds__(64 * kPNW) void fused_ir_persist_kernel(PIRArgs a) 
         f16x8 v[9];
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap)
-          v[tap] = *reinterpret_cast<const f16x8*>(E + (size_t)(pofs[g] + ((tap / 3) * TIW + tap % 3) * dl) * ES + kq * 8);
+          v[tap] = *reinterpret_cast<const f16x8*>(E + pofs[g] + (tap / 3) * dw_row + (tap % 3) * dw_col + kq * 8);
         d[g] = bdv;
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) d[g] = v[tap] * wdv[tap] + d[g];
@@ -226,8 +251,8 @@ __global__ __launch_bounds__(64 * kPNW) void fused_ir_persist_kernel(PIRArgs a) 
 #pragma unroll
     for (int g = 0; g < GPW; ++g) {
       if (!pval[g]) continue;
-      bf16* op = a.out + (((size_t)b * a.OH + oyv[g]) * a.OW + oxv[g]) * a.Cout;
-      const bf16* rp = X + (size_t)(pofs[g] + dl * TIW + dl) * XS;
+      bf16* op = a.out + (((size_t)b * a.OH + oy0 + opy[g]) * a.OW + ox0 + opx[g]) * a.Cout;
+      const bf16* rp = X + (size_t)((opy[g] * s + dl) * TIW + opx[g] * s + dl) * XS;
 #pragma unroll
       for (int n = 0; n < NSUB; ++n) {
         const int co = n * 16 + kq * 4;
@@ -286,6 +311,7 @@ size_t fused_ir_persist_lds(int CinP, int hidP, int Cout, int stride, int dil, i
   const int in_groups = (TIH * TIW + 15) / 16;
   const int CoutP = (Cout + 15) / 16 * 16;
   if ((size_t)in_groups * 16 * (CinP / 8) > (size_t)kPXPF * 64 * kPNW) return 0;  // prefetch registers
+  if (in_groups > kPMaxG * kPNW) return 0;                                       // expansion groups per wave
   return (size_t)playout(CinP, hidP, CoutP, in_groups).total;
 }
 

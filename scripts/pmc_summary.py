@@ -21,8 +21,9 @@ def load(d):
 sets = [load(d) for d in sys.argv[1:]]
 # last step: from the last stem_kernel dispatch on
 def last_step(ds):
-    idx = [i for i, d in enumerate(ds) if "stem_kernel" in d["name"]]
-    return ds[idx[-1]:]
+    # one steady-state step: after the second-to-last post-processing finalize
+    idx = [i for i, d in enumerate(ds) if "k_finalize" in d["name"]]
+    return ds[idx[-2] + 1: idx[-1] + 1] if len(idx) >= 2 else ds
 
 
 steps = [last_step(s) for s in sets]
