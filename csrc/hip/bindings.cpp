@@ -90,6 +90,22 @@ PYBIND11_MODULE(_hip, m) {
           dw_project(p, S(stream));
         });
 
+  m.def("dw_proj_fused",
+        [](uintptr_t h, uintptr_t w, uintptr_t bp, uintptr_t res, uintptr_t out, int B, int IH,
+           int IW, int hid, int Cout, int OH, int OW, int stride, int dil, int waves,
+           uintptr_t stream, int rows) {
+          DwProjFusedParams p;
+          p.rows = rows;
+          p.h = P<const void>(h); p.w = P<const void>(w); p.bp = P<const float>(bp);
+          p.res = P<const bf16>(res); p.out = P<bf16>(out);
+          p.B = B; p.IH = IH; p.IW = IW; p.hid = hid; p.Cout = Cout; p.OH = OH; p.OW = OW;
+          p.stride = stride; p.dil = dil; p.waves = waves;
+          dw_proj_fused(p, S(stream));
+        },
+        py::arg("h"), py::arg("w"), py::arg("bp"), py::arg("res"), py::arg("out"), py::arg("B"),
+        py::arg("IH"), py::arg("IW"), py::arg("hid"), py::arg("Cout"), py::arg("OH"), py::arg("OW"),
+        py::arg("stride"), py::arg("dil"), py::arg("waves"), py::arg("stream"), py::arg("rows") = 0);
+
   m.def("depthwise3x3",
         [](uintptr_t in, uintptr_t w, uintptr_t bias, uintptr_t out, int B, int IH, int IW, int C,
            int OH, int OW, int stride, int dil, int act, uintptr_t stream) {
@@ -113,14 +129,19 @@ PYBIND11_MODULE(_hip, m) {
   m.def("pw_conv",
         [](uintptr_t in, uintptr_t w, uintptr_t img_bias, uintptr_t res,
            uintptr_t out, int M, int K, int N, int HW, int ldo, int co_off, int ldr, int act,
-           int mt, int nch, uintptr_t stream) {
+           int mt, int nch, uintptr_t stream, int out_f16) {
           PwConvParams p;
+          p.out_f16 = out_f16;
           p.in = P<const bf16>(in); p.w = P<const bf16>(w);
           p.img_bias = P<const float>(img_bias); p.res = P<const bf16>(res); p.out = P<bf16>(out);
           p.M = M; p.K = K; p.N = N; p.HW = HW; p.ldo = ldo; p.co_off = co_off; p.ldr = ldr;
           p.act = act; p.mt = mt; p.nch = nch;
           pw_conv(p, S(stream));
-        });
+        },
+        py::arg("in"), py::arg("w"), py::arg("img_bias"), py::arg("res"), py::arg("out"),
+        py::arg("M"), py::arg("K"), py::arg("N"), py::arg("HW"), py::arg("ldo"), py::arg("co_off"),
+        py::arg("ldr"), py::arg("act"), py::arg("mt"), py::arg("nch"), py::arg("stream"),
+        py::arg("out_f16") = 0);
   m.def("pw_conv_supported_ks", &pw_conv_supported_ks);
   m.def("tap_conv",
         [](uintptr_t in, uintptr_t w, uintptr_t bias, uintptr_t out, uintptr_t perm, int Mp, int B,

@@ -39,6 +39,7 @@ struct PwConvParams {
   int M = 0, K = 0, N = 0, HW = 1, ldo = 0, co_off = 0, ldr = 0, act = 0;
   int mt = 2;   // 16*mt pixels per wave (2 or 4)
   int nch = 1;  // 64-channel chunks per workgroup
+  int out_f16 = 0;  // 1: write fp16 instead of bf16 (same 2-byte layout)
 };
 void pw_conv(const PwConvParams& p, hipStream_t s);
 
@@ -139,6 +140,22 @@ struct DwProjectParams {
   int B = 0, IH = 0, IW = 0, hid = 0, Cout = 0, OH = 0, OW = 0, stride = 1, dil = 1;
 };
 void dw_project(const DwProjectParams& p, hipStream_t s);
+
+// Depthwise + projection, weight-streamed (dw_proj.hip), fp16 internals. w is
+// host-packed per 32-channel hidden chunk: [Cout/16 subtiles][64 lanes][8] fp16
+// projection fragments, then [9][32] fp16 depthwise weights and [32] fp16 biases,
+// padded to (Cout/16 + 1) KiB (hip_ops.pack_dw_proj).
+struct DwProjFusedParams {
+  const void* h = nullptr;     // [B, IH, IW, hid] expanded activations, fp16
+  const void* w = nullptr;     // packed
+  const float* bp = nullptr;   // [Cout] projection bias
+  const bf16* res = nullptr;   // optional [B, OH, OW, Cout]
+  bf16* out = nullptr;         // [B, OH, OW, Cout]
+  int B = 0, IH = 0, IW = 0, hid = 0, Cout = 0, OH = 0, OW = 0, stride = 1, dil = 1;
+  int waves = 4;               // 4 or 8 waves (16 pixels each) per workgroup
+  int rows = 0;                // > 0: row-tile variant, this many output rows per workgroup
+};
+void dw_proj_fused(const DwProjFusedParams& p, hipStream_t s);
 
 // Depthwise KxK (K=3) conv, NHWC, pad = dil, bias + act. w: [9, C] fp32.
 void depthwise3x3(const bf16* in, const float* w, const float* bias, bf16* out, int B, int IH,

@@ -1004,7 +1004,10 @@ void postprocess(const PostParams& p, hipStream_t s) {
   if (st++ < stages) hipLaunchKernelGGL(k_ccl_boundary, gp, blk, 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_compress, gp, blk, 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_roots, gp, blk, 0, s, a);
-  const dim3 gs(kQuadBlocks, p.B);
+  // strip-privatised passes: kQuadBlocks strips per frame (SSA_QUAD_BLOCKS overrides, tuning)
+  const char* qb_env = getenv("SSA_QUAD_BLOCKS");
+  const int qblocks = qb_env ? std::max(1, atoi(qb_env)) : kQuadBlocks;
+  const dim3 gs(qblocks, p.B);
   if (st++ < stages) hipLaunchKernelGGL(k_quads, gs, blk, 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_tree, gp, blk, 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_select, gp, blk, 0, s, a);

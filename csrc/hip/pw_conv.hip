@@ -35,11 +35,12 @@ namespace {
 struct PwArgs {
   const bf16* in; const bf16* w; const float* img_bias; const bf16* res;
   bf16* out;
-  int M, K, N, HW, ldo, co_off, ldr, act, nch, ngroups, NC, out_bytes;
+  int M, K, N, HW, ldo, co_off, ldr, act, nch, ngroups, NC, out_bytes, out_f16;
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 template <int MT, int KS>
 __global__ __launch_bounds__(256) void pw_conv_kernel(PwArgs a) {
@@ -176,11 +177,20 @@ __global__ __launch_bounds__(256) void pw_conv_kernel(PwArgs a) {
 #pragma unroll
           for (int q = 0; q < 8; ++q) v[q] += (float)rv[q];
         }
-        bf16x8 o;
+        u32x4 ob;
+        if (a.out_f16) {  // fp16 activations for the fp16 depthwise consumers (dw_proj.hip)
+          f16x8 o;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) o[q] = (bf16)fminf(fmaxf(v[q], lo), hi);
+          for (int q = 0; q < 8; ++q) o[q] = (_Float16)fminf(fmaxf(v[q], lo), hi);
+          ob = __builtin_bit_cast(u32x4, o);
+        } else {
+          bf16x8 o;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) o[q] = (bf16)fminf(fmaxf(v[q], lo), hi);
+          ob = __builtin_bit_cast(u32x4, o);
+        }
         const int off = ok ? (m * a.ldo + a.co_off + n) * 2 : a.out_bytes;  // >= num_records: dropped
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), orsrc, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(ob, orsrc, off, 0, 0);
       }
     }
   }
@@ -233,7 +243,7 @@ void pw_conv(const PwConvParams& p, hipStream_t s) {
     throw std::invalid_argument("pw_conv: tensor too large for 32-bit buffer offsets");
   const int NC = (p.N + 63) / 64;
   PwArgs a{p.in, p.w, p.img_bias, p.res, p.out, p.M, p.K, p.N, p.HW, p.ldo, p.co_off,
-           p.ldr, p.act, p.nch, (NC + p.nch - 1) / p.nch, NC, (int)out_bytes};
+           p.ldr, p.act, p.nch, (NC + p.nch - 1) / p.nch, NC, (int)out_bytes, p.out_f16};
   const bool ok = p.mt == 4 ? dispatch_pw<4>(a, KS, s) : dispatch_pw<2>(a, KS, s);
   if (!ok) throw std::invalid_argument("pw_conv: no kernel for this K");
 }

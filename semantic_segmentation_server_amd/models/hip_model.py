@@ -408,6 +408,24 @@ class HipDeepLab:
             d, pw_, pb_, out, B=B, IH=OH, IW=OW, Cin=hid, OH=OH, OW=OW, Cout=s.cout, k=1,
             act=None, res=res))
         variants = [("unfused", unfused)]
+        if (blk["expand"] is not None and hid % 32 == 0 and s.cout in K.DWP_COUT
+                and K.pw_supported(c, hid)):
+            # expansion (weight-streamed, fp16 out) -> fused depthwise + projection
+            ew, eb = blk["expand"]
+            e16 = buf(f"b{i}_exp16", B, h, w, hid, dtype=torch.float16)
+            ewpk = K.pack_pw_weights(ew, eb)
+            wpk_dp = K.pack_dw_proj(pw_[:, 0, 0, :], dw_w, dw_b)
+            M = B * h * w
+            dwp_cfgs = [("w", 4, 0)] + ([("r", 4, ty) for ty in (2, 3, 4)] if s.stride == 1 else [])
+            for mt, nch in ((2, 3),):
+                for kind, nw, ty in dwp_cfgs:
+                    variants.append((f"dwp{kind}{nw if not ty else ty}.pw{mt}x{nch}", [
+                        lambda *_, x=inp, e16=e16, M=M, c=c, mt=mt, nch=nch: K.pw_conv(
+                            x, ewpk, e16, M=M, K=c, N=hid, act="relu6", mt=mt, nch=nch),
+                        lambda *_, e16=e16, out=out, h=h, w=w, OH=OH, OW=OW, res=res, nw=nw, ty=ty:
+                        K.dw_proj_fused(e16, wpk_dp, pb_, out, B=B, IH=h, IW=w, hid=hid,
+                                        Cout=s.cout, OH=OH, OW=OW, stride=s.stride,
+                                        dil=s.dilation, res=res, waves=nw, rows=ty)]))
         if "dwproj" in blk:
             dpw, dpb = blk["dwproj"]
             e = unfused_expand_out

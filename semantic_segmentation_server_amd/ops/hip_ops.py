@@ -161,7 +161,8 @@ def pack_pw_weights(w: torch.Tensor, bias: torch.Tensor, N_out: Optional[int] = 
 def pw_conv(x, wpk, out, *, M, K, N, ldo=None, co_off=0, act=None, res=None, ldr=None,
             img_bias=None, HW=1, mt=2, nch=1) -> torch.Tensor:
     """Weight-streamed 1x1 conv (pw_conv.hip). x: [M, K] bf16 (NHWC pixels), wpk from
-    ``pack_pw_weights`` (weights + bias), out [M, ldo] bf16 at channel offset co_off."""
+    ``pack_pw_weights`` (weights + bias), out [M, ldo] bf16 (or fp16: written as fp16)
+    at channel offset co_off."""
     ldo = N if ldo is None else ldo
     ldr = N if ldr is None else ldr
     if not pw_supported(K, N) or ldo % 8 or co_off % 8 or (res is not None and ldr % 8):
@@ -171,7 +172,8 @@ def pw_conv(x, wpk, out, *, M, K, N, ldo=None, co_off=0, act=None, res=None, ldr
     NC, KS = -(-N // 64), -(-K // 32)
     _chk(x, torch.bfloat16, "x", M * K)
     _chk(wpk, torch.bfloat16, "wpk", NC * (4 * KS + 1) * 512)
-    _chk(out, torch.bfloat16, "out", M * ldo)
+    out_f16 = out.dtype == torch.float16
+    _chk(out, torch.float16 if out_f16 else torch.bfloat16, "out", M * ldo)
     if res is not None:
         _chk(res, torch.bfloat16, "res", M * ldr)
     if img_bias is not None:
@@ -179,7 +181,7 @@ def pw_conv(x, wpk, out, *, M, K, N, ldo=None, co_off=0, act=None, res=None, ldr
         if M % HW:
             raise ValueError("pw_conv: M must be a multiple of HW with img_bias")
     _hip_mod().pw_conv(_ptr(x), _ptr(wpk), _ptr(img_bias), _ptr(res), _ptr(out), M, K, N, HW, ldo,
-                       co_off, ldr, ACT[act], mt, nch, _stream())
+                       co_off, ldr, ACT[act], mt, nch, _stream(), int(out_f16))
     _dbg('pw_conv')
     return out
 
@@ -283,6 +285,47 @@ def dw_project(hid_in, wd, bd, wp, bp, out, *, B, IH, IW, hid, Cout, OH, OW, str
     _hip_mod().dw_project(_ptr(hid_in), _ptr(wd), _ptr(bd), _ptr(wp), _ptr(bp), _ptr(res), _ptr(out),
                           B, IH, IW, hid, Cout, OH, OW, stride, dil, _stream())
     _dbg('dw_project')
+    return out
+
+
+DWP_COUT = (64, 96, 160, 320)  # dw_proj_fused instantiations
+
+
+def pack_dw_proj(wp: torch.Tensor, wd9: torch.Tensor, bd: torch.Tensor) -> torch.Tensor:
+    """Operand of dw_proj_fused (fp16). wp [Cout, hid] projection, wd9 [9, hid]
+    depthwise (tap-major), bd [hid]. Per 32-channel hidden chunk c: the projection
+    fragments [Cout/16][64 lanes][8], element (n, lane, e) = wp[n*16 + lane%16][c*32 +
+    (lane//16)*8 + e], then wd9[:, c*32:(c+1)*32] and bd[c*32:(c+1)*32], zero-padded
+    to (Cout/16 + 1) KiB."""
+    Cout, hid = wp.shape
+    NS, NC = Cout // 16, hid // 32
+    frag = wp.float().reshape(NS, 16, NC, 4, 8).permute(2, 0, 3, 1, 4).reshape(NC, NS * 512)
+    dw = torch.zeros(NC, 512, dtype=torch.float32, device=wp.device)  # 1 KiB of fp16
+    dw[:, :288] = wd9.float().reshape(9, NC, 32).permute(1, 0, 2).reshape(NC, 288)
+    dw[:, 288:320] = bd.float().reshape(NC, 32)
+    return torch.cat([frag, dw], dim=1).to(torch.float16).contiguous()
+
+
+def dw_proj_fused(h, wpk, bp, out, *, B, IH, IW, hid, Cout, OH, OW, stride=1, dil=1, res=None,
+                  waves=4, rows=0):
+    """Depthwise 3x3 + ReLU6 + 1x1 projection (+ residual), dw_proj.hip. h [B,IH,IW,hid]
+    fp16 (pw_conv out_f16); wpk from ``pack_dw_proj``; bp [Cout] fp32; out bf16.
+    ``rows > 0``: row-tile variant (``rows`` output rows per workgroup, halo in LDS)."""
+    if hid % 32 or Cout not in DWP_COUT or waves not in (4, 8):
+        raise ValueError(f"dw_proj_fused: unsupported hid={hid} Cout={Cout}")
+    if rows and (stride != 1 or -(-rows * OW // 16) > 16):
+        raise ValueError("dw_proj_fused: row tiles need stride 1 and <= 256 pixels")
+    if (OH, OW) != ((IH - 1) // stride + 1, (IW - 1) // stride + 1):
+        raise ValueError("dw_proj_fused: output size mismatch")
+    _chk(h, torch.float16, "h", B * IH * IW * hid)
+    _chk(wpk, torch.float16, "wpk", (hid // 32) * (Cout // 16 + 1) * 512)
+    _chk(bp, torch.float32, "bp", Cout)
+    _chk(out, torch.bfloat16, "out", B * OH * OW * Cout)
+    if res is not None:
+        _chk(res, torch.bfloat16, "res", B * OH * OW * Cout)
+    _hip_mod().dw_proj_fused(_ptr(h), _ptr(wpk), _ptr(bp), _ptr(res), _ptr(out), B, IH, IW, hid,
+                             Cout, OH, OW, stride, dil, waves, _stream(), rows)
+    _dbg('dw_proj_fused')
     return out
 
 

@@ -576,6 +576,53 @@ def test_dw_project(hid, cout, stride, dil, res):
     assert _rel(_nchw(out).cpu(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("hid,cout,stride,dil,res", [(576, 96, 1, 1, True), (576, 160, 1, 1, False),
+                                                     (960, 160, 1, 2, True), (960, 320, 1, 2, False),
+                                                     (384, 64, 2, 1, False), (384, 64, 1, 1, True)])
+@pytest.mark.parametrize("waves,rows", [(4, 0), (8, 0), (4, 2), (4, 3)])
+def test_dw_proj_fused(hid, cout, stride, dil, res, waves, rows):
+    """Weight-streamed depthwise + projection (dw_proj.hip) vs the torch composition."""
+    K = _hip()
+    if rows and stride != 1:
+        pytest.skip("row tiles: stride 1 only")
+    g = torch.Generator().manual_seed(11)
+    B, H = 3, 19
+    x = F.relu6(torch.randn(B, hid, H, H, generator=g) * 2).to(torch.bfloat16)
+    wd = torch.randn(hid, 1, 3, 3, generator=g) / 3
+    bd = torch.randn(hid, generator=g) * 0.1
+    wp = (torch.randn(cout, hid, generator=g) / hid ** 0.5).to(torch.bfloat16)
+    bp = torch.randn(cout, generator=g) * 0.1
+    d = F.relu6(F.conv2d(x.float(), wd, bd, stride, dil, dil, groups=hid)).to(torch.bfloat16).float()
+    ref = F.conv2d(d, wp.float()[:, :, None, None], bp)
+    OH, OW = ref.shape[-2:]
+    r = torch.randn(B, cout, OH, OW, generator=g).to(torch.bfloat16) if res else None
+    if res:
+        ref = ref + r.float()
+    wpk = K.pack_dw_proj(wp.to(DEV), wd.reshape(hid, 9).t().contiguous().to(DEV), bd.to(DEV))
+    out = torch.full((B, OH, OW, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
+    K.dw_proj_fused(_nhwc(x).to(DEV).half(), wpk, bp.to(DEV), out, B=B, IH=H, IW=H, hid=hid, Cout=cout,
+                    OH=OH, OW=OW, stride=stride, dil=dil, res=None if r is None else _nhwc(r).to(DEV),
+                    waves=waves, rows=rows)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    assert _rel(_nchw(out).cpu(), ref) < 2e-2  # fp16 depthwise: rounding differs from bf16
+
+
+def test_pw_conv_fp16_out():
+    K = _hip()
+    g = torch.Generator().manual_seed(12)
+    M, Cin, Cout = 1500, 96, 576
+    x = (torch.randn(M, Cin, generator=g) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(Cout, Cin, generator=g) / Cin ** 0.5).to(torch.bfloat16)
+    b = torch.randn(Cout, generator=g)
+    ref = F.relu6(x.float() @ w.float().t() + b)
+    out = torch.empty(M, Cout, dtype=torch.float16, device=DEV)
+    K.pw_conv(x.to(DEV), K.pack_pw_weights(w.to(DEV), b.to(DEV)), out, M=M, K=Cin, N=Cout,
+              act="relu6", mt=2, nch=3)
+    torch.cuda.synchronize()
+    assert _rel(out.float().cpu(), ref) < 2e-3
+
+
 @pytest.mark.parametrize("Cin,Cout,k,stride,dil,res,mode", [
     (64, 256, 1, 1, 1, True, "i8"), (256, 64, 3, 2, 1, False, "i8"), (512, 512, 3, 1, 2, False, "i8"),
     (256, 19, 1, 1, 1, False, "bf16"), (1024, 256, 1, 1, 1, False, "i8")])

@@ -71,3 +71,26 @@ def test_pack_tap_roundtrip():
     want = w.to(torch.bfloat16).float().reshape(Cout, 9, Cin).permute(1, 0, 2)
     assert torch.equal(rec[:, :Cout, :Cin], want) and rec[:, Cout:].abs().sum() == 0
     assert torch.equal(bp[:Cout], b) and bp[Cout:].abs().sum() == 0
+
+
+def test_pack_dw_proj_layout():
+    g = torch.Generator().manual_seed(2)
+    Cout, hid = 96, 192
+    wp = torch.randn(Cout, hid, generator=g)
+    wd9 = torch.randn(9, hid, generator=g)
+    bd = torch.randn(hid, generator=g)
+    p = K.pack_dw_proj(wp, wd9, bd)
+    assert p.dtype == torch.float16
+    NS, NC = Cout // 16, hid // 32
+    chunks = p.reshape(NC, (NS + 1) * 512).float()
+    for c in range(NC):
+        frag = chunks[c, :NS * 512].reshape(NS, 64, 8)
+        for n in range(NS):
+            for lane in range(64):
+                r, kq = lane % 16, lane // 16
+                want = wp[n * 16 + r, c * 32 + kq * 8: c * 32 + kq * 8 + 8].half().float()
+                assert torch.equal(frag[n, lane], want)
+        dw = chunks[c, NS * 512:]
+        assert torch.equal(dw[:288].reshape(9, 32), wd9[:, c * 32:(c + 1) * 32].half().float())
+        assert torch.equal(dw[288:320], bd[c * 32:(c + 1) * 32].half().float())
+        assert dw[320:].abs().sum() == 0
