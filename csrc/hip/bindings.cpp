@@ -5,6 +5,8 @@
 // live in the Python wrappers (semantic_segmentation_server_amd/ops/hip_ops.py).
 #include <pybind11/pybind11.h>
 
+#include <vector>
+
 #include "kernels.h"
 
 namespace py = pybind11;
@@ -38,6 +40,31 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("OW"), py::arg("Cout"), py::arg("KH"), py::arg("KW"), py::arg("stride"),
         py::arg("dil"), py::arg("ldo"), py::arg("co_off"), py::arg("ldr"), py::arg("act"),
         py::arg("stream"), py::arg("variant") = 0, py::arg("perm") = 0, py::arg("Mp") = 0);
+
+  m.def("conv_gemm_grouped",
+        [](py::list groups, uintptr_t order, int nblocks, int variant, uintptr_t stream) {
+          // groups: tuples (in, w, bias, img_bias, res, out, B, IH, IW, Cin, OH, OW, Cout,
+          //                 KH, KW, stride, dil, ldo, co_off, ldr, act, perm, Mp)
+          std::vector<ConvParams> ps;
+          for (auto item : groups) {
+            auto t = item.cast<py::tuple>();
+            if (t.size() != 23) throw std::invalid_argument("conv_gemm_grouped: 23-tuple per conv");
+            auto I = [&](int i) { return t[i].cast<int>(); };
+            auto U = [&](int i) { return t[i].cast<uintptr_t>(); };
+            ConvParams p;
+            p.in = P<const bf16>(U(0)); p.w = P<const bf16>(U(1)); p.bias = P<const float>(U(2));
+            p.img_bias = P<const float>(U(3)); p.res = P<const bf16>(U(4)); p.out = P<bf16>(U(5));
+            p.B = I(6); p.IH = I(7); p.IW = I(8); p.Cin = I(9); p.OH = I(10); p.OW = I(11);
+            p.Cout = I(12); p.KH = I(13); p.KW = I(14); p.stride = I(15); p.dil = I(16);
+            p.ldo = I(17); p.co_off = I(18); p.ldr = I(19); p.act = I(20);
+            p.perm = P<const int>(U(21)); p.Mp = I(22);
+            ps.push_back(p);
+          }
+          conv_gemm_grouped(ps.data(), (int)ps.size(), P<const int>(order), nblocks, variant,
+                            S(stream));
+        },
+        py::arg("groups"), py::arg("order"), py::arg("nblocks"), py::arg("variant"),
+        py::arg("stream"));
 
   m.def("fused_ir",
         [](uintptr_t in, uintptr_t we, uintptr_t be, uintptr_t wd, uintptr_t bd, uintptr_t wp,

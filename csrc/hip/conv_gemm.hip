@@ -36,6 +36,12 @@ struct ConvArgs {
   int Mp;           // rows of the permuted GEMM (perm != null)
 };
 
+constexpr int kMaxConvGroup = 4;
+struct ConvGroupArgs {
+  ConvArgs g[kMaxConvGroup];
+  const int* order;  // [nblocks] (group << 24) | tile
+};
+
 template <int MT, int NT>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   const int lane = threadIdx.x & 63;
@@ -470,15 +476,16 @@ __device__ __attribute__((aligned(16))) int4 g_zero_page[8];
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-template <int MT, int NT, int ST, int WM = 2, int WN = 2>
-__global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(ConvArgs a) {
+// One BM x BN output tile (tile index bid in row-major (m-tile, n-tile) order) of
+// the LDS-DMA conv GEMM; shared by the single-conv kernel and the grouped kernel.
+template <int MT, int NT, int ST, int WM, int WN>
+__device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char* smem) {
   constexpr int NW = WM * WN;                            // waves: WM (pixels) x WN (channels)
   constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN, ROWB = 128;  // BK = 64 bf16 per stage row
   constexpr int GA = BM / (8 * NW), GB = BN / (8 * NW);  // glds per thread per stage
   static_assert(GA * 8 * NW == BM && GB * 8 * NW == BN, "tile rows must split over the waves");
   constexpr int SB = (BM + BN) * ROWB;
   constexpr int VM_INFLIGHT = (ST - 2) * (GA + GB);
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   int* s_tap = reinterpret_cast<int*>(smem + ST * SB);
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -489,8 +496,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(ConvArgs a) {
   // of equal tap validity into whole tiles (dilated ASPP branches: the tile tap
   // mask below then skips every all-padding tap, not only the row-uniform ones)
   const int M = a.perm ? a.Mp : a.B * a.OH * a.OW;
-  const int tiles_m = cdiv_dev(M, BM), tiles_n = cdiv_dev(a.Cout, BN);
-  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tiles_n = cdiv_dev(a.Cout, BN);
   const int tn = bid % tiles_n, tm = bid / tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int taps = a.KH * a.KW;
@@ -648,6 +654,50 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(ConvArgs a) {
 }
 
 template <int MT, int NT, int ST, int WM = 2, int WN = 2>
+__global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN;
+  const int M = a.perm ? a.Mp : a.B * a.OH * a.OW;
+  const int tiles = cdiv_dev(M, BM) * cdiv_dev(a.Cout, BN);
+  glds_tile<MT, NT, ST, WM, WN>(a, xcd_remap(blockIdx.x, tiles), smem);
+}
+
+// Grouped launch: up to kMaxConvGroup independent convs (the ASPP branches, which
+// read the same input and write disjoint channel slices of one concat buffer) in
+// ONE grid. Block i runs tile order[i] = (group << 24) | tile; the host sorts the
+// tiles by live-tap work, heaviest first (LPT), so the per-branch grids that left
+// half the CUs idle (137 256x256 tiles of a 34848 x 256 GEMM on 256 CUs) become
+// one balanced grid with no per-branch tail.
+template <int MT, int NT, int ST, int WM = 2, int WN = 2>
+__global__ __launch_bounds__(64 * WM * WN) void conv_glds_group_kernel(ConvGroupArgs ga) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int e = __builtin_amdgcn_readfirstlane(ga.order[blockIdx.x]);
+  const int t = e & 0xffffff;
+  switch (e >> 24) {  // constant indices: each arm reads its ConvArgs straight from kernarg
+    case 0: glds_tile<MT, NT, ST, WM, WN>(ga.g[0], t, smem); break;
+    case 1: glds_tile<MT, NT, ST, WM, WN>(ga.g[1], t, smem); break;
+    case 2: glds_tile<MT, NT, ST, WM, WN>(ga.g[2], t, smem); break;
+    default: glds_tile<MT, NT, ST, WM, WN>(ga.g[3], t, smem); break;
+  }
+}
+
+template <int MT, int NT, int ST, int WM = 2, int WN = 2>
+static void launch_conv_glds_group(const ConvGroupArgs& ga, int nblocks, hipStream_t s) {
+  constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN;
+  const size_t lds = (size_t)ST * (BM + BN) * 128 + 16;
+  static bool attr_set = false;
+  if (!attr_set) {
+    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_glds_group_kernel<MT, NT, ST, WM, WN>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
+          "conv_glds_group attr");
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((conv_glds_group_kernel<MT, NT, ST, WM, WN>), dim3(nblocks),
+                     dim3(64 * WM * WN), lds, s, ga);
+  check_launch("conv_glds_group");
+}
+
+template <int MT, int NT, int ST, int WM = 2, int WN = 2>
 static void launch_conv_glds(const ConvArgs& a, hipStream_t s) {
   constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN;
   const int M = a.perm ? a.Mp : a.B * a.OH * a.OW;
@@ -792,6 +842,36 @@ void conv_gemm(const ConvParams& p, hipStream_t s) {
     launch_conv<2, 2>(a, s);  // 64 px x 64 ch
   } else {
     launch_conv<2, 4>(a, s);  // 64 px x 128 ch
+  }
+}
+
+static ConvArgs to_args(const ConvParams& p) {
+  return ConvArgs{p.in, p.w, p.bias, p.img_bias, p.res, p.out, p.B, p.IH, p.IW, p.Cin, p.OH, p.OW,
+                  p.Cout, p.KH, p.KW, p.stride, p.dil, p.ldo, p.co_off, p.ldr, p.act, p.perm, p.Mp};
+}
+
+void conv_gemm_grouped(const ConvParams* ps, int n, const int* order, int nblocks, int variant,
+                       hipStream_t s) {
+  if (n < 1 || n > kMaxConvGroup) throw std::invalid_argument("conv_gemm_grouped: 1..4 convs");
+  if (!order || nblocks < 1) throw std::invalid_argument("conv_gemm_grouped: empty tile order");
+  ConvGroupArgs ga{};
+  for (int i = 0; i < kMaxConvGroup; ++i) {
+    const ConvParams& p = ps[i < n ? i : 0];
+    if (p.Cin % 8 != 0 || p.KH * p.KW > 16 || p.Cout != ps[0].Cout)
+      throw std::invalid_argument("conv_gemm_grouped: Cin % 8, <= 16 taps and one Cout required");
+    if ((long long)p.B * p.IH * p.IW * p.Cin >= (1LL << 31) ||
+        (long long)p.Cout * p.KH * p.KW * p.Cin >= (1LL << 31))
+      throw std::invalid_argument("conv_gemm_grouped: tensor too large for 32-bit offsets");
+    ga.g[i] = to_args(p);
+  }
+  ga.order = order;
+  switch (variant) {
+    case 5: launch_conv_glds_group<4, 4, 2, 2, 4>(ga, nblocks, s); break;   // 128 x 256, 8 waves
+    case 6: launch_conv_glds_group<8, 4, 2, 2, 4>(ga, nblocks, s); break;   // 256 x 256, 8 waves
+    case 8: launch_conv_glds_group<4, 4, 3, 2, 4>(ga, nblocks, s); break;   // 128 x 256, 3 stages
+    case 10: launch_conv_glds_group<4, 4, 4, 2, 2>(ga, nblocks, s); break;  // 128 x 128, 4 stages
+    case 11: launch_conv_glds_group<4, 4, 2, 2, 2>(ga, nblocks, s); break;  // 128 x 128, 2 stages
+    default: throw std::invalid_argument("conv_gemm_grouped: variant must be 5, 6, 8, 10 or 11");
   }
 }
 

@@ -26,6 +26,12 @@ struct ConvParams {
   int Mp = 0;
 };
 void conv_gemm(const ConvParams& p, hipStream_t s);
+// n (<= 4) independent LDS-DMA convs with one Cout in one grid; order[i] =
+// (group << 24) | tile picks block i's tile (row-major (m-tile, n-tile) of that
+// conv's GEMM, BM x BN of the variant: 5 128x256, 6 256x256, 8 128x256 3-stage,
+// 10 128x128 4-stage, 11 128x128 2-stage).
+void conv_gemm_grouped(const ConvParams* ps, int n, const int* order, int nblocks, int variant,
+                       hipStream_t s);
 
 // Pointwise conv, weight-streamed (pw_conv.hip). w is host-packed per 64-channel
 // chunk: weights in MFMA fragment order [4][ceil(K/32)][64 lanes][8] bf16 followed by

@@ -275,6 +275,7 @@ class HipDeepLab:
         A = self.aspp_c
         cat = buf("aspp_cat", B, h, w, self.cat_c)
         b0w, b0b = self.aspp_b0
+        aspp_at = len(ops)
         ops.append(pw_choice("aspp.b0", lambda *_, x=x, h=h, w=w, c=c: K.conv_gemm(
             x, b0w, b0b, cat, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w, Cout=A, k=1, ldo=self.cat_c,
             co_off=0, act="relu"), x, b0w, b0b, cat, M=B * h * w, Cin=c, Cout=A, ldo=self.cat_c,
@@ -301,6 +302,25 @@ class HipDeepLab:
                         ldo=self.cat_c, co_off=(j + 1) * A, act="relu", variant=variant,
                         perm=perm)]))
             ops.append(Choice(f"aspp.rate{rate}", variants))
+        if len(self.aspp_atrous) <= 3 and c % 8 == 0:
+            # all spatial branches (1x1 + atrous) in ONE LPT-ordered LDS-DMA grid
+            # (conv_gemm_grouped) against the per-branch launches above
+            seq = ("separate", ops[aspp_at:])
+            grouped = []
+            for gv in (5, 6, 8, 11):
+                BM = K.GROUP_TILE[gv][0]
+                convs = [dict(x=x, w=b0w, bias=b0b, out=cat, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w,
+                              Cout=A, k=1, dil=1, ldo=self.cat_c, co_off=0, act="relu")]
+                for j, ((aw, ab), rate) in enumerate(self.aspp_atrous):
+                    convs.append(dict(x=x, w=aw, bias=ab, out=cat, B=B, IH=h, IW=w, Cin=c, OH=h,
+                                      OW=w, Cout=A, k=3, dil=rate, ldo=self.cat_c,
+                                      co_off=(j + 1) * A, act="relu",
+                                      perm=K.tap_group_perm(B, h, w, 3, rate, BM, dev)))
+                order = K.grouped_tile_order(convs, gv, dev)
+                bufs[f"aspp_order{gv}"] = order
+                grouped.append((f"grouped_v{gv}", [
+                    lambda *_, convs=convs, order=order, gv=gv: K.conv_gemm_grouped(convs, order, gv)]))
+            ops[aspp_at:] = [Choice("aspp.branches", grouped + [seq])]
         img_bias = None
         if self.has_pool:
             gap = buf("gap", B, c, dtype=torch.float32)

@@ -7,7 +7,7 @@ capture that is the capture stream, so the launches are recorded into the graph.
 """
 from __future__ import annotations
 
-from typing import Optional
+from typing import List, Optional
 
 import os
 
@@ -127,6 +127,103 @@ def tap_group_perm(B: int, H: int, W: int, k: int, dil: int, BM: int, device=Non
         if pad:
             order.append(torch.full((pad,), -1, dtype=torch.long))
     return torch.cat(order).to(torch.int32).to(device).contiguous()
+
+
+GROUP_TILE = {5: (128, 256), 6: (256, 256), 8: (128, 256), 10: (128, 128), 11: (128, 128)}
+
+
+def _tile_taps(B: int, H: int, W: int, k: int, dil: int, BM: int,
+               perm: Optional[torch.Tensor]) -> torch.Tensor:
+    """Live taps per BM-row tile of a stride-1 'same' kxk conv's GEMM (the union of
+    the in-image taps of the tile's rows, as the kernel's per-tile tap mask)."""
+    r = dil * (k // 2)
+    ys, xs = torch.arange(H), torch.arange(W)
+    bits = torch.zeros(H, W, dtype=torch.long)
+    for t in range(k * k):
+        dy, dx = (t // k) * dil - r, (t % k) * dil - r
+        oky = ((ys + dy >= 0) & (ys + dy < H))[:, None]
+        okx = ((xs + dx >= 0) & (xs + dx < W))[None, :]
+        bits |= (oky & okx).long() << t
+    rows = bits.reshape(-1).repeat(B)  # [B*H*W], raster GEMM rows
+    if perm is not None:
+        pc = perm.cpu().long()
+        rows = torch.where(pc >= 0, rows[pc.clamp(min=0)], torch.zeros_like(pc))
+    pad = (-rows.numel()) % BM
+    rows = torch.cat([rows, torch.zeros(pad, dtype=torch.long)]).reshape(-1, BM)
+    tile = torch.zeros(rows.shape[0], dtype=torch.long)
+    for j in range(BM):  # bitwise OR-reduce over the tile's rows
+        tile |= rows[:, j]
+    return sum(((tile >> t) & 1) for t in range(k * k))
+
+
+def grouped_tile_order(convs: List[dict], variant: int, device=None) -> torch.Tensor:
+    """Block -> tile table of ``conv_gemm_grouped``: every tile of every conv as
+    (group << 24) | tile, heaviest first (work = live taps x 64-channel K chunks;
+    longest-processing-time order, so the short 1x1 / edge tiles fill the tail)."""
+    BM, BN = GROUP_TILE[variant]
+    ent, cost = [], []
+    for g, c in enumerate(convs):
+        tn = -(-c["Cout"] // BN)
+        taps = _tile_taps(c["B"], c["OH"], c["OW"], c["k"], c["dil"], BM, c.get("perm"))
+        kch = -(-c["Cin"] // 64)
+        for tm in range(taps.numel()):
+            for n in range(tn):
+                ent.append((g << 24) | (tm * tn + n))
+                cost.append(int(taps[tm]) * kch)
+    idx = sorted(range(len(ent)), key=lambda i: (-cost[i], i))
+    return torch.tensor([ent[i] for i in idx], dtype=torch.int32).to(device).contiguous()
+
+
+def conv_gemm_grouped(convs: List[dict], order: torch.Tensor, variant: int = 5) -> None:
+    """Up to 4 independent stride-1 'same' NHWC convs with one Cout (the ASPP branches)
+    in ONE LDS-DMA grid, tiles in the ``grouped_tile_order`` table. Each conv is a
+    dict of conv_gemm's arguments: x, w, bias, out, B, IH, IW, Cin, OH, OW, Cout, k,
+    dil, ldo, co_off, act, and optionally perm (tap_group_perm with the variant's BM)."""
+    if not 1 <= len(convs) <= 4:
+        raise ValueError("conv_gemm_grouped: 1..4 convs")
+    if variant not in GROUP_TILE:
+        raise ValueError(f"conv_gemm_grouped: variant must be one of {sorted(GROUP_TILE)}")
+    BM, BN = GROUP_TILE[variant]
+    tiles = []
+    groups = []
+    for c in convs:
+        B, IH, IW, Cin, OH, OW, Cout, k = (c[n] for n in ("B", "IH", "IW", "Cin", "OH", "OW", "Cout", "k"))
+        dil, ldo, co_off = c.get("dil", 1), c.get("ldo", Cout), c.get("co_off", 0)
+        if Cin % 8 or k * k > 16 or Cout != convs[0]["Cout"] or (OH, OW) != (IH, IW):
+            raise ValueError("conv_gemm_grouped: stride-1 'same' convs, Cin % 8 == 0, <= 16 taps, one Cout")
+        if co_off + Cout > ldo:
+            raise ValueError("conv_gemm_grouped: co_off + Cout > ldo")
+        _chk(c["x"], torch.bfloat16, "x", B * IH * IW * Cin)
+        _chk(c["w"], torch.bfloat16, "w", Cout * k * k * Cin)
+        _chk(c["bias"], torch.float32, "bias", Cout)
+        _chk(c["out"], torch.bfloat16, "out", B * OH * OW * ldo)
+        perm = c.get("perm")
+        Mp = 0
+        if perm is not None:
+            _chk(perm, torch.int32, "perm")
+            Mp = perm.numel()
+            if Mp % BM:
+                raise ValueError("conv_gemm_grouped: perm rows must be a multiple of the tile height")
+            if not getattr(perm, "_ssa_checked", False):
+                pc = perm.cpu()
+                if pc.min().item() < -1 or pc.max().item() >= B * OH * OW:
+                    raise ValueError("conv_gemm_grouped: perm entry out of range")
+                perm._ssa_checked = True
+        M = Mp or B * OH * OW
+        tiles.append(-(-M // BM) * -(-Cout // BN))
+        groups.append((_ptr(c["x"]), _ptr(c["w"]), _ptr(c["bias"]), 0, 0, _ptr(c["out"]), B, IH, IW,
+                       Cin, OH, OW, Cout, k, k, 1, dil, ldo, co_off, Cout, ACT[c.get("act")],
+                       _ptr(perm), Mp))
+    _chk(order, torch.int32, "order")
+    if not getattr(order, "_ssa_checked", False):  # every block maps to a real tile
+        oc = order.cpu().long()
+        g, t = oc >> 24, oc & 0xFFFFFF
+        lim = torch.tensor(tiles)[g.clamp(0, len(tiles) - 1)]
+        if (g < 0).any() or (g >= len(convs)).any() or (t >= lim).any():
+            raise ValueError("conv_gemm_grouped: order entry out of range")
+        order._ssa_checked = True
+    _hip_mod().conv_gemm_grouped(groups, _ptr(order), order.numel(), variant, _stream())
+    _dbg('conv_gemm_grouped')
 
 
 def pw_supported(K: int, N: int) -> bool:

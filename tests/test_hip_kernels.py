@@ -107,6 +107,36 @@ def test_conv_gemm_tap_grouped(B, H, W, rate, variant, bm):
     assert torch.all(out[..., :co_off] == 7.0) and torch.all(out[..., co_off + Cout:] == 7.0)
 
 
+@pytest.mark.parametrize("B,H,W,Cin,Cout,variant", [
+    (3, 33, 33, 320, 256, 5), (2, 33, 33, 320, 256, 6), (2, 17, 19, 64, 200, 8),
+    (2, 21, 20, 96, 136, 11)])
+def test_conv_gemm_grouped_aspp(B, H, W, Cin, Cout, variant):
+    """ASPP branches (1x1 + atrous 6/12/18, tap-grouped rows) in one LPT-ordered grid:
+    each branch's channel slice matches F.conv2d, the other channels stay untouched."""
+    K = _hip()
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(B, Cin, H, W, generator=g).to(torch.bfloat16)
+    xd = _nhwc(x).to(DEV)
+    ldo = 4 * Cout + 16
+    out = torch.full((B, H, W, ldo), 7.0, dtype=torch.bfloat16, device=DEV)
+    BM = K.GROUP_TILE[variant][0]
+    convs, refs = [], []
+    for j, (k, rate) in enumerate(((1, 1), (3, 6), (3, 12), (3, 18))):
+        w = (torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5).to(torch.bfloat16)
+        b = torch.randn(Cout, generator=g)
+        refs.append(F.relu(F.conv2d(x.float(), w.float(), b, 1, rate * (k // 2), rate)))
+        convs.append(dict(x=xd, w=w.permute(0, 2, 3, 1).contiguous().to(DEV), bias=b.to(DEV), out=out,
+                          B=B, IH=H, IW=W, Cin=Cin, OH=H, OW=W, Cout=Cout, k=k, dil=rate, ldo=ldo,
+                          co_off=j * Cout, act="relu",
+                          perm=K.tap_group_perm(B, H, W, 3, rate, BM, DEV) if k == 3 else None))
+    order = K.grouped_tile_order(convs, variant, DEV)
+    K.conv_gemm_grouped(convs, order, variant)
+    torch.cuda.synchronize()
+    for j, ref in enumerate(refs):
+        assert _rel(_nchw(out[..., j * Cout:(j + 1) * Cout]).cpu(), ref) < 1e-2, j
+    assert torch.all(out[..., 4 * Cout:] == 7.0)
+
+
 @pytest.mark.parametrize("B,H,W,Cin,Cout,rate,grouped", [
     (3, 33, 33, 320, 256, 6, True), (2, 33, 33, 320, 256, 12, False), (2, 33, 33, 320, 256, 18, True),
     (2, 17, 21, 160, 96, 24, True), (1, 9, 11, 64, 200, 1, False), (2, 20, 20, 256, 136, 2, True)])

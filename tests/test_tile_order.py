@@ -1,0 +1,15 @@
+"""CPU checks of the host-side tile tables of the grouped ASPP GEMM."""
+
+
+def test_grouped_tile_order_cpu():
+    """Every tile of every conv appears once, heaviest (most live taps) first."""
+    from semantic_segmentation_server_amd.ops import hip_ops as K
+    convs = [dict(B=2, OH=33, OW=33, k=1, dil=1, Cin=320, Cout=256)] + [
+        dict(B=2, OH=33, OW=33, k=3, dil=r, Cin=320, Cout=256, perm=K.tap_group_perm(2, 33, 33, 3, r, 128))
+        for r in (6, 12, 18)]
+    o = K.grouped_tile_order(convs, 5).tolist()
+    assert len(o) == len(set(o))
+    for gi, c in enumerate(convs):
+        M = c["perm"].numel() if "perm" in c else 2 * 33 * 33
+        assert sorted(v & 0xFFFFFF for v in o if v >> 24 == gi) == list(range(-(-M // 128)))
+    assert o[0] >> 24 == 1 and o[-1] >> 24 in (0, 3)  # a full 9-tap rate-6 tile leads
