@@ -82,7 +82,11 @@ def main() -> int:
     else:
         engine = Engine(cfg, ctx.device)
     hub = ResultHub(ctx.world * a.streams, maxlen=4096) if ctx.is_root else None
-    pipe = DataParallelPipeline(ctx, engine, cam_w, cam_h, a.batch, a.ingest, hub, a.streams)
+    # lag=1: step k collects step k-1's records, so the next graph launch and the host
+    # unpack overlap the GPU instead of idling it; run_steps flushes the last step
+    # inside the timed region (every timed step's records reach the hub)
+    pipe = DataParallelPipeline(ctx, engine, cam_w, cam_h, a.batch, a.ingest, hub, a.streams,
+                                lag=1)
 
     # synthetic camera frames, pinned; distinct per rank
     src = SyntheticSource(cam_w, cam_h, stream=ctx.rank, seed=1, pool=max(2, min(a.batch, 8)))
@@ -95,13 +99,22 @@ def main() -> int:
 
     verbose = os.environ.get("SSA_BENCH_VERBOSE", "0") == "1"
 
-    def run_steps(n: int, k0: int = 0) -> None:
-        # double-buffered ingest: the next batch's H2D overlaps this step's compute
-        pipe.prefetch(host_batches[k0 % 2])
+    staged = [False]  # the first batch of a run is already on its way (steady state)
+
+    def run_steps(n: int, k0: int = 0, stage_next: bool = True) -> None:
+        # double-buffered ingest: the next batch's H2D overlaps this step's compute;
+        # the last step of a run stages the first batch of the next run
+        if n <= 0:
+            return
+        if not staged[0]:
+            pipe.prefetch(host_batches[k0 % 2])
         for k in range(n):
-            pipe.step(next_frames=host_batches[(k0 + k + 1) % 2] if k + 1 < n else None)
+            last = k + 1 == n
+            pipe.step(next_frames=host_batches[(k0 + k + 1) % 2] if (not last or stage_next) else None)
             if verbose:
                 print(f"[rank {ctx.rank}] step {k0 + k} ok", file=sys.stderr, flush=True)
+        pipe.flush()
+        staged[0] = stage_next
 
     sync = (lambda: torch.cuda.synchronize(ctx.device)) if ctx.device.type == "cuda" else (lambda: None)
     t_w0 = time.perf_counter()

@@ -57,8 +57,14 @@ def unpack_records(packed: np.ndarray, K: int, frame_ids, ts, streams) -> np.nda
 class DataParallelPipeline:
     def __init__(self, ctx: DistContext, engine, cam_w: int, cam_h: int, batch: int,
                  ingest: str = "local", hub: Optional[ResultHub] = None,
-                 streams_per_rank: int = 1):
+                 streams_per_rank: int = 1, lag: int = 0):
+        """``lag=1``: step k returns (and pushes) the records of step k-1, so the host
+        never waits for the step it just enqueued -- the next graph launch and the
+        host-side unpack overlap the GPU's compute instead of idling it between
+        steps; ``flush()`` collects the last step. ``lag=0``: step k returns its own
+        records (synchronous)."""
         self.ctx = ctx
+        self.lag = 1 if lag else 0
         self.engine = engine
         self.B = int(batch)
         self.ingest = ingest
@@ -85,12 +91,24 @@ class DataParallelPipeline:
                                           device=cdev)
             self.meta_buf = torch.empty((ctx.world, self.B, 3), dtype=torch.float64, device=cdev)
         self.meta = torch.zeros((self.B, 3), dtype=torch.float64, device=cdev)
-        self.meta_host = torch.zeros((self.B, 3), dtype=torch.float64, pin_memory=self.cuda)
-        self.host_rec = torch.empty((ctx.world, self.B, self.rec_width), dtype=torch.float32,
-                                    pin_memory=self.cuda)
+        # host-side buffers are double-buffered: with lag=1 step k+1 refills them
+        # while step k's async copies may still be queued behind its compute
+        self.meta_host = [torch.zeros((self.B, 3), dtype=torch.float64, pin_memory=self.cuda)
+                          for _ in range(2)]
+        self.host_rec = [torch.empty((ctx.world, self.B, self.rec_width), dtype=torch.float32,
+                                     pin_memory=self.cuda) for _ in range(2)]
+        if ctx.is_root and ctx.initialized:
+            self.host_meta = [torch.empty((ctx.world, self.B, 3), dtype=torch.float64,
+                                          pin_memory=self.cuda) for _ in range(2)]
+        self._rslot = 0
+        self._pending = None  # (slot, event, fids, streams, ts) of the step not yet collected
         self.frames_done = 0
         self.records_out = 0
         self._prev_done = None  # compute-done event of the previous step
+        if self.cuda and hasattr(engine, "bind_inputs"):
+            # one hipGraph per staging slot reads the slot in place (no per-step D2D
+            # copy of the B x Hc x Wc x 3 frames into a single static input)
+            engine.bind_inputs(self.staging)
 
     # ---------------------------------------------------------------- ingest
     def prefetch(self, host_frames: torch.Tensor) -> None:
@@ -151,11 +169,14 @@ class DataParallelPipeline:
         if packed is None:  # host post-processing path (torch backend / exact mode)
             self.frames_done += B * self.ctx.world
             return self.engine.records_from_labels(labels, fids, tss, strm)
+        slot = self._rslot
+        self._rslot ^= 1
         if self.ctx.initialized:
-            self.meta_host[:, 0] = torch.tensor(fids, dtype=torch.float64)
-            self.meta_host[:, 1] = torch.tensor(strm, dtype=torch.float64)
-            self.meta_host[:, 2] = torch.tensor(tss, dtype=torch.float64)
-            self.meta.copy_(self.meta_host, non_blocking=True)
+            mh = self.meta_host[slot]
+            mh[:, 0] = torch.tensor(fids, dtype=torch.float64)
+            mh[:, 1] = torch.tensor(strm, dtype=torch.float64)
+            mh[:, 2] = torch.tensor(tss, dtype=torch.float64)
+            self.meta.copy_(mh, non_blocking=True)
             send = packed if self.ctx.backend == "nccl" else packed.cpu()
             dst = list(self.gather_buf.unbind(0)) if self.ctx.is_root else None
             dist.gather(send, dst, dst=0)
@@ -167,15 +188,34 @@ class DataParallelPipeline:
         self.frames_done += B * self.ctx.world
         if not self.ctx.is_root:
             return np.zeros(0, RECORD_DTYPE)
-        self.host_rec.copy_(src, non_blocking=True)
+        self.host_rec[slot].copy_(src, non_blocking=True)
         if self.ctx.initialized:
-            meta = self.meta_buf.cpu().numpy().reshape(-1, 3)
+            self.host_meta[slot].copy_(self.meta_buf, non_blocking=True)
+        ev = None
+        if self.cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.dev))
+        cur = (slot, ev, fids, strm, tss)
+        if not self.lag:
+            return self._collect(cur)
+        prev, self._pending = self._pending, cur
+        return self._collect(prev) if prev is not None else np.zeros(0, RECORD_DTYPE)
+
+    def flush(self) -> np.ndarray:
+        """Collect the records of the last step (lag=1); no-op otherwise."""
+        prev, self._pending = self._pending, None
+        return self._collect(prev) if prev is not None else np.zeros(0, RECORD_DTYPE)
+
+    def _collect(self, pending) -> np.ndarray:
+        slot, ev, fids, strm, tss = pending
+        if ev is not None:
+            ev.synchronize()
+        if self.ctx.initialized:
+            meta = self.host_meta[slot].numpy().reshape(-1, 3)
         else:
             meta = np.stack([np.asarray(fids, np.float64), np.asarray(strm, np.float64),
                              np.asarray(tss, np.float64)], 1)
-        if self.cuda:
-            torch.cuda.current_stream(self.dev).synchronize()
-        flat = self.host_rec.numpy().reshape(-1, self.rec_width)
+        flat = self.host_rec[slot].numpy().reshape(-1, self.rec_width)
         recs = unpack_records(flat, self.K, meta[:, 0].astype(np.int64), meta[:, 2],
                               meta[:, 1].astype(np.int64))
         self.records_out += len(recs)

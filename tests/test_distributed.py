@@ -45,7 +45,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, ingest, q):
+def _worker(rank, world, port, ingest, q, lag=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     from semantic_segmentation_server_amd.parallel import dist as D
@@ -54,7 +54,7 @@ def _worker(rank, world, port, ingest, q):
     ctx = D.init("gloo")
     B = 2
     hub = ResultHub(world) if ctx.is_root else None
-    pipe = DataParallelPipeline(ctx, FakeEngine(), 8, 6, B, ingest, hub)
+    pipe = DataParallelPipeline(ctx, FakeEngine(), 8, 6, B, ingest, hub, lag=lag)
     if ingest == "scatter":
         nb = B * world if ctx.is_root else B
         frames = torch.zeros(nb, 6, 8, 3, dtype=torch.uint8)
@@ -67,6 +67,13 @@ def _worker(rank, world, port, ingest, q):
             frames[i, 0, 0, 0] = 10 + rank * B + i
     pipe.prefetch(frames)
     recs = pipe.step()
+    if lag:  # records arrive one step late; the second step's come with flush()
+        assert len(recs) == 0
+        pipe.prefetch(frames)
+        recs = pipe.step()
+        last = pipe.flush()
+        if ctx.is_root:
+            assert np.array_equal(last["cx"], recs["cx"]) and np.all(last["frame"] == recs["frame"] + B)
     t = D.allreduce_max(ctx, float(rank))
     if ctx.is_root:
         q.put((recs["cx"].tolist(), recs["stream"].tolist(), t, hub.depth))
@@ -74,12 +81,13 @@ def _worker(rank, world, port, ingest, q):
     D.destroy(ctx)
 
 
-@pytest.mark.parametrize("world,ingest", [(2, "local"), (2, "scatter"), (3, "scatter")])
-def test_dp_gather_and_scatter(world, ingest):
+@pytest.mark.parametrize("world,ingest,lag", [(2, "local", 0), (2, "scatter", 0), (3, "scatter", 0),
+                                              (2, "local", 1), (2, "scatter", 1)])
+def test_dp_gather_and_scatter(world, ingest, lag):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, ingest, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, ingest, q, lag)) for r in range(world)]
     for p in procs:
         p.start()
     cx, streams, tmax, depth = q.get(timeout=120)
@@ -91,7 +99,7 @@ def test_dp_gather_and_scatter(world, ingest):
     assert np.allclose(cx, exp, atol=1e-6)          # frame i went to rank i // B, came back in order
     assert streams == [i // B for i in range(world * B)]
     assert tmax == world - 1
-    assert depth == world * B
+    assert depth == world * B * (2 if lag else 1)
 
 
 def test_unpack_records_order():

@@ -437,6 +437,30 @@ def test_engine_graph_replay_matches_eager():
     assert p2 is not None and p2.shape == (2, 1 + 5 * cfg.max_segments)
 
 
+def test_engine_bound_input_graphs():
+    """bind_inputs: a graph per persistent input buffer reads it in place; results
+    equal the eager step, alternating between the buffers after they are refilled."""
+    from semantic_segmentation_server_amd.runtime.engine import Engine
+    from semantic_segmentation_server_amd.runtime.sources import SyntheticSource
+    cfg = _small_cfg(graph=True)
+    eng = Engine(cfg, torch.device(DEV))
+    eng.set_camera(200, 150)
+    src = SyntheticSource(200, 150, pool=4, seed=3)
+    bufs = [torch.empty((2, 150, 200, 3), dtype=torch.uint8, device=DEV) for _ in range(2)]
+    eng.bind_inputs(bufs)
+    for it in range(3):
+        for b in bufs:
+            f, _, _ = src.read_batch(2)
+            b.copy_(torch.from_numpy(f))
+            want = eng._infer_eager(b).clone()
+            want_post = eng._device_post(want).clone()
+            got, post = eng.run_device(b)
+            torch.cuda.synchronize()
+            assert torch.equal(got, want), it
+            assert torch.equal(post, want_post), it
+    assert len(eng._bound_graphs) == 2
+
+
 def test_engine_step_records_flow():
     from semantic_segmentation_server_amd.runtime.engine import Engine
     from semantic_segmentation_server_amd.runtime.sources import SyntheticSource
