@@ -192,8 +192,13 @@ void dispatch_dwp(const DPPArgs& a, int ns, hipStream_t s) {
 // reads its 9 taps from LDS.
 __device__ __attribute__((aligned(16))) int4 g_dwp_zero[8];
 
-template <int NS>
-__global__ __launch_bounds__(1024) void dw_proj_rows_kernel(DPPArgs a, int TY, int HPP) {
+// ST-stage LDS ring (ST - 1 chunks in flight across each barrier, counted vmcnt):
+// per chunk a workgroup only has ~NS MFMAs per wave of work against a full L2/MALL
+// round trip for the next chunk's halo, so one chunk of lookahead leaves the
+// waves waiting on the DMA. XCD: row tiles of one image go to one XCD (their halo
+// rows overlap, so the re-reads hit that XCD's L2).
+template <int NS, int ST>
+__global__ __launch_bounds__(1024) void dw_proj_rows_kernel(DPPArgs a, int TY, int HPP, int xcd) {
   // HPP: halo pixels rounded up to 16 (one 1 KiB DMA piece per 16 pixels)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int WB = (NS + 1) * 1024;            // weight image per chunk
@@ -204,7 +209,8 @@ __global__ __launch_bounds__(1024) void dw_proj_rows_kernel(DPPArgs a, int TY, i
   const int r16 = lane & 15, kq = lane >> 4;
   const int dl = a.dil, HWW = a.OW + 2 * dl;  // halo row width
   const int rows_per_img = cdiv_dev(a.OH, TY);
-  const int b = blockIdx.x / rows_per_img, oy0 = (blockIdx.x - b * rows_per_img) * TY;
+  const int bid = xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int b = bid / rows_per_img, oy0 = (bid - b * rows_per_img) * TY;
   // this lane's output pixel
   const int p = wid * 16 + r16;
   const int py = p / a.OW, px = p - py * a.OW;
@@ -246,13 +252,39 @@ __global__ __launch_bounds__(1024) void dw_proj_rows_kernel(DPPArgs a, int TY, i
   for (int n = 0; n < NS; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int trow = dl * HWW * 64, tcol = dl * 64;  // tap strides (bytes)
 
-  issue(0, 0);
+  // DMA instructions this wave issues per chunk (wave-uniform, fixed over chunks)
+  int kw = 0;
+#pragma unroll
+  for (int k = 0; k < MAXP; ++k) kw += (wid + k * NW < npieces) ? 1 : 0;
+  for (int q = wid; q < NS + 1; q += NW) ++kw;
+#pragma unroll
+  for (int s = 0; s < ST - 1; ++s)
+    if (s < nchunks) issue(s, s);
   for (int c = 0; c < nchunks; ++c) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (ST == 2 || c + ST - 2 >= nchunks) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {  // leave the newer chunks' DMAs (ST - 2 chunks x kw) in flight
+      switch (kw * (ST - 2)) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+        case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+        case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+        case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+      }
+    }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (c + 1 < nchunks) issue(c + 1, (c + 1) & 1);
-    const char* Hb = smem + (c & 1) * BUF;
+    if (c + ST - 1 < nchunks) issue(c + ST - 1, (c + ST - 1) % ST);
+    const char* Hb = smem + (c % ST) * BUF;
     const char* W = Hb + HPP * 64;
     const f16* wd = reinterpret_cast<const f16*>(W + NS * 1024);
     f16x8 d = *reinterpret_cast<const f16x8*>(wd + 9 * 32 + kq * 8);
@@ -302,24 +334,33 @@ __global__ __launch_bounds__(1024) void dw_proj_rows_kernel(DPPArgs a, int TY, i
   }
 }
 
-template <int NS>
-void launch_dwp_rows(const DPPArgs& a, int TY, hipStream_t s) {
+template <int NS, int ST>
+void launch_dwp_rows_st(const DPPArgs& a, int TY, int xcd, hipStream_t s) {
   const int HP = (TY + 2 * a.dil) * (a.OW + 2 * a.dil);
   const int HPP = (HP + 15) / 16 * 16;
   const int nw = (TY * a.OW + 15) / 16;
-  const size_t lds = 2 * ((size_t)HPP * 64 + (NS + 1) * 1024);
+  const size_t lds = ST * ((size_t)HPP * 64 + (NS + 1) * 1024);
   if (nw > 16 || lds > 160 * 1024 || HPP / 16 > 4 * nw)
     throw std::invalid_argument("dw_proj_fused rows: tile too large");
   static bool attr = false;
   if (!attr) {
-    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&dw_proj_rows_kernel<NS>),
+    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&dw_proj_rows_kernel<NS, ST>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
           "dw_proj_rows attr");
     attr = true;
   }
   const int grid = a.B * cdiv(a.OH, TY);
-  hipLaunchKernelGGL((dw_proj_rows_kernel<NS>), dim3(grid), dim3(64 * nw), lds, s, a, TY, HPP);
+  hipLaunchKernelGGL((dw_proj_rows_kernel<NS, ST>), dim3(grid), dim3(64 * nw), lds, s, a, TY, HPP, xcd);
   check_launch("dw_proj_rows");
+}
+
+template <int NS>
+void launch_dwp_rows(const DPPArgs& a, int rows, hipStream_t s) {
+  // rows = TY | stages << 8 | xcd << 12
+  const int TY = rows & 0xff, st = (rows >> 8) & 0xf, xcd = (rows >> 12) & 1;
+  if (st == 3) launch_dwp_rows_st<NS, 3>(a, TY, xcd, s);
+  else if (st == 4) launch_dwp_rows_st<NS, 4>(a, TY, xcd, s);
+  else launch_dwp_rows_st<NS, 2>(a, TY, xcd, s);
 }
 
 }  // namespace

@@ -142,6 +142,14 @@ def pw_choice(name: str, gemm_op: Callable, x: torch.Tensor, w: torch.Tensor, b:
     return Choice(name, variants)
 
 
+def _dwp_rows_fit(ty: int, stages: int, dil: int, OW: int, cout: int) -> bool:
+    """dw_proj_rows tile (ty rows x OW, <= 16 waves) and its LDS ring fit the CU."""
+    if -(-ty * OW // 16) > 16:
+        return False
+    halo = (ty + 2 * dil) * (OW + 2 * dil)
+    return stages * ((-(-halo // 16) * 16) * 64 + (cout // 16 + 1) * 1024) <= 160 * 1024
+
+
 class HipDeepLab:
     def __init__(self, model: DeepLabV3, device: torch.device, cfg=None):
         if device.type != "cuda":
@@ -436,16 +444,23 @@ class HipDeepLab:
             ewpk = K.pack_pw_weights(ew, eb)
             wpk_dp = K.pack_dw_proj(pw_[:, 0, 0, :], dw_w, dw_b)
             M = B * h * w
-            dwp_cfgs = [("w", 4, 0)] + ([("r", 4, ty) for ty in (2, 3, 4)] if s.stride == 1 else [])
+            dwp_cfgs = [("w", 4, 0, 2, False)]
+            if s.stride == 1:
+                dwp_cfgs += [("r", 4, ty, 2, False) for ty in (2, 3, 4)]
+                dwp_cfgs += [("r", 4, ty, st, True) for ty in (2, 3, 4, 6) for st in (2, 3, 4)
+                             if _dwp_rows_fit(ty, st, s.dilation, OW, s.cout)]
             for mt, nch in ((2, 3),):
-                for kind, nw, ty in dwp_cfgs:
-                    variants.append((f"dwp{kind}{nw if not ty else ty}.pw{mt}x{nch}", [
+                for kind, nw, ty, st, xcd in dwp_cfgs:
+                    tag = f"dwp{kind}{nw if not ty else ty}" + (f"s{st}x" if xcd else "")
+                    variants.append((f"{tag}.pw{mt}x{nch}", [
                         lambda *_, x=inp, e16=e16, M=M, c=c, mt=mt, nch=nch: K.pw_conv(
                             x, ewpk, e16, M=M, K=c, N=hid, act="relu6", mt=mt, nch=nch),
-                        lambda *_, e16=e16, out=out, h=h, w=w, OH=OH, OW=OW, res=res, nw=nw, ty=ty:
+                        lambda *_, e16=e16, out=out, h=h, w=w, OH=OH, OW=OW, res=res, nw=nw, ty=ty,
+                        st=st, xcd=xcd:
                         K.dw_proj_fused(e16, wpk_dp, pb_, out, B=B, IH=h, IW=w, hid=hid,
                                         Cout=s.cout, OH=OH, OW=OW, stride=s.stride,
-                                        dil=s.dilation, res=res, waves=nw, rows=ty)]))
+                                        dil=s.dilation, res=res, waves=nw, rows=ty, stages=st,
+                                        xcd=xcd)]))
         if "dwproj" in blk:
             dpw, dpb = blk["dwproj"]
             e = unfused_expand_out

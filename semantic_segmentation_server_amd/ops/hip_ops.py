@@ -404,12 +404,20 @@ def pack_dw_proj(wp: torch.Tensor, wd9: torch.Tensor, bd: torch.Tensor) -> torch
 
 
 def dw_proj_fused(h, wpk, bp, out, *, B, IH, IW, hid, Cout, OH, OW, stride=1, dil=1, res=None,
-                  waves=4, rows=0):
+                  waves=4, rows=0, stages=2, xcd=False):
     """Depthwise 3x3 + ReLU6 + 1x1 projection (+ residual), dw_proj.hip. h [B,IH,IW,hid]
     fp16 (pw_conv out_f16); wpk from ``pack_dw_proj``; bp [Cout] fp32; out bf16.
-    ``rows > 0``: row-tile variant (``rows`` output rows per workgroup, halo in LDS)."""
+    ``rows > 0``: row-tile variant (``rows`` output rows per workgroup, halo in LDS,
+    a ``stages``-deep LDS ring, ``xcd``: an image's row tiles on one XCD)."""
     if hid % 32 or Cout not in DWP_COUT or waves not in (4, 8):
         raise ValueError(f"dw_proj_fused: unsupported hid={hid} Cout={Cout}")
+    if rows and not (1 <= rows <= 255 and stages in (2, 3, 4)):
+        raise ValueError("dw_proj_fused: rows 1..255, stages 2..4")
+    if rows:
+        halo = (rows + 2 * dil) * (OW + 2 * dil)
+        lds = stages * ((-(-halo // 16) * 16) * 64 + (Cout // 16 + 1) * 1024)
+        if lds > 160 * 1024:
+            raise ValueError("dw_proj_fused: row tile too large for LDS at this depth")
     if rows and (stride != 1 or -(-rows * OW // 16) > 16):
         raise ValueError("dw_proj_fused: row tiles need stride 1 and <= 256 pixels")
     if (OH, OW) != ((IH - 1) // stride + 1, (IW - 1) // stride + 1):
@@ -421,7 +429,8 @@ def dw_proj_fused(h, wpk, bp, out, *, B, IH, IW, hid, Cout, OH, OW, stride=1, di
     if res is not None:
         _chk(res, torch.bfloat16, "res", B * OH * OW * Cout)
     _hip_mod().dw_proj_fused(_ptr(h), _ptr(wpk), _ptr(bp), _ptr(res), _ptr(out), B, IH, IW, hid,
-                             Cout, OH, OW, stride, dil, waves, _stream(), rows)
+                             Cout, OH, OW, stride, dil, waves, _stream(),
+                             (rows | (stages << 8) | (int(bool(xcd)) << 12)) if rows else 0)
     _dbg('dw_proj_fused')
     return out
 

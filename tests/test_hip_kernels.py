@@ -633,8 +633,10 @@ def test_dw_project(hid, cout, stride, dil, res):
 @pytest.mark.parametrize("hid,cout,stride,dil,res", [(576, 96, 1, 1, True), (576, 160, 1, 1, False),
                                                      (960, 160, 1, 2, True), (960, 320, 1, 2, False),
                                                      (384, 64, 2, 1, False), (384, 64, 1, 1, True)])
-@pytest.mark.parametrize("waves,rows", [(4, 0), (8, 0), (4, 2), (4, 3)])
-def test_dw_proj_fused(hid, cout, stride, dil, res, waves, rows):
+@pytest.mark.parametrize("waves,rows,stages,xcd", [(4, 0, 2, False), (8, 0, 2, False), (4, 2, 2, False),
+                                                   (4, 3, 2, False), (4, 3, 3, True), (4, 2, 4, True),
+                                                   (4, 6, 3, True)])
+def test_dw_proj_fused(hid, cout, stride, dil, res, waves, rows, stages, xcd):
     """Weight-streamed depthwise + projection (dw_proj.hip) vs the torch composition."""
     K = _hip()
     if rows and stride != 1:
@@ -656,7 +658,7 @@ def test_dw_proj_fused(hid, cout, stride, dil, res, waves, rows):
     out = torch.full((B, OH, OW, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
     K.dw_proj_fused(_nhwc(x).to(DEV).half(), wpk, bp.to(DEV), out, B=B, IH=H, IW=H, hid=hid, Cout=cout,
                     OH=OH, OW=OW, stride=stride, dil=dil, res=None if r is None else _nhwc(r).to(DEV),
-                    waves=waves, rows=rows)
+                    waves=waves, rows=rows, stages=stages, xcd=xcd)
     torch.cuda.synchronize()
     assert torch.isfinite(out).all()
     assert _rel(_nchw(out).cpu(), ref) < 2e-2  # fp16 depthwise: rounding differs from bf16
