@@ -454,7 +454,7 @@ __global__ __launch_bounds__(64 * NW) void fused_ir_tile_kernel(IRTArgs a) {
 // depthwise and fp16-MFMA projection.
 struct SB0Args {
   const uint8_t* frames; const int32_t* lut_x; const int32_t* lut_y;
-  const bf16* ws;  // stem weights [32 out][32 K] bf16, K = (ky*3 + kx)*3 + c (RGB), zero-padded
+  const bf16* ws;  // stem weights [32 out][48 K] bf16, K = tap*4 + c (RGB + zero), taps 9..11 zero
   const float* bs; // stem bias [32]
   const f16* wd; const f16* bd;  // depthwise [9][32], [32] fp16
   const f16* wp;   // projection [16][32] fp16
@@ -462,6 +462,13 @@ struct SB0Args {
   bf16* out;       // [B, SH, SW, Cout]
   int B, Hc, Wc, H, W, SH, SW, Cout, TY, TX, tiles_y, tiles_x;
 };
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+// i / d for the small non-negative tile indices here (i < 2^14, d < 128): one
+// float multiply instead of a ~20-instruction integer division (the kernel is
+// VALU-bound; these divisions were a large share of its instructions)
+__device__ __forceinline__ int sdiv(int i, float inv_d) { return (int)(((float)i + 0.5f) * inv_d); }
 
 template <int GPW>
 __global__ __launch_bounds__(256) void stem_block0_kernel(SB0Args a) {
@@ -480,10 +487,12 @@ __global__ __launch_bounds__(256) void stem_block0_kernel(SB0Args a) {
   const int iy0 = 2 * sy0 - 1, ix0 = 2 * sx0 - 1;   // input region origin
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int r16 = lane & 15, kq = lane >> 4;
+  const float inv_iwt = 1.f / IWT, inv_swt = 1.f / SWT, inv_tx = 1.f / a.TX;
 
   const uint8_t* fb = a.frames + (size_t)b * a.Hc * a.Wc * 3;
   for (int i = tid; i < IHT * IWT; i += 256) {
-    const int y = iy0 + i / IWT, x = ix0 + i % IWT;
+    const int ry = sdiv(i, inv_iwt);
+    const int y = iy0 + ry, x = ix0 + (i - ry * IWT);
     float rgb[3] = {0.f, 0.f, 0.f};  // conv zero padding outside the model input
     if (y >= 0 && y < a.H && x >= 0 && x < a.W) {
       const int sy = a.lut_y[y], sx = a.lut_x[x];
@@ -499,36 +508,43 @@ __global__ __launch_bounds__(256) void stem_block0_kernel(SB0Args a) {
     bf16x4 v = {(bf16)rgb[0], (bf16)rgb[1], (bf16)rgb[2], (bf16)0.f};
     *reinterpret_cast<bf16x4*>(IN + (size_t)i * 4) = v;
   }
-  // stem weights (A operand): rows = out channels sub*16 + r16, K = kq*8 .. +7
-  bf16x8 wst[2];
+  // Stem conv on v_mfma_f32_16x16x16_bf16: K = 12 taps x 4 channels (RGB + the zero
+  // 4th channel of IN, taps 9..11 zero) in 3 MFMAs; lane kq of MFMA m holds tap
+  // 4m + kq, i.e. ONE 8-byte LDS read of the pixel's 4 channels (no per-element
+  // gathers). A operand: weight rows sub*16 + r16, K = m*16 + kq*4 .. +3.
+  s16x4 wst[2][3];
   f32x4 bst[2];
 #pragma unroll
   for (int sub = 0; sub < 2; ++sub) {
-    wst[sub] = ld8(a.ws + (size_t)(sub * 16 + r16) * 32 + kq * 8);
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+      wst[sub][m] = *reinterpret_cast<const s16x4*>(a.ws + (size_t)(sub * 16 + r16) * 48 + m * 16 + kq * 4);
     bst[sub] = *reinterpret_cast<const f32x4*>(a.bs + sub * 16 + kq * 4);
   }
-  // per-lane K gather offsets into IN (relative to the stem pixel's window origin)
-  int koff[8];
+  int toff[3];  // element offset of this lane's tap in IN, relative to the window origin
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int k = kq * 8 + e;
-    const int tap = k / 3, c = k % 3;
-    koff[e] = k < 27 ? (((tap / 3) * IWT + (tap % 3)) * 4 + c) : -1;
+  for (int m = 0; m < 3; ++m) {
+    const int tp = m * 4 + kq;
+    toff[m] = tp < 9 ? ((tp / 3) * IWT + tp % 3) * 4 : -1;
   }
   __syncthreads();
   const f16x4 z4 = {0, 0, 0, 0}, s4 = {6, 6, 6, 6};
+  const s16x4 zs = {0, 0, 0, 0};
   for (int gi = wid; gi < s_groups; gi += 4) {
     const int sp = gi * 16 + r16;
-    const int ty = sp / SWT, tx = sp - ty * SWT;
+    const int ty = sdiv(sp, inv_swt), tx = sp - ty * SWT;
     const int sy = sy0 + ty, sx = sx0 + tx;
     const bool inside = sp < s_px && sy >= 0 && sy < a.SH && sx >= 0 && sx < a.SW;
     const int base = sp < s_px ? ((2 * ty) * IWT + 2 * tx) * 4 : 0;
-    bf16x8 xf;
+    s16x4 xf[3];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) xf[e] = koff[e] >= 0 ? IN[base + koff[e]] : (bf16)0.f;
+    for (int m = 0; m < 3; ++m)
+      xf[m] = toff[m] >= 0 ? *reinterpret_cast<const s16x4*>(IN + base + toff[m]) : zs;
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
-      f32x4 e4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wst[sub], xf, bst[sub], 0, 0, 0);
+      f32x4 e4 = bst[sub];
+#pragma unroll
+      for (int m = 0; m < 3; ++m) e4 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wst[sub][m], xf[m], e4, 0, 0, 0);
       f16x4 o = {(f16)e4[0], (f16)e4[1], (f16)e4[2], (f16)e4[3]};
       o = __builtin_elementwise_min(__builtin_elementwise_max(o, z4), s4);
       if (!inside) o = z4;  // depthwise zero padding outside the stem image
@@ -546,7 +562,7 @@ __global__ __launch_bounds__(256) void stem_block0_kernel(SB0Args a) {
 #pragma unroll
   for (int g = 0; g < GPW; ++g) {
     const int p = (wid * GPW + g) * 16 + r16;
-    const int py = p / a.TX, px = p - py * a.TX;
+    const int py = sdiv(p, inv_tx), px = p - py * a.TX;
     const int oy = oy0 + py, ox = ox0 + px;
     const bool valid = p < a.TY * a.TX && oy < a.SH && ox < a.SW;
     const int pofs = valid ? py * SWT + px : 0;
@@ -637,7 +653,8 @@ void fused_ir_tile(const FusedIRParams& p, hipStream_t st) {
 
 void stem_block0(const StemBlock0Params& p, hipStream_t st) {
   if (p.Cout != 16) throw std::invalid_argument("stem_block0: block 0 must project to 16 channels");
-  if (p.TY < 1 || p.TX < 1 || (p.TY * p.TX + 15) / 16 > 8) throw std::invalid_argument("stem_block0: bad tile");
+  if (p.TY < 1 || p.TX < 1 || (p.TY * p.TX + 15) / 16 > 16 || p.TX > 120)
+    throw std::invalid_argument("stem_block0: bad tile");
   if (p.SH != (p.H - 1) / 2 + 1 || p.SW != (p.W - 1) / 2 + 1) throw std::invalid_argument("stem_block0: bad stem size");
   SB0Args a{p.frames, p.lut_x, p.lut_y, p.ws, p.bs, reinterpret_cast<const f16*>(p.wd),
             reinterpret_cast<const f16*>(p.bd), reinterpret_cast<const f16*>(p.wp), p.bp, p.out,
@@ -647,10 +664,21 @@ void stem_block0(const StemBlock0Params& p, hipStream_t st) {
                      (size_t)((SHT * SWT + 15) / 16) * 16 * 40 * 2;
   const int grid = p.B * a.tiles_y * a.tiles_x;
   const int groups = (p.TY * p.TX + 15) / 16;
+  if (lds > 160 * 1024) throw std::invalid_argument("stem_block0: tile too large for LDS");
+  static bool attr = false;
+  if (!attr) {
+    for (const void* k : {reinterpret_cast<const void*>(&stem_block0_kernel<1>),
+                          reinterpret_cast<const void*>(&stem_block0_kernel<2>),
+                          reinterpret_cast<const void*>(&stem_block0_kernel<4>)})
+      check(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024), "stem_block0 attr");
+    attr = true;
+  }
   if (groups <= 4)
     hipLaunchKernelGGL(stem_block0_kernel<1>, dim3(grid), dim3(256), lds, st, a);
-  else
+  else if (groups <= 8)
     hipLaunchKernelGGL(stem_block0_kernel<2>, dim3(grid), dim3(256), lds, st, a);
+  else
+    hipLaunchKernelGGL(stem_block0_kernel<4>, dim3(grid), dim3(256), lds, st, a);
   check_launch("stem_block0");
 }
 

@@ -276,7 +276,7 @@ class HipDeepLab:
                     fused = [(f"stem_block0_{ty}x{tx}", [
                         lambda frames, lx, ly, out0=out0, ty=ty, tx=tx, sbp=sbp: K.stem_block0(
                             frames, lx, ly, sbp, out0, H=H, W=W, tile=(ty, tx))])
-                        for ty, tx in ((8, 16), (4, 16), (8, 8))]
+                        for ty, tx in ((8, 16), (4, 16), (8, 8), (16, 16), (8, 32), (12, 16))]
                     sep = ("separate", [ops[stem_at], ops[stem_at + 1]])
                     ops[stem_at:stem_at + 2] = [Choice("stem+block0", fused + [sep])]
         # ---- ASPP

@@ -498,8 +498,9 @@ def pack_stem_block0(stem, wd, bd, wp, bp, device) -> dict:
     """Weights of the fused stem + block-0 kernel. stem: ConvBNAct (3x3 s2, 3 -> 32);
     wd [32, 3, 3], bd [32], wp [16, 32], bp [16] (BN folded)."""
     w, b = stem.fold()                                   # [32, 3, 3, 3] (RGB in)
-    ws = torch.zeros(32, 32, dtype=torch.float32)
-    ws[:, :27] = w.permute(0, 2, 3, 1).reshape(32, 27)   # K = (ky*3 + kx)*3 + c
+    ws = torch.zeros(32, 12, 4, dtype=torch.float32)     # K = tap*4 + c: 3 x 16x16x16 MFMA
+    ws[:, :9, :3] = w.permute(0, 2, 3, 1).reshape(32, 9, 3)
+    ws = ws.reshape(32, 48)
     f32 = dict(dtype=torch.float32, device=device)
     return dict(
         ws=ws.to(device=device, dtype=torch.bfloat16).contiguous(), bs=b.to(**f32).contiguous(),
@@ -510,8 +511,12 @@ def pack_stem_block0(stem, wd, bd, wp, bp, device) -> dict:
 
 
 def stem_block0(frames, lut_x, lut_y, packed: dict, out, *, H, W, tile=(8, 16)):
-    """Fused stem + MobileNetV2 block 0. frames [B, Hc, Wc, 3] u8 BGR; out [B, SH, SW, 16] bf16."""
+    """Fused stem + MobileNetV2 block 0. frames [B, Hc, Wc, 3] u8 BGR; out [B, SH, SW, 16] bf16.
+    tile = (TY, TX) output pixels per workgroup, TY*TX <= 256."""
     B, Hc, Wc, _ = frames.shape
+    if not (tile[0] >= 1 and 1 <= tile[1] <= 120 and tile[0] * tile[1] <= 256):
+        raise ValueError("stem_block0: tile must hold <= 256 pixels")
+    _chk(packed["ws"], torch.bfloat16, "ws", 32 * 48)
     SH, SW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
     _chk(frames, torch.uint8, "frames", B * Hc * Wc * 3)
     _chk(out, torch.bfloat16, "out", B * SH * SW * packed["Cout"])

@@ -513,7 +513,8 @@ def test_fused_inverted_residual(cin, cout, t, stride, H):
 
 
 @pytest.mark.parametrize("cam,H,tile", [((640, 480), 513, (8, 16)), ((200, 150), 129, (4, 16)),
-                                        ((97, 131), 65, (8, 8))])
+                                        ((97, 131), 65, (8, 8)), ((640, 480), 129, (16, 16)),
+                                        ((200, 150), 129, (8, 32)), ((97, 131), 65, (12, 16))])
 def test_stem_block0_fused(cam, H, tile):
     from semantic_segmentation_server_amd.models.layers import ConvBNAct, init_random
     from semantic_segmentation_server_amd.models.mobilenetv2 import InvertedResidual, IRSpec
