@@ -610,7 +610,8 @@ __global__ __launch_bounds__(256) void k_roots(KArgs a) {
 // component is reduced by shuffles first; a full table falls back to global
 // atomics, so correctness never depends on the table size.
 constexpr int kHash = 128;
-constexpr int kQuadBlocks = 64;  // blocks per frame for the strip-privatised passes
+constexpr int kQuadBlocks = 256;  // blocks per frame for the strip-privatised quad pass
+constexpr int kHistBlocks = 512;  // blocks per frame for the histogram pass
 
 struct QuadTable {
   int key[kHash];
@@ -649,8 +650,10 @@ __device__ __forceinline__ void agg_add(QuadTable& T, FrameWS& f, int node, int 
   const int leader = __ffsll((long long)act) - 1;
   const int lnode = __shfl(node, leader, 64);
   if (__all(!active || node == lnode)) {
+    // one quad's pieces are < 2^13 (6x + 3, x < 1024), so a 64-lane sum fits in
+    // 32 bits: reduce in int32 (half the cross-lane traffic of the 64-bit sums)
     int s00 = active ? d00 : 0;
-    long long s10 = active ? d10 : 0, s01 = active ? d01 : 0;
+    int s10 = active ? (int)d10 : 0, s01 = active ? (int)d01 : 0;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       s00 += __shfl_xor(s00, o, 64);
@@ -958,6 +961,8 @@ size_t post_workspace_bytes(int B, int H, int W, int K, int num_bins) {
 void postprocess(const PostParams& p, hipStream_t s) {
   if (p.K > 256) throw std::invalid_argument("postprocess: K > 256");
   if ((size_t)p.K * p.num_bins > (size_t)kMaxHist) throw std::invalid_argument("postprocess: K * bins too large");
+  if (p.H > 65535 || p.W > 65535)  // k_quads' 32-bit wave sums of 6x + 3 pieces
+    throw std::invalid_argument("postprocess: maps larger than 65535 pixels per side");
   if (p.crop_h > p.H || p.crop_w > p.W || p.crop_h <= 0 || p.crop_w <= 0)
     throw std::invalid_argument("postprocess: bad crop");
   KArgs a;
@@ -1008,11 +1013,17 @@ void postprocess(const PostParams& p, hipStream_t s) {
   const char* qb_env = getenv("SSA_QUAD_BLOCKS");
   const int qblocks = qb_env ? std::max(1, atoi(qb_env)) : kQuadBlocks;
   const dim3 gs(qblocks, p.B);
+  // k_hist only runs on frames with a selected contour (usually a few of the batch):
+  // many more, shorter strips per frame so those frames' dependent per-pixel
+  // L -> slot -> parent chains are spread over the whole chip instead of 64 blocks
+  const char* hb_env = getenv("SSA_HIST_BLOCKS");
+  const int hblocks = hb_env ? std::max(1, atoi(hb_env)) : kHistBlocks;
+  const dim3 gh(hblocks, p.B);
   if (st++ < stages) hipLaunchKernelGGL(k_quads, gs, blk, 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_tree, gp, blk, 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_select, gp, blk, 0, s, a);
   if (st++ < stages)
-    hipLaunchKernelGGL(k_hist, gs, blk, (size_t)std::min(p.K, 256) * p.num_bins * 4, s, a);
+    hipLaunchKernelGGL(k_hist, gh, blk, (size_t)std::min(p.K, 256) * p.num_bins * 4, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_finalize, dim3(p.B), dim3(64), 0, s, a);
   check_launch("postprocess");
 }

@@ -21,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--blocks", default="64,128,256,512")
+    ap.add_argument("--env", default="SSA_QUAD_BLOCKS", help="variable the --blocks values go to")
     a = ap.parse_args()
     dev = torch.device("cuda")
     B, H, W, ch, cw = 32, 513, 513, 385, 513
@@ -33,7 +34,7 @@ def main():
         lab = torch.from_numpy(maps).to(dev)
         line = [name]
         for qb in a.blocks.split(","):
-            os.environ["SSA_QUAD_BLOCKS"] = qb
+            os.environ[a.env] = qb
             for _ in range(3):
                 post.run(lab, cw, ch, 0.05 * H * W)
             st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
