@@ -46,7 +46,7 @@ struct FrameWS {
   long long* t10;      // [N]
   long long* t01;      // [N]
   int32_t* hist;       // [K][bins]
-  int32_t* nslot;      // [1] (+ overflow flag at [1])
+  int32_t* nslot;      // [0] selected, [1] overflow flag, [2] cross-tile edges, [3] selected holes
   int32_t* slot_node;  // [K]
   int32_t* cidx;       // [N] per tile-local root pixel: its index among the tile's roots
   int32_t* rootpix;    // [ntiles][kTileRoots] raster index of each tile-local root
@@ -119,6 +119,7 @@ struct KArgs {
   char* ws;
   Layout lay;
   float* records;
+  int dbg;  // SSA_POST_DBG ablation bits (timing experiments only; 0 in production)
 };
 
 __device__ __forceinline__ int reflect101(int i, int n) {
@@ -780,6 +781,7 @@ __global__ __launch_bounds__(256) void k_select(KArgs a) {
   if (s < a.K) {
     f.slot[p] = s;
     f.slot_node[s] = p + 1;
+    if (!f.mask[p]) atomicAdd(f.nslot + 3, 1);  // a selected hole: k_hist needs its ring
   } else {
     f.nslot[1] = 1;  // overflow: contour dropped
   }
@@ -792,16 +794,20 @@ __global__ __launch_bounds__(256) void k_select(KArgs a) {
 // first) and flushes its non-zero counters once.
 constexpr int kMaxHist = 256 * 32;
 
+// Wave-aggregated histogram add: the wave's lanes are grouped by key (one ballot
+// per distinct key; class maps are blobby, so 64 consecutive pixels carry 1-4
+// distinct (slot, class) keys) and ONE lane per group adds the group's count --
+// instead of up to 64 same-address LDS atomics serialising on a bank.
 __device__ __forceinline__ void hist_add(int* sh, int bins, int slot, int label) {
   const int key = slot >= 0 ? slot * bins + label : -1;
-  const unsigned long long act = __ballot(key >= 0);
-  if (act == 0) return;
-  const int leader = __ffsll((long long)act) - 1;
-  const int lkey = __shfl(key, leader, 64);
-  if (__all(key < 0 || key == lkey)) {
-    if ((int)(threadIdx.x & 63) == leader) atomicAdd(sh + lkey, __popcll(act));
-  } else if (key >= 0) {
-    atomicAdd(sh + key, 1);
+  unsigned long long act = __ballot(key >= 0);
+  const int me = (int)(threadIdx.x & 63);
+  while (act) {  // wave-uniform loop, at most 64 iterations
+    const int leader = __ffsll((long long)act) - 1;
+    const int lkey = __shfl(key, leader, 64);
+    const unsigned long long grp = __ballot(key == lkey) & act;
+    if (me == leader) atomicAdd(sh + lkey, __popcll(grp));
+    act &= ~grp;
   }
 }
 
@@ -813,6 +819,9 @@ __global__ __launch_bounds__(256) void k_hist(KArgs a) {
   const int ns = min(*f.nslot, a.K);
   if (ns == 0) return;  // block-uniform early exit: no contour selected
   const int nh = ns * a.bins;
+  // ring pixels only exist around selected holes; frames without one (the usual
+  // case: selected contours are blobs) skip the 4-neighbour checks entirely
+  const bool sel_holes = f.nslot[3] > 0 && !(a.dbg & 2);
   for (int i = threadIdx.x; i < nh; i += 256) sh[i] = 0;
   __syncthreads();
   const int per = (N + gridDim.x - 1) / gridDim.x;
@@ -831,14 +840,14 @@ __global__ __launch_bounds__(256) void k_hist(KArgs a) {
     }
     // ancestors (inclusive): the fill of every enclosing contour contains p
     for (int depth = 0; depth <= 65536; ++depth) {
-      if (!__any(n != 0)) break;
+      if ((a.dbg & 1) || !__any(n != 0)) break;
       const int s = (n != 0) ? f.slot[n - 1] : -1;
       hist_add(sh, a.bins, s, label);
       if (n != 0) n = f.parent[n - 1];
     }
     // ring: a foreground pixel 4-adjacent to a selected hole of its own component
     int hs[4] = {-1, -1, -1, -1};
-    if (p < p1 && fgp) {
+    if (p < p1 && fgp && sel_holes) {
       const int me = f.L[p + 1];
       const int nb[4] = {x > 0 ? p - 1 : -1, x + 1 < a.cw ? p + 1 : -1, y > 0 ? p - a.cw : -1,
                          y + 1 < a.ch ? p + a.cw : -1};
@@ -972,6 +981,10 @@ void postprocess(const PostParams& p, hipStream_t s) {
   a.ws = static_cast<char*>(p.ws);
   a.lay = layout(p.H, p.W, p.K, p.num_bins);
   a.records = p.records;
+  {
+    const char* e = getenv("SSA_POST_DBG");
+    a.dbg = e ? atoi(e) : 0;
+  }
   // zero the per-frame counters and histograms (one contiguous, 256-B aligned region).
   // A kernel, not hipMemsetAsync: a memset node captured by torch.cuda.graph faulted
   // (illegal address) on its second replay on ROCm 7.x; kernel nodes replay cleanly.
@@ -982,7 +995,7 @@ void postprocess(const PostParams& p, hipStream_t s) {
   const dim3 blk(256);
   const dim3 gp(cdiv(N, 256), p.B);
   // SSA_POST_STAGES=n (debug) launches only the first n stages
-  static const int stages = [] {
+  const int stages = [] {  // read per call (host only; graph capture records one value)
     const char* e = getenv("SSA_POST_STAGES");
     return e ? atoi(e) : 99;
   }();
