@@ -57,7 +57,7 @@ struct FrameWS {
   int32_t* edges;      // [kEdgeCap][2] cross-tile unions (tile-local root pairs, -1 = outside)
 };
 
-constexpr int TW = 32, TH = 16;     // local CCL tile
+constexpr int TW = 32, TH = 32;     // local CCL tile
 constexpr int kTileRoots = TW * TH;  // worst case roots per tile
 constexpr int kMergeCap = 12288;     // compact nodes the per-frame LDS merge handles
 constexpr int kEdgeCap = 1 << 16;    // cross-tile union pairs per frame
@@ -171,8 +171,8 @@ __device__ void unite(int32_t* L, int a, int b) {
 }
 
 // ---------------------------------------------------------------- mask + local CCL
-// One 512-thread block = one TW x TH = 32 x 16 pixel tile, one thread per pixel,
-// half a wave per tile row.
+// One 512-thread block = one TW x TH = 32 x 32 pixel tile, two pixels per thread
+// (rows ty and ty + 16), half a wave per tile row.
 //  1. mask: the tile's labels + 1-pixel REFLECT_101 halo are staged in LDS, the
 //     palette colours are box-summed separably (horizontal 3-sums in LDS, then
 //     vertical), rounded per channel like cv2.blur, converted with the fixed-point
@@ -218,30 +218,39 @@ __device__ void lunite(int* l, int a, int b) {
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
-__global__ __launch_bounds__(TW * TH) void k_ccl_local(KArgs a, const int32_t* __restrict__ pal) {
-  constexpr int HW2 = TW + 2, HH2 = TH + 2;
+// 512 threads per TW x TH tile: each thread owns RPT = TH / 16 pixels of one column
+// (rows ty + 16 k), so a block's global-load and barrier latency is paid once per
+// RPT pixels, and the bigger tile halves the cross-tile edges / tile-local roots
+// the merge handles.
+constexpr int kCclThreads = 512;
+constexpr int RPT = TH * TW / kCclThreads;
+static_assert(RPT * kCclThreads == TW * TH && TW == 32, "k_ccl_local: 32-wide tiles, 512 threads");
+
+__global__ __launch_bounds__(kCclThreads) void k_ccl_local(KArgs a, const int32_t* __restrict__ pal) {
+  constexpr int HW2 = TW + 2, HH2 = TH + 2, RS = kCclThreads / TW;  // RS: row stride of a thread's pixels
   __shared__ int spal[256 * 3];
   __shared__ uint8_t slab[HH2 * HW2];
   __shared__ int hs[3][HH2 * TW];
   __shared__ int lbl[TW * TH];
   __shared__ unsigned fgrow[TH], bgrow[TH];
+  __shared__ int s_nroot;
   const int tid = threadIdx.x;
-  for (int i = tid; i < 256 * 3; i += TW * TH) spal[i] = pal[i];
+  for (int i = tid; i < 256 * 3; i += kCclThreads) spal[i] = pal[i];
+  if (tid == 0) s_nroot = 0;
   const int b = blockIdx.z;
   const int x0 = blockIdx.x * TW, y0 = blockIdx.y * TH;
-  const int tx = tid % TW, ty = tid / TW;
-  const int x = x0 + tx, y = y0 + ty;
-  const bool in = x < a.cw && y < a.ch;
+  const int tx = tid % TW, ty0 = tid / TW;
+  const int x = x0 + tx;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
   if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) f.L[0] = 0;
   const uint8_t* lab = a.labels + (size_t)b * a.H * a.W;
-  for (int i = tid; i < HH2 * HW2; i += TW * TH) {
+  for (int i = tid; i < HH2 * HW2; i += kCclThreads) {
     const int yy = clampi(reflect101(y0 - 1 + i / HW2, a.ch), 0, a.ch - 1);
     const int xx = clampi(reflect101(x0 - 1 + i % HW2, a.cw), 0, a.cw - 1);
     slab[i] = lab[yy * a.W + xx];
   }
   __syncthreads();
-  for (int i = tid; i < HH2 * TW; i += TW * TH) {
+  for (int i = tid; i < HH2 * TW; i += kCclThreads) {
     const int r = i / TW, c = i % TW;
     const uint8_t* sr = slab + r * HW2 + c;
     const int l0 = sr[0], l1 = sr[1], l2 = sr[2];
@@ -249,68 +258,80 @@ __global__ __launch_bounds__(TW * TH) void k_ccl_local(KArgs a, const int32_t* _
     for (int ch = 0; ch < 3; ++ch) hs[ch][i] = spal[l0 * 3 + ch] + spal[l1 * 3 + ch] + spal[l2 * 3 + ch];
   }
   __syncthreads();
-  bool m = false;
-  if (in) {
-    int c[3];
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-      const int sum = hs[ch][ty * TW + tx] + hs[ch][(ty + 1) * TW + tx] + hs[ch][(ty + 2) * TW + tx];
-      c[ch] = (sum * 2 + 9) / 18;
-    }
-    const int g = (c[0] * 1868 + c[1] * 9617 + c[2] * 4899 + (1 << 13)) >> 14;
-    m = g > a.thr;
-    f.mask[y * a.cw + x] = m ? 1 : 0;
-  }
-  // per-row run bitmasks (bit = column); lanes 0-31 / 32-63 of a wave are two rows
-  const unsigned long long bf = __ballot(in && m), bb = __ballot(in && !m);
+  bool m[RPT], in[RPT];
+  unsigned fgm[RPT], bgm[RPT];
+  int start[RPT];
   const int half = (tid & 63) >> 5;
-  const unsigned fgm = (unsigned)(bf >> (32 * half)), bgm = (unsigned)(bb >> (32 * half));
-  if ((tid & 31) == 0) {
-    fgrow[ty] = fgm;
-    bgrow[ty] = bgm;
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const int ty = ty0 + k * RS, y = y0 + ty;
+    in[k] = x < a.cw && y < a.ch;
+    m[k] = false;
+    if (in[k]) {
+      int c[3];
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        const int sum = hs[ch][ty * TW + tx] + hs[ch][(ty + 1) * TW + tx] + hs[ch][(ty + 2) * TW + tx];
+        c[ch] = (sum * 2 + 9) / 18;
+      }
+      const int g = (c[0] * 1868 + c[1] * 9617 + c[2] * 4899 + (1 << 13)) >> 14;
+      m[k] = g > a.thr;
+      f.mask[y * a.cw + x] = m[k] ? 1 : 0;
+    }
+    // per-row run bitmasks (bit = column); lanes 0-31 / 32-63 of a wave are two rows
+    const unsigned long long bf = __ballot(in[k] && m[k]), bb = __ballot(in[k] && !m[k]);
+    fgm[k] = (unsigned)(bf >> (32 * half));
+    bgm[k] = (unsigned)(bb >> (32 * half));
+    if ((tid & 31) == 0) {
+      fgrow[ty] = fgm[k];
+      bgrow[ty] = bgm[k];
+    }
+    const unsigned mine = m[k] ? fgm[k] : bgm[k];
+    const int me = ty * TW + tx;
+    start[k] = me;
+    if (in[k]) {
+      const unsigned starts = mine & ~(mine << 1);
+      start[k] = ty * TW + 31 - __clz(starts & (0xffffffffu >> (31 - tx)));
+    }
+    lbl[me] = start[k];
   }
-  const unsigned mine = m ? fgm : bgm;
-  const int me = tid;
-  int start = me;
-  if (in) {
-    const unsigned starts = mine & ~(mine << 1);
-    start = ty * TW + 31 - __clz(starts & (0xffffffffu >> (31 - tx)));
-  }
-  lbl[me] = start;
   __syncthreads();
-  if (in && ty > 0) {
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const int ty = ty0 + k * RS, me = ty * TW + tx;
+    if (!in[k] || ty == 0) continue;
     const unsigned bit = 1u << tx;
     const int up = me - TW;
-    if (m) {
+    if (m[k]) {
       const unsigned u = fgrow[ty - 1];
-      const unsigned ends = fgm & ~(fgm >> 1);
-      const bool first = (me == start);
+      const unsigned ends = fgm[k] & ~(fgm[k] >> 1);
+      const bool first = (me == start[k]);
       const bool last = (ends & bit) != 0;
-      if ((u & bit) && (first || !(u & (bit >> 1)))) lunite(lbl, start, up);
-      if (first && tx > 0 && (u & (bit >> 1)) && !(u & bit)) lunite(lbl, start, up - 1);
-      if (last && tx < 31 && (u & (bit << 1)) && !(u & bit)) lunite(lbl, start, up + 1);
+      if ((u & bit) && (first || !(u & (bit >> 1)))) lunite(lbl, start[k], up);
+      if (first && tx > 0 && (u & (bit >> 1)) && !(u & bit)) lunite(lbl, start[k], up - 1);
+      if (last && tx < 31 && (u & (bit << 1)) && !(u & bit)) lunite(lbl, start[k], up + 1);
     } else {
       const unsigned u = bgrow[ty - 1];
-      if ((u & bit) && (me == start || !(u & (bit >> 1)))) lunite(lbl, start, up);
+      if ((u & bit) && (me == start[k] || !(u & (bit >> 1)))) lunite(lbl, start[k], up);
     }
   }
   __syncthreads();
-  __shared__ int s_nroot;
-  if (tid == 0) s_nroot = 0;
-  __syncthreads();
-  if (in) {
-    const int r = lfind(lbl, start);
+  const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const int ty = ty0 + k * RS, y = y0 + ty, me = ty * TW + tx;
+    if (!in[k]) continue;
+    const int r = lfind(lbl, start[k]);
     const int rx = x0 + r % TW, ry = y0 + r / TW;
     f.L[y * a.cw + x + 1] = ry * a.cw + rx + 1;
     if (r == me) {  // tile-local root: number it for the compact merge
-      const int tile = blockIdx.y * gridDim.x + blockIdx.x;
       const int c = atomicAdd(&s_nroot, 1);
       f.cidx[y * a.cw + x] = c;
       f.rootpix[(size_t)tile * kTileRoots + c] = y * a.cw + x;
     }
   }
   __syncthreads();
-  if (tid == 0) f.ntroot[blockIdx.y * gridDim.x + blockIdx.x] = s_nroot;
+  if (tid == 0) f.ntroot[tile] = s_nroot;
 }
 
 // ---------------------------------------------------------------- compact merge
@@ -1001,7 +1022,7 @@ void postprocess(const PostParams& p, hipStream_t s) {
   }();
   int st = 0;
   const dim3 gt(cdiv(p.crop_w, TW), cdiv(p.crop_h, TH), p.B);
-  if (st++ < stages) hipLaunchKernelGGL(k_ccl_local, gt, dim3(TW * TH), 0, s, a, p.palette);
+  if (st++ < stages) hipLaunchKernelGGL(k_ccl_local, gt, dim3(kCclThreads), 0, s, a, p.palette);
   {
     const int tx_n = cdiv(p.crop_w, TW), ty_n = cdiv(p.crop_h, TH);
     const int nt = tx_n * ty_n;
