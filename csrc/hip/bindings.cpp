@@ -187,8 +187,9 @@ PYBIND11_MODULE(_hip, m) {
         [](uintptr_t in, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t img_bias,
            uintptr_t res, float res_scale, uintptr_t out, float inv_out_scale, int out_mode, int B,
            int IH, int IW, int Cin, int OH, int OW, int Cout, int KH, int KW, int stride, int dil,
-           int ldo, int co_off, int act, uintptr_t stream) {
+           int ldo, int co_off, int act, uintptr_t stream, int variant) {
           ConvI8Params p;
+          p.variant = variant;
           p.in = P<const int8_t>(in); p.w = P<const int8_t>(w); p.scale = P<const float>(scale);
           p.bias = P<const float>(bias); p.img_bias = P<const float>(img_bias);
           p.res = P<const int8_t>(res); p.res_scale = res_scale; p.out = P<void>(out);
@@ -197,7 +198,13 @@ PYBIND11_MODULE(_hip, m) {
           p.KH = KH; p.KW = KW; p.stride = stride; p.dil = dil; p.ldo = ldo; p.co_off = co_off;
           p.act = act;
           conv_i8(p, S(stream));
-        });
+        },
+        py::arg("in"), py::arg("w"), py::arg("scale"), py::arg("bias"), py::arg("img_bias"),
+        py::arg("res"), py::arg("res_scale"), py::arg("out"), py::arg("inv_out_scale"),
+        py::arg("out_mode"), py::arg("B"), py::arg("IH"), py::arg("IW"), py::arg("Cin"),
+        py::arg("OH"), py::arg("OW"), py::arg("Cout"), py::arg("KH"), py::arg("KW"),
+        py::arg("stride"), py::arg("dil"), py::arg("ldo"), py::arg("co_off"), py::arg("act"),
+        py::arg("stream"), py::arg("variant") = 0);
   m.def("maxpool3x3s2_i8", [](uintptr_t in, uintptr_t out, int B, int IH, int IW, int C, int OH,
                               int OW, uintptr_t stream) {
     maxpool3x3s2_i8(P<const int8_t>(in), P<int8_t>(out), B, IH, IW, C, OH, OW, S(stream));

@@ -141,6 +141,197 @@ void launch_i8(const I8Args& a, hipStream_t s) {
   check_launch("conv_i8");
 }
 
+// ---------------------------------------------------------------------------
+// LDS-DMA pipelined int8 variant (the structure of conv_gemm.hip's glds kernel):
+// BM x BN tiles, operand rows of 128 K-bytes go global -> LDS with
+// global_load_lds_dwordx4 (XOR-swizzled on the source address, padded chunks
+// read a zero page), a 2-stage ring with one barrier per 128-deep K step, and
+// the 16-byte fragments of v_mfma_i32_16x16x64_i8 read back from LDS. The
+// register-fed kernel above loads every fragment from global memory in each wave
+// (no reuse across a workgroup's waves); here a 128 x 128 tile's operands are
+// fetched once per workgroup.
+__device__ __attribute__((aligned(16))) int4 g_i8_zero[8];
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+template <int MT, int NT, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void conv_i8_glds_kernel(I8Args a) {
+  constexpr int NW = WM * WN, ST = 2;
+  constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN, ROWB = 128;  // 128 int8 of K per row
+  constexpr int GA = BM / (8 * NW), GB = BN / (8 * NW);
+  static_assert(GA * 8 * NW == BM && GB * 8 * NW == BN, "tile rows must split over the waves");
+  constexpr int SB = (BM + BN) * ROWB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* s_tap = reinterpret_cast<int*>(smem + ST * SB);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int r16 = lane & 15, kq = lane >> 4;
+  const int M = a.B * a.OH * a.OW;
+  const int tiles_m = cdiv_dev(M, BM), tiles_n = cdiv_dev(a.Cout, BN);
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tn = bid % tiles_n, tm = bid / tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int taps = a.KH * a.KW;
+  const int grow = lane >> 3, lc = (lane & 7) ^ grow;
+
+  int ay[GA], ax[GA];
+  long long aoff[GA];
+  bool av[GA];
+  int tapbits = 0;
+#pragma unroll
+  for (int i = 0; i < GA; ++i) {
+    const int m = m0 + wid * (BM / NW) + i * 8 + grow;
+    av[i] = m < M;
+    const int mm = av[i] ? m : 0;
+    const int b = mm / (a.OH * a.OW);
+    const int rem = mm - b * a.OH * a.OW;
+    ay[i] = (rem / a.OW) * a.stride;
+    ax[i] = (rem % a.OW) * a.stride;
+    aoff[i] = (((long long)b * a.IH + ay[i]) * a.IW + ax[i]) * a.Cin;
+    if (av[i])
+      for (int t = 0; t < taps; ++t) {
+        const int iy = ay[i] + (t / a.KW - a.KH / 2) * a.dil;
+        const int ix = ax[i] + (t % a.KW - a.KW / 2) * a.dil;
+        if (iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW) tapbits |= 1 << t;
+      }
+  }
+  long long boff[GB];
+  bool bv[GB];
+#pragma unroll
+  for (int j = 0; j < GB; ++j) {
+    const int n = n0 + wid * (BN / NW) + j * 8 + grow;
+    bv[j] = n < a.Cout;
+    boff[j] = (long long)(bv[j] ? n : 0) * taps * a.Cin;
+  }
+  if (tid == 0) *s_tap = 0;
+  __syncthreads();
+  if (tapbits) atomicOr(s_tap, tapbits);
+  __syncthreads();
+  const int tapmask = __builtin_amdgcn_readfirstlane(*s_tap);
+  unsigned long long tl = 0;
+  int ntap = 0;
+  for (int t = 0; t < taps; ++t)
+    if ((tapmask >> t) & 1) { tl |= (unsigned long long)t << (4 * ntap); ++ntap; }
+  const int cch = cdiv_dev(a.Cin, 128);
+  const int total = ntap * cch;
+
+  int is_tap = 0, is_c = 0;
+  auto issue = [&](int stage) {
+    const int t = (int)((tl >> (4 * is_tap)) & 15);
+    const int dy = (t / a.KW - a.KH / 2) * a.dil, dx = (t % a.KW - a.KW / 2) * a.dil;
+    const int c = is_c * 128 + lc * 16;
+    const bool cok = c < a.Cin;
+    const long long doff = ((long long)dy * a.IW + dx) * a.Cin + c;
+    char* sA = smem + stage * SB;
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      const int iy = ay[i] + dy, ix = ax[i] + dx;
+      const bool ok = av[i] && cok && iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW;
+      const void* src = ok ? (const void*)(a.in + aoff[i] + doff) : (const void*)g_i8_zero;
+      __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(sA + (wid * (BM / NW) + i * 8) * ROWB), 16, 0, 0);
+    }
+    char* sB = sA + BM * ROWB;
+    const long long wofs = (long long)t * a.Cin + c;
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      const void* src = (bv[j] && cok) ? (const void*)(a.w + boff[j] + wofs) : (const void*)g_i8_zero;
+      __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(sB + (wid * (BN / NW) + j * 8) * ROWB), 16, 0, 0);
+    }
+    if (++is_c == cch) { is_c = 0; ++is_tap; }
+  };
+
+  i32x4v acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = i32x4v{0, 0, 0, 0};
+
+  if (total > 0) issue(0);
+  for (int k = 0; k < total; ++k) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (k + 1 < total) issue((k + 1) % ST);
+    const char* sA = smem + (k % ST) * SB;
+    const char* sB = sA + BM * ROWB;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int kc = ks * 4 + kq;
+      i32x4v bfr[MT], afr[NT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int r = wm * 16 * MT + i * 16 + r16;
+        bfr[i] = *reinterpret_cast<const i32x4v*>(sA + r * ROWB + ((kc ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = wn * 16 * NT + j * 16 + r16;
+        afr[j] = *reinterpret_cast<const i32x4v*>(sB + n * ROWB + ((kc ^ (n & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[j], bfr[i], acc[i][j], 0, 0, 0);
+    }
+  }
+
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int m = m0 + wm * 16 * MT + i * 16 + r16;
+    if (m >= M) continue;
+    const int b = m / (a.OH * a.OW);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = n0 + wn * 16 * NT + j * 16 + kq * 4;
+      if (n >= a.Cout) continue;
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (n + q >= a.Cout) { v[q] = 0.f; continue; }
+        v[q] = (float)acc[i][j][q] * a.scale[n + q] + a.bias[n + q];
+        if (a.img_bias) v[q] += a.img_bias[(long long)b * a.Cout + n + q];
+        if (a.res) v[q] += (float)a.res[(long long)m * a.Cout + n + q] * a.res_scale;
+        v[q] = apply_act(v[q], a.act);
+      }
+      const long long o = (long long)m * a.ldo + a.co_off + n;
+      if (a.out_mode == 0) {
+        int8_t* op = static_cast<int8_t*>(a.out) + o;
+        signed char qv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          qv[q] = (signed char)fminf(fmaxf(rintf(v[q] * a.inv_out_scale), -127.f), 127.f);
+        if (n + 3 < a.Cout && ((a.ldo | a.co_off) & 3) == 0) {
+          *reinterpret_cast<char4*>(op) = make_char4(qv[0], qv[1], qv[2], qv[3]);
+        } else {
+          for (int q = 0; q < 4; ++q) if (n + q < a.Cout) op[q] = qv[q];
+        }
+      } else {
+        bf16* op = static_cast<bf16*>(a.out) + o;
+        for (int q = 0; q < 4; ++q) if (n + q < a.Cout) op[q] = (bf16)v[q];
+      }
+    }
+  }
+}
+
+template <int MT, int NT, int WM, int WN>
+void launch_i8_glds(const I8Args& a, hipStream_t s) {
+  constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN;
+  const int M = a.B * a.OH * a.OW;
+  const int grid = cdiv(M, BM) * cdiv(a.Cout, BN);
+  const size_t lds = 2 * (size_t)(BM + BN) * 128 + 16;
+  static bool attr = false;
+  if (!attr) {
+    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_i8_glds_kernel<MT, NT, WM, WN>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
+          "conv_i8_glds attr");
+    attr = true;
+  }
+  hipLaunchKernelGGL((conv_i8_glds_kernel<MT, NT, WM, WN>), dim3(grid), dim3(64 * WM * WN), lds, s, a);
+  check_launch("conv_i8_glds");
+}
+
 // ---- int8 helpers: max pool and global average pool on int8 NHWC
 __global__ void maxpool_i8_kernel(const int8_t* __restrict__ in, int8_t* __restrict__ out, int B,
                                   int IH, int IW, int C, int OH, int OW) {
@@ -202,6 +393,18 @@ void conv_i8(const ConvI8Params& p, hipStream_t s) {
            p.out_mode, p.B, p.IH, p.IW, p.Cin, p.OH, p.OW, p.Cout, p.KH, p.KW, p.stride, p.dil,
            p.ldo, p.co_off, p.act};
   const long long M = (long long)p.B * p.OH * p.OW;
+  // variant: 0 auto, 1 register-fed, 2 LDS-DMA 128 x 128 (4 waves), 3 LDS-DMA
+  // 128 x 256 (8 waves), 4 LDS-DMA 256 x 128 (8 waves)
+  const bool glds_ok = p.KH * p.KW <= 16 && (long long)p.B * p.IH * p.IW * p.Cin < (1LL << 40);
+  int v = p.variant;
+  if (v == 0) v = (glds_ok && p.Cout >= 64 && M >= 8192) ? (p.Cout >= 256 ? 3 : 2) : 1;
+  if (v >= 2 && !glds_ok) throw std::invalid_argument("conv_i8: LDS-DMA variants need <= 16 taps");
+  switch (v) {
+    case 2: launch_i8_glds<4, 4, 2, 2>(a, s); return;
+    case 3: launch_i8_glds<4, 4, 2, 4>(a, s); return;
+    case 4: launch_i8_glds<4, 4, 4, 2>(a, s); return;
+    default: break;
+  }
   if (p.Cout <= 32) launch_i8<4, 1>(a, s);
   else if (p.Cout <= 64 || M < 8192) launch_i8<2, 2>(a, s);
   else launch_i8<2, 4>(a, s);

@@ -81,6 +81,7 @@ struct ConvI8Params {
   int out_mode = 0;
   int B = 0, IH = 0, IW = 0, Cin = 0, OH = 0, OW = 0, Cout = 0;
   int KH = 1, KW = 1, stride = 1, dil = 1, ldo = 0, co_off = 0, act = 0;
+  int variant = 0;  // 0 auto, 1 register-fed, 2/3/4 LDS-DMA 128x128 / 128x256 / 256x128
 };
 void conv_i8(const ConvI8Params& p, hipStream_t s);
 void maxpool3x3s2_i8(const int8_t* in, int8_t* out, int B, int IH, int IW, int C, int OH, int OW,

@@ -26,6 +26,17 @@ from .deeplab import DeepLabV3, synthetic_normalized
 from .quant import calibrate, pack_int8
 
 
+_I8_VARIANTS = (1, 2, 3, 4)  # register-fed, LDS-DMA 128x128 / 128x256 / 256x128
+
+
+def I8(*args, **kw):
+    """One int8 conv step as an autotuned Choice over the conv_i8 kernel variants."""
+    from .hip_model import Choice
+    I8.n = getattr(I8, "n", 0) + 1
+    return Choice(f"i8conv{I8.n}", [(f"v{v}", [lambda *_, v=v: K.conv_i8(*args, variant=v, **kw)])
+                                    for v in _I8_VARIANTS])
+
+
 class HipDeepLabInt8:
     def __init__(self, model: DeepLabV3, device: torch.device, cfg=None,
                  scales: Optional[Dict[str, float]] = None, calib_hw: int = 257):
@@ -108,11 +119,11 @@ class HipDeepLabInt8:
         cat = buf("aspp_cat", B, h, w, self.cat_c)
         s_cat = S["aspp.cat"]
         w8, sc, bi = self.aspp_b0
-        ops.append(lambda *_, x=x, h=h, w=w, c=c: K.conv_i8(
+        ops.append(I8(
             x, w8, sc, bi, cat, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w, Cout=A, ldo=self.cat_c,
             co_off=0, act="relu", out_scale=s_cat))
         for j, ((aw, asc, ab), rate) in enumerate(self.aspp_atrous):
-            ops.append(lambda *_, x=x, h=h, w=w, c=c, aw=aw, asc=asc, ab=ab, rate=rate, j=j: K.conv_i8(
+            ops.append(I8(
                 x, aw, asc, ab, cat, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w, Cout=A, k=3, dil=rate,
                 ldo=self.cat_c, co_off=(j + 1) * A, act="relu", out_scale=s_cat))
         gap = buf("gap", B, c, dtype=torch.float32)
@@ -126,19 +137,37 @@ class HipDeepLabInt8:
         ops.append(lambda *_: K.matvec(pooled, self.proj_pool_w, None, img_bias, B=B, N=A, K=A))
         proj = buf("aspp_proj", B, h, w, A)
         pw8, psc, pb = self.proj
-        ops.append(lambda *_, h=h, w=w: K.conv_i8(
+        ops.append(I8(
             cat, pw8, psc, pb, proj, B=B, IH=h, IW=w, Cin=self.cat_c, OH=h, OW=w, Cout=A,
             act="relu", img_bias=img_bias, out_scale=S["aspp.proj"]))
         logits = buf("logits", B, h, w, self.ldk, dtype=torch.bfloat16)
         lw8, lsc, lb = self.logits_p
-        ops.append(lambda *_, h=h, w=w: K.conv_i8(
+        ops.append(I8(
             proj, lw8, lsc, lb, logits, B=B, IH=h, IW=w, Cin=A, OH=h, OW=w,
             Cout=self.num_classes, ldo=self.ldk, act=None))
         labels = buf("labels", B, H, W, dtype=torch.uint8)
         ops.append(lambda *_, h=h, w=w: K.upsample_argmax(
             logits, labels, B=B, h=h, w=w, K=self.num_classes, ldk=self.ldk, H=H, W=W))
         self._plans[key] = (ops, bufs)
+        self._autotune(ops, B, Hc, Wc)
         return self._plans[key]
+
+    def _autotune(self, ops, B, Hc, Wc) -> None:
+        """Time each int8 conv's kernel variants on the plan's real buffers, keep the fastest."""
+        from .hip_model import Choice
+        if torch.cuda.is_current_stream_capturing():
+            return
+        dev = self.device
+        frames = torch.zeros((B, Hc, Wc, 3), dtype=torch.uint8, device=dev)
+        lx = torch.zeros(self.W, dtype=torch.int32, device=dev)
+        ly = torch.zeros(self.H, dtype=torch.int32, device=dev)
+        for op in ops:  # populate every buffer once
+            op(frames, lx, ly)
+        for op in ops:
+            if isinstance(op, Choice):
+                op.autotune((frames, lx, ly), reps=3)
+        torch.cuda.synchronize(dev)
+        self.choices = {op.name: op.variants[op.pick][0] for op in ops if isinstance(op, Choice)}
 
     def _block(self, ops, buf, i, d, x, B, h, w, c):
         S = self.scales
@@ -147,25 +176,25 @@ class HipDeepLabInt8:
         OH, OW = conv_out_hw(h, w, 3, m.stride, m.dilation)
         w1, s1, b1 = d["c1"]
         t1 = buf(f"r{i}_c1", B, h, w, width)
-        ops.append(lambda *_, x=x, t1=t1, h=h, w=w, c=c: K.conv_i8(
+        ops.append(I8(
             x, w1, s1, b1, t1, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w, Cout=width, act="relu",
             out_scale=S[f"b{i}.c1"]))
         w2, s2, b2 = d["c2"]
         t2 = buf(f"r{i}_c2", B, OH, OW, width)
-        ops.append(lambda *_, t1=t1, t2=t2, h=h, w=w, OH=OH, OW=OW: K.conv_i8(
+        ops.append(I8(
             t1, w2, s2, b2, t2, B=B, IH=h, IW=w, Cin=width, OH=OH, OW=OW, Cout=width, k=3,
             stride=m.stride, dil=m.dilation, act="relu", out_scale=S[f"b{i}.c2"]))
         if d["down"] is not None:
             wd, sd, bd = d["down"]
             idt = buf(f"r{i}_down", B, OH, OW, cout)
-            ops.append(lambda *_, x=x, idt=idt, h=h, w=w, c=c, OH=OH, OW=OW: K.conv_i8(
+            ops.append(I8(
                 x, wd, sd, bd, idt, B=B, IH=h, IW=w, Cin=c, OH=OH, OW=OW, Cout=cout,
                 stride=m.stride, act=None, out_scale=S[f"b{i}.down"]))
         else:
             idt = x
         w3, s3, b3 = d["c3"]
         out = buf(f"r{i}_out", B, OH, OW, cout)
-        ops.append(lambda *_, t2=t2, out=out, idt=idt, OH=OH, OW=OW: K.conv_i8(
+        ops.append(I8(
             t2, w3, s3, b3, out, B=B, IH=OH, IW=OW, Cin=width, OH=OH, OW=OW, Cout=cout,
             act="relu", res=idt, res_scale=d["s_res"], out_scale=S[f"b{i}.out"]))
         return out, OH, OW, cout

@@ -566,8 +566,11 @@ def stem_conv(frames, lut_x, lut_y, w, bias, out, *, H, W, OH, OW, Cout, k, stri
 
 def conv_i8(x, w8, scale, bias, out, *, B, IH, IW, Cin, OH, OW, Cout, k=1, stride=1, dil=1,
             ldo=None, co_off=0, act=None, res=None, res_scale=0.0, img_bias=None,
-            out_scale=None) -> torch.Tensor:
-    """int8 NHWC conv. out int8 (out_scale given: v / out_scale rounded) or bf16."""
+            out_scale=None, variant=0) -> torch.Tensor:
+    """int8 NHWC conv. out int8 (out_scale given: v / out_scale rounded) or bf16.
+    variant: 0 auto, 1 register-fed, 2/3/4 LDS-DMA 128x128 / 128x256 / 256x128 tiles."""
+    if variant not in (0, 1, 2, 3, 4) or (variant >= 2 and k * k > 16):
+        raise ValueError("conv_i8: bad variant")
     ldo = Cout if ldo is None else ldo
     if Cin % 16:
         raise ValueError("conv_i8: Cin must be a multiple of 16")
@@ -585,7 +588,8 @@ def conv_i8(x, w8, scale, bias, out, *, B, IH, IW, Cin, OH, OW, Cout, k=1, strid
         _chk(img_bias, torch.float32, "img_bias", B * Cout)
     _hip_mod().conv_i8(_ptr(x), _ptr(w8), _ptr(scale), _ptr(bias), _ptr(img_bias), _ptr(res),
                        float(res_scale), _ptr(out), 1.0 / out_scale if mode == 0 else 1.0, mode, B,
-                       IH, IW, Cin, OH, OW, Cout, k, k, stride, dil, ldo, co_off, ACT[act], _stream())
+                       IH, IW, Cin, OH, OW, Cout, k, k, stride, dil, ldo, co_off, ACT[act], _stream(),
+                       variant)
     _dbg('conv_i8')
     return out
 

@@ -680,10 +680,11 @@ def test_pw_conv_fp16_out():
     assert _rel(out.float().cpu(), ref) < 2e-3
 
 
+@pytest.mark.parametrize("variant", [1, 2, 3, 4])
 @pytest.mark.parametrize("Cin,Cout,k,stride,dil,res,mode", [
     (64, 256, 1, 1, 1, True, "i8"), (256, 64, 3, 2, 1, False, "i8"), (512, 512, 3, 1, 2, False, "i8"),
-    (256, 19, 1, 1, 1, False, "bf16"), (1024, 256, 1, 1, 1, False, "i8")])
-def test_conv_i8(Cin, Cout, k, stride, dil, res, mode):
+    (256, 19, 1, 1, 1, False, "bf16"), (1024, 256, 1, 1, 1, False, "i8"), (208, 136, 3, 1, 3, True, "i8")])
+def test_conv_i8(Cin, Cout, k, stride, dil, res, mode, variant):
     K = _hip()
     g = torch.Generator().manual_seed(12)
     B, H = 2, 17
@@ -706,7 +707,7 @@ def test_conv_i8(Cin, Cout, k, stride, dil, res, mode):
         K.conv_i8(xin, wk, sc.to(DEV), bi.to(DEV), out, B=B, IH=H, IW=H, Cin=Cin, OH=OH, OW=OW,
                   Cout=Cout, k=k, stride=stride, dil=dil, act="relu",
                   res=None if r8 is None else _nhwc(r8.to(torch.int8)).to(DEV), res_scale=0.02,
-                  out_scale=0.05)
+                  out_scale=0.05, variant=variant)
         torch.cuda.synchronize()
         exp = torch.clamp(torch.round(ref / 0.05), -127, 127)
         diff = (_nchw(out).cpu().float() - exp).abs()
@@ -714,7 +715,7 @@ def test_conv_i8(Cin, Cout, k, stride, dil, res, mode):
     else:
         out = torch.empty(B, OH, OW, Cout, dtype=torch.bfloat16, device=DEV)
         K.conv_i8(xin, wk, sc.to(DEV), bi.to(DEV), out, B=B, IH=H, IW=H, Cin=Cin, OH=OH, OW=OW,
-                  Cout=Cout, k=k, stride=stride, dil=dil, act="relu")
+                  Cout=Cout, k=k, stride=stride, dil=dil, act="relu", variant=variant)
         torch.cuda.synchronize()
         assert _rel(_nchw(out).cpu(), ref) < 5e-3
 
