@@ -33,8 +33,11 @@ def I8(*args, **kw):
     """One int8 conv step as an autotuned Choice over the conv_i8 kernel variants."""
     from .hip_model import Choice
     I8.n = getattr(I8, "n", 0) + 1
-    return Choice(f"i8conv{I8.n}", [(f"v{v}", [lambda *_, v=v: K.conv_i8(*args, variant=v, **kw)])
-                                    for v in _I8_VARIANTS])
+    c = Choice(f"i8conv{I8.n}", [(f"v{v}", [lambda *_, v=v: K.conv_i8(*args, variant=v, **kw)])
+                                 for v in _I8_VARIANTS])
+    c.desc = (f"M={kw['B'] * kw['OH'] * kw['OW']} Cin={kw['Cin']} Cout={kw['Cout']} "
+              f"k={kw.get('k', 1)} s={kw.get('stride', 1)} d={kw.get('dil', 1)}")
+    return c
 
 
 class HipDeepLabInt8:
@@ -168,6 +171,14 @@ class HipDeepLabInt8:
                 op.autotune((frames, lx, ly), reps=3)
         torch.cuda.synchronize(dev)
         self.choices = {op.name: op.variants[op.pick][0] for op in ops if isinstance(op, Choice)}
+        import os
+        if os.environ.get("SSA_LOG_AUTOTUNE", "0") == "1":
+            import sys
+            for op in ops:
+                if isinstance(op, Choice) and hasattr(op, "times"):
+                    print(f"[autotune int8 B={B}] {op.name} {getattr(op, 'desc', '')}: " + ", ".join(
+                        f"{n}={t * 1e3:.1f}us" for (n, _), t in zip(op.variants, op.times)) +
+                        f" -> {op.variants[op.pick][0]}", file=sys.stderr)
 
     def _block(self, ops, buf, i, d, x, B, h, w, c):
         S = self.scales

@@ -18,6 +18,7 @@ record gather is tiny and latency-bound, so it is one collective per step.
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 from typing import List, Optional, Tuple
 
@@ -107,8 +108,10 @@ class DataParallelPipeline:
         self._prev_done = None  # compute-done event of the previous step
         if self.cuda and hasattr(engine, "bind_inputs"):
             # one hipGraph per staging slot reads the slot in place (no per-step D2D
-            # copy of the B x Hc x Wc x 3 frames into a single static input)
-            engine.bind_inputs(self.staging)
+            # copy of the B x Hc x Wc x 3 frames into a single static input); with
+            # lag >= 1 the post-processing graph of step k also runs on its own
+            # stream, concurrently with step k+1's model
+            engine.bind_inputs(self.staging, split_post=bool(self.lag))
 
     # ---------------------------------------------------------------- ingest
     def prefetch(self, host_frames: torch.Tensor) -> None:
@@ -171,30 +174,34 @@ class DataParallelPipeline:
             return self.engine.records_from_labels(labels, fids, tss, strm)
         slot = self._rslot
         self._rslot ^= 1
-        if self.ctx.initialized:
-            mh = self.meta_host[slot]
-            mh[:, 0] = torch.tensor(fids, dtype=torch.float64)
-            mh[:, 1] = torch.tensor(strm, dtype=torch.float64)
-            mh[:, 2] = torch.tensor(tss, dtype=torch.float64)
-            self.meta.copy_(mh, non_blocking=True)
-            send = packed if self.ctx.backend == "nccl" else packed.cpu()
-            dst = list(self.gather_buf.unbind(0)) if self.ctx.is_root else None
-            dist.gather(send, dst, dst=0)
-            mdst = list(self.meta_buf.unbind(0)) if self.ctx.is_root else None
-            dist.gather(self.meta, mdst, dst=0)
-            src = self.gather_buf if self.ctx.is_root else None
-        else:
-            src = packed.unsqueeze(0)
-        self.frames_done += B * self.ctx.world
-        if not self.ctx.is_root:
-            return np.zeros(0, RECORD_DTYPE)
-        self.host_rec[slot].copy_(src, non_blocking=True)
-        if self.ctx.initialized:
-            self.host_meta[slot].copy_(self.meta_buf, non_blocking=True)
-        ev = None
-        if self.cuda:
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(self.dev))
+        # the packed records are produced on the engine's result stream when its
+        # post-processing runs on a stream of its own: gather + D2H go there too
+        rs = getattr(self.engine, "result_stream", None) if self.cuda else None
+        with (torch.cuda.stream(rs) if rs is not None else contextlib.nullcontext()):
+            if self.ctx.initialized:
+                mh = self.meta_host[slot]
+                mh[:, 0] = torch.tensor(fids, dtype=torch.float64)
+                mh[:, 1] = torch.tensor(strm, dtype=torch.float64)
+                mh[:, 2] = torch.tensor(tss, dtype=torch.float64)
+                self.meta.copy_(mh, non_blocking=True)
+                send = packed if self.ctx.backend == "nccl" else packed.cpu()
+                dst = list(self.gather_buf.unbind(0)) if self.ctx.is_root else None
+                dist.gather(send, dst, dst=0)
+                mdst = list(self.meta_buf.unbind(0)) if self.ctx.is_root else None
+                dist.gather(self.meta, mdst, dst=0)
+                src = self.gather_buf if self.ctx.is_root else None
+            else:
+                src = packed.unsqueeze(0)
+            self.frames_done += B * self.ctx.world
+            if not self.ctx.is_root:
+                return np.zeros(0, RECORD_DTYPE)
+            self.host_rec[slot].copy_(src, non_blocking=True)
+            if self.ctx.initialized:
+                self.host_meta[slot].copy_(self.meta_buf, non_blocking=True)
+            ev = None
+            if self.cuda:
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(self.dev))
         cur = (slot, ev, fids, strm, tss)
         if not self.lag:
             return self._collect(cur)

@@ -200,14 +200,25 @@ class Engine:
         self._graph = g
         self._graph_B = B
 
-    def bind_inputs(self, bufs) -> None:
+    def bind_inputs(self, bufs, split_post: bool = False) -> None:
         """Declare persistent frame buffers (e.g. the DP pipeline's double-buffered
         staging slots): ``run_device`` on one of them replays a graph captured with
         that buffer as its input, so the step reads the frames in place instead of
         copying them into the single static input first (one D2D copy of
-        B x Hc x Wc x 3 bytes and one launch per step saved)."""
+        B x Hc x Wc x 3 bytes and one launch per step saved).
+
+        ``split_post``: per slot, TWO graphs -- the model (frames -> the slot's own
+        label maps) on the caller's stream and the device post-processing (labels
+        -> packed records) on ``result_stream``. The post-processing kernels are
+        latency-bound (union-find chains, per-frame merges, few workgroups), so step
+        k's post-processing runs concurrently with step k+1's model instead of
+        idling the chip at the end of every step. Consumers of the packed records
+        must be ordered after ``result_stream`` (the DP pipeline enqueues its gather
+        and D2H copy there)."""
         if not (self.cfg.graph and self.is_cuda):
             return
+        self._split = bool(split_post) and self._use_device_post()
+        self.result_stream = torch.cuda.Stream(self.device) if self._split else None
         self._bound = {b.data_ptr(): b for b in bufs}
         self._bound_graphs = {}
         if self.cam is not None:  # capture now, not inside the first timed steps
@@ -230,10 +241,20 @@ class Engine:
                 for _ in range(2):  # warm up allocator / lazy init outside capture
                     self._step_device(b)
             torch.cuda.current_stream(self.device).wait_stream(s)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                labels, post = self._step_device(b)
-            ent = (tuple(frames.shape), g, labels, post)
+            if getattr(self, "_split", False):
+                lab = torch.empty((b.shape[0], self.H, self.W), dtype=torch.uint8, device=self.device)
+                gm = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gm):
+                    lab.copy_(self._infer_eager(b))  # the slot's own label maps
+                gp = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gp):
+                    post = self._device_post(lab)
+                ent = (tuple(frames.shape), gm, lab, post, gp, torch.cuda.Event())
+            else:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    labels, post = self._step_device(b)
+                ent = (tuple(frames.shape), g, labels, post, None, None)
             self._bound_graphs[key] = ent
         return ent
 
@@ -242,14 +263,28 @@ class Engine:
 
         With ``cfg.graph`` the step is captured on first use per (B, camera) and
         replayed; outputs then live in static buffers overwritten by the next call.
-        Frames in a buffer declared with ``bind_inputs`` run that buffer's own graph.
+        Frames in a buffer declared with ``bind_inputs`` run that buffer's own graph
+        (with ``split_post``, the records are produced on ``result_stream``).
         """
         B = frames.shape[0]
         if self.cfg.graph and self.is_cuda:
             ent = self._bound_graph(frames)
             if ent is not None:
-                ent[1].replay()
-                return ent[2], ent[3]
+                _, g, labels, post, gpost, post_done = ent
+                if gpost is None:
+                    g.replay()
+                    return labels, post
+                cur = torch.cuda.current_stream(self.device)
+                cur.wait_event(post_done)  # this slot's previous post-processing read `labels`
+                g.replay()
+                ready = torch.cuda.Event()
+                ready.record(cur)
+                rs = self.result_stream
+                rs.wait_event(ready)
+                with torch.cuda.stream(rs):
+                    gpost.replay()
+                post_done.record(rs)
+                return labels, post
             if self._graph is None or self._graph_B != B:
                 self._capture(B)
             self._static["frames"].copy_(frames, non_blocking=True)

@@ -437,9 +437,11 @@ def test_engine_graph_replay_matches_eager():
     assert p2 is not None and p2.shape == (2, 1 + 5 * cfg.max_segments)
 
 
-def test_engine_bound_input_graphs():
+@pytest.mark.parametrize("split", [False, True])
+def test_engine_bound_input_graphs(split):
     """bind_inputs: a graph per persistent input buffer reads it in place; results
-    equal the eager step, alternating between the buffers after they are refilled."""
+    equal the eager step, alternating between the buffers after they are refilled.
+    split: model and post-processing graphs on two streams (records on result_stream)."""
     from semantic_segmentation_server_amd.runtime.engine import Engine
     from semantic_segmentation_server_amd.runtime.sources import SyntheticSource
     cfg = _small_cfg(graph=True)
@@ -447,17 +449,30 @@ def test_engine_bound_input_graphs():
     eng.set_camera(200, 150)
     src = SyntheticSource(200, 150, pool=4, seed=3)
     bufs = [torch.empty((2, 150, 200, 3), dtype=torch.uint8, device=DEV) for _ in range(2)]
-    eng.bind_inputs(bufs)
+    eng.bind_inputs(bufs, split_post=split)
     for it in range(3):
         for b in bufs:
             f, _, _ = src.read_batch(2)
             b.copy_(torch.from_numpy(f))
+            torch.cuda.synchronize()
             want = eng._infer_eager(b).clone()
             want_post = eng._device_post(want).clone()
+            torch.cuda.synchronize()
             got, post = eng.run_device(b)
             torch.cuda.synchronize()
             assert torch.equal(got, want), it
             assert torch.equal(post, want_post), it
+    # pipelined: both slots in flight before anything is read back
+    outs = []
+    for b in bufs:
+        got, post = eng.run_device(b)
+        rs = getattr(eng, "result_stream", None) or torch.cuda.current_stream()
+        with torch.cuda.stream(rs):
+            outs.append((got.clone(), post.clone()))
+    torch.cuda.synchronize()
+    for (got, post), b in zip(outs, bufs):
+        want = eng._infer_eager(b).clone()
+        assert torch.equal(got, want) and torch.equal(post, eng._device_post(want))
     assert len(eng._bound_graphs) == 2
 
 
