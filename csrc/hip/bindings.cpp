@@ -66,6 +66,12 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("groups"), py::arg("order"), py::arg("nblocks"), py::arg("variant"),
         py::arg("stream"));
 
+  m.def("bias_act", [](uintptr_t in, uintptr_t bias, uintptr_t img_bias, uintptr_t out, long long M,
+                       int N, int HW, int act, uintptr_t stream) {
+    bias_act(P<const bf16>(in), P<const float>(bias), P<const float>(img_bias), P<bf16>(out), M, N, HW,
+             act, S(stream));
+  });
+
   m.def("fused_ir",
         [](uintptr_t in, uintptr_t we, uintptr_t be, uintptr_t wd, uintptr_t bd, uintptr_t wp,
            uintptr_t bp, uintptr_t out, int B, int IH, int IW, int Cin, int CinP, int hidP,

@@ -187,6 +187,9 @@ size_t gap_workspace_floats(int B, int C);
 void global_avgpool(const bf16* in, float* out, float* ws, int B, int HW, int C, hipStream_t s);
 
 // out[b, n] = act(sum_k W[n, k] * x[b, k] + bias[n]), fp32 everywhere (tiny).
+// out = act(in + bias[n] + img_bias[m / HW][n]) over an [M, N] bf16 matrix (GEMM epilogue)
+void bias_act(const bf16* in, const float* bias, const float* img_bias, bf16* out, long long M, int N,
+              int HW, int act, hipStream_t s);
 void matvec(const float* x, const float* w, const float* bias, float* out, int B, int N, int K,
             int act, hipStream_t s);
 

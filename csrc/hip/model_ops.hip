@@ -360,6 +360,44 @@ __global__ __launch_bounds__(256) void matvec_kernel(const float* __restrict__ x
   if (lane == 0) out[item] = apply_act(s + (bias ? bias[n] : 0.f), act);
 }
 
+// Epilogue of a library GEMM (the ASPP projection on hipBLASLt):
+//   out[m, n] = act(in[m, n] + bias[n] + img_bias[m / HW][n]), bf16, 8 channels per thread
+__global__ __launch_bounds__(256) void bias_act_kernel(const bf16* __restrict__ in,
+                                                       const float* __restrict__ bias,
+                                                       const float* __restrict__ img_bias,
+                                                       bf16* __restrict__ out, int M, int N,
+                                                       int HW, int act) {
+  // 32-bit index math (host checks M * N < 2^31): the 64-bit divisions of a naive
+  // version cost more than the memory traffic
+  const int NG = N >> 3;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= M * NG) return;
+  const int m = t / NG;
+  const int n = (t - m * NG) * 8;
+  const bf16x8 v = ld8(in + (size_t)m * N + n);
+  float4 b0 = *reinterpret_cast<const float4*>(bias + n), b1 = *reinterpret_cast<const float4*>(bias + n + 4);
+  if (img_bias) {
+    const float* ib = img_bias + (size_t)(m / HW) * N + n;
+    const float4 i0 = *reinterpret_cast<const float4*>(ib), i1 = *reinterpret_cast<const float4*>(ib + 4);
+    b0.x += i0.x; b0.y += i0.y; b0.z += i0.z; b0.w += i0.w;
+    b1.x += i1.x; b1.y += i1.y; b1.z += i1.z; b1.w += i1.w;
+  }
+  const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+  bf16x8 o;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) o[q] = (bf16)apply_act((float)v[q] + bb[q], act);
+  st8(out + (size_t)m * N + n, o);
+}
+
+void bias_act(const bf16* in, const float* bias, const float* img_bias, bf16* out, long long M, int N,
+              int HW, int act, hipStream_t s) {
+  if (N % 8 || HW < 1) throw std::invalid_argument("bias_act: N % 8 == 0 and HW >= 1 required");
+  if (M * (long long)N >= (1LL << 31)) throw std::invalid_argument("bias_act: matrix too large");
+  hipLaunchKernelGGL(bias_act_kernel, dim3(cdiv(M * (N / 8), 256)), dim3(256), 0, s, in, bias, img_bias,
+                     out, (int)M, N, HW, act);
+  check_launch("bias_act");
+}
+
 void matvec(const float* x, const float* w, const float* bias, float* out, int B, int N, int K,
             int act, hipStream_t s) {
   hipLaunchKernelGGL(matvec_kernel, dim3(cdiv((long long)B * N, 4)), dim3(256), 0, s, x, w, bias,

@@ -342,10 +342,22 @@ class HipDeepLab:
                                                 K=c, act="relu"))
             ops.append(lambda *_: K.matvec(pooled, self.proj_pool_w, None, img_bias, B=B, N=A, K=A))
         proj = buf("aspp_proj", B, h, w, A)
-        ops.append(Choice("aspp.proj", [(f"v{v}", [
+        proj_variants = [(f"v{v}", [
             lambda *_, h=h, w=w, v=v: K.conv_gemm(
                 cat, self.proj_w, self.proj_b, proj, B=B, IH=h, IW=w, Cin=self.cat_c, OH=h, OW=w,
-                Cout=A, k=1, act="relu", img_bias=img_bias, variant=v)]) for v in (4, 3, 5, 6)]))
+                Cout=A, k=1, act="relu", img_bias=img_bias, variant=v)]) for v in (4, 3, 5, 6)]
+        if A % 8 == 0:
+            # the projection is a plain [B*h*w, 1024] x [1024, 256] GEMM: hipBLASLt, then
+            # one fused bias + per-image pooling bias + ReLU pass
+            raw = buf("aspp_proj_raw", B * h * w, A)
+            Mp = B * h * w
+            wt = self.proj_w.t().contiguous()  # [1024, 256] row-major: hipBLASLt's fast NN layout
+            bufs["aspp_proj_wt"] = wt
+            proj_variants.append(("blaslt", [
+                lambda *_, wt=wt: torch.mm(cat.view(Mp, self.cat_c), wt, out=raw),
+                lambda *_, h=h, w=w: K.bias_act(raw, self.proj_b, proj, M=Mp, N=A, HW=h * w,
+                                                img_bias=img_bias, act="relu")]))
+        ops.append(Choice("aspp.proj", proj_variants))
         logits = buf("logits", B, h, w, self.ldk)
         ops.append(pw_choice("logits", lambda *_, h=h, w=w: K.conv_gemm(
             proj, self.logit_w, self.logit_b, logits, B=B, IH=h, IW=w, Cin=A, OH=h, OW=w,

@@ -226,6 +226,22 @@ def conv_gemm_grouped(convs: List[dict], order: torch.Tensor, variant: int = 5) 
     _dbg('conv_gemm_grouped')
 
 
+def bias_act(x, bias, out, *, M: int, N: int, HW: int = 1, img_bias=None, act=None):
+    """out[m, n] = act(x[m, n] + bias[n] + img_bias[m // HW][n]); x, out [M, N] bf16."""
+    _chk(x, torch.bfloat16, "x", M * N)
+    _chk(out, torch.bfloat16, "out", M * N)
+    _chk(bias, torch.float32, "bias", N)
+    if img_bias is not None:
+        _chk(img_bias, torch.float32, "img_bias", (M // HW) * N)
+        if M % HW:
+            raise ValueError("bias_act: M must be a multiple of HW")
+    if N % 8:
+        raise ValueError("bias_act: N must be a multiple of 8")
+    _hip_mod().bias_act(_ptr(x), _ptr(bias), _ptr(img_bias), _ptr(out), M, N, HW, ACT[act], _stream())
+    _dbg('bias_act')
+    return out
+
+
 def pw_supported(K: int, N: int) -> bool:
     """True if pw_conv has an instantiation for this (K = Cin, N = Cout) pair."""
     ks = (K + 31) // 32

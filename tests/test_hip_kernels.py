@@ -137,6 +137,24 @@ def test_conv_gemm_grouped_aspp(B, H, W, Cin, Cout, variant):
     assert torch.all(out[..., 4 * Cout:] == 7.0)
 
 
+@pytest.mark.parametrize("img", [True, False])
+def test_bias_act(img):
+    """GEMM epilogue: act(x + bias + per-image bias) vs torch."""
+    K = _hip()
+    g = torch.Generator().manual_seed(3)
+    B, HW, N = 3, 37, 264
+    x = torch.randn(B * HW, N, generator=g).to(torch.bfloat16)
+    b = torch.randn(N, generator=g)
+    ib = torch.randn(B, N, generator=g)
+    ref = x.float() + b + (ib.repeat_interleave(HW, 0) if img else 0)
+    ref = torch.relu(ref)
+    out = torch.empty(B * HW, N, dtype=torch.bfloat16, device=DEV)
+    K.bias_act(x.to(DEV), b.to(DEV), out, M=B * HW, N=N, HW=HW, img_bias=ib.to(DEV) if img else None,
+               act="relu")
+    torch.cuda.synchronize()
+    assert _rel(out.float().cpu(), ref) < 1e-2
+
+
 @pytest.mark.parametrize("B,H,W,Cin,Cout,rate,grouped", [
     (3, 33, 33, 320, 256, 6, True), (2, 33, 33, 320, 256, 12, False), (2, 33, 33, 320, 256, 18, True),
     (2, 17, 21, 160, 96, 24, True), (1, 9, 11, 64, 200, 1, False), (2, 20, 20, 256, 136, 2, True)])
