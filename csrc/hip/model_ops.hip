@@ -506,13 +506,7 @@ __global__ __launch_bounds__(256) void upsample_argmax_interval_kernel(
     }
   }
   uint8_t* op = labels + ((size_t)b * H + Y) * W;
-#pragma unroll
-  for (int e = 0; e < PXMAX; ++e) {
-    const int X = xs + e;
-    if (X >= W) break;
-    const float fx = sw * (float)X;
-    if ((int)fx != j) break;
-    const float lx1 = j < w - 1 ? fx - (float)j : 0.f;
+  auto argmax_at = [&](float lx1) {
     float best = -3.0e38f;
     int arg = 0;
 #pragma unroll
@@ -520,7 +514,34 @@ __global__ __launch_bounds__(256) void upsample_argmax_interval_kernel(
       const float v = v0[k] + lx1 * dv[k];
       if (k < K && v > best) { best = v; arg = k; }
     }
-    op[X] = (uint8_t)arg;
+    return arg;
+  };
+  // pixels of this interval: X in [xs, xe)
+  int xe = xs;
+#pragma unroll
+  for (int e = 0; e < PXMAX; ++e) {
+    const int X = xs + e;
+    if (X >= W || (int)(sw * (float)X) != j) break;
+    xe = X + 1;
+  }
+  if (xe == xs) return;
+  // Along the interval every class score is LINEAR in lx1, and the max of linear
+  // functions is convex: when one class wins at both end pixels it wins at every
+  // pixel in between. The common case (smooth logits) then costs two argmaxes
+  // instead of one per pixel (up to 16).
+  const float lxa = j < w - 1 ? sw * (float)xs - (float)j : 0.f;
+  const float lxb = j < w - 1 ? sw * (float)(xe - 1) - (float)j : 0.f;
+  const int a0 = argmax_at(lxa);
+  const int a1 = xe - 1 > xs ? argmax_at(lxb) : a0;
+  if (a0 == a1) {
+    for (int X = xs; X < xe; ++X) op[X] = (uint8_t)a0;
+    return;
+  }
+  op[xs] = (uint8_t)a0;
+  op[xe - 1] = (uint8_t)a1;
+  for (int X = xs + 1; X < xe - 1; ++X) {
+    const float lx1 = j < w - 1 ? sw * (float)X - (float)j : 0.f;
+    op[X] = (uint8_t)argmax_at(lx1);
   }
 }
 

@@ -232,6 +232,7 @@ class HipDeepLab:
         self.logit_w = lw[:, :, 0, 0].reshape(lw.shape[0], 1, 1, -1).contiguous().to(dev, torch.bfloat16)
         self.logit_b = lb.to(dev, torch.float32)
         self._plans: Dict[tuple, Tuple[List[Callable], Dict[str, torch.Tensor]]] = {}
+        self._labels_out: Optional[torch.Tensor] = None
 
     # ------------------------------------------------------------------ plan
     def _plan(self, B: int, Hc: int, Wc: int):
@@ -365,8 +366,11 @@ class HipDeepLab:
             self.logit_b, logits, M=B * h * w, Cin=A, Cout=self.num_classes, ldo=self.ldk, act=None,
             N_out=self.ldk))
         labels = buf("labels", B, H, W, dtype=torch.uint8)
+        # labels_out (segment's out=): write the label maps straight into a caller
+        # buffer (the engine's per-slot maps) instead of the plan's static one
         ops.append(lambda *_, h=h, w=w: K.upsample_argmax(
-            logits, labels, B=B, h=h, w=w, K=self.num_classes, ldk=self.ldk, H=H, W=W))
+            logits, self._labels_out if self._labels_out is not None else labels, B=B, h=h, w=w,
+            K=self.num_classes, ldk=self.ldk, H=H, W=W))
         self._plans[key] = (ops, bufs)
         self._autotune(ops, B, Hc, Wc)
         return self._plans[key]
@@ -536,16 +540,25 @@ class HipDeepLab:
         return out, OH, OW, cout
 
     # ------------------------------------------------------------------ run
-    def segment(self, frames: torch.Tensor, lut_x: torch.Tensor, lut_y: torch.Tensor) -> torch.Tensor:
-        """frames: (B, Hc, Wc, 3) uint8 BGR on device -> (B, H, W) uint8 labels (static buffer)."""
+    def segment(self, frames: torch.Tensor, lut_x: torch.Tensor, lut_y: torch.Tensor,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """frames: (B, Hc, Wc, 3) uint8 BGR on device -> (B, H, W) uint8 labels (static
+        buffer, or ``out``)."""
         B, Hc, Wc, _ = frames.shape
         if lut_x.numel() != self.W or lut_y.numel() != self.H:
             raise ValueError("letterbox LUTs do not match the model input size")
         ops, bufs = self._plan(B, Hc, Wc)
+        if out is not None and (out.shape != bufs["labels"].shape or out.dtype != torch.uint8
+                                or not out.is_contiguous() or out.device != bufs["labels"].device):
+            raise ValueError("segment: out must match the (B, H, W) uint8 label buffer")
         frames = frames.contiguous()
-        for op in ops:
-            op(frames, lut_x, lut_y)
-        return bufs["labels"]
+        self._labels_out = out
+        try:
+            for op in ops:
+                op(frames, lut_x, lut_y)
+        finally:
+            self._labels_out = None
+        return bufs["labels"] if out is None else out
 
     def logits(self, frames, lut_x, lut_y) -> torch.Tensor:
         """Run and return the NHWC logits buffer (tests)."""

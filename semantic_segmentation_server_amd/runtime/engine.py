@@ -244,8 +244,11 @@ class Engine:
             if getattr(self, "_split", False):
                 lab = torch.empty((b.shape[0], self.H, self.W), dtype=torch.uint8, device=self.device)
                 gm = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gm):
-                    lab.copy_(self._infer_eager(b))  # the slot's own label maps
+                with torch.cuda.graph(gm):  # the model writes the slot's own label maps
+                    if hasattr(self._hip_model, "_labels_out"):
+                        self._hip_model.segment(b, self.lut_x, self.lut_y, out=lab)
+                    else:
+                        lab.copy_(self._infer_eager(b))
                 gp = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gp):
                     post = self._device_post(lab)

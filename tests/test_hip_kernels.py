@@ -506,16 +506,20 @@ def test_dp_pipeline_records_match_eager(lag):
     from semantic_segmentation_server_amd.runtime.sources import SyntheticSource
     kw = dict(batch=2, input_size=257, min_area_ratio=0.002)
     eng = Engine(_small_cfg(graph=True, **kw), torch.device(DEV))
-    ref = Engine(_small_cfg(graph=False, **kw), torch.device(DEV), model=eng.model)
-    ctx = D.init()
-    pipe = DataParallelPipeline(ctx, eng, 160, 120, 2, "local", None, lag=lag)
     src = SyntheticSource(160, 120, seed=7, pool=4)
     batches = [torch.from_numpy(np.ascontiguousarray(src.read_batch(2)[0])) for _ in range(2)]
+    # expected: the same engine's eager (ungraphed, single-stream) step -- same weights and
+    # the same autotuned kernel picks, so the records must match exactly
+    eng.set_camera(160, 120)
     want = []
     for k in range(6):
-        f = batches[k % 2]
-        r = ref.step(f.numpy(), [k * 2, k * 2 + 1], [0.0, 0.0], 0)
+        f = batches[k % 2].to(DEV)
+        _, post = eng._step_device(f)
+        r = eng._hip_post.fetch(post, [k * 2, k * 2 + 1], [0.0, 0.0], [0, 0], eng.W, eng.H)
         want.append(sorted(zip(r["frame"].tolist(), r["label"].tolist(), r["area"].round(6).tolist())))
+    torch.cuda.synchronize()
+    ctx = D.init()
+    pipe = DataParallelPipeline(ctx, eng, 160, 120, 2, "local", None, lag=lag)
     got_all = []
     pipe.prefetch(batches[0].pin_memory())
     for k in range(6):
