@@ -46,7 +46,22 @@ struct PLayout {  // byte offsets into dynamic LDS
   int we, wp, wd, bd, be, bp, X, E, total;
 };
 
-__host__ __device__ inline PLayout playout(int CinP, int hidP, int CoutP, int in_groups) {
+// Row pitch of the expanded chunk E, in 16-byte units (one halo pixel = 5 units:
+// 32 fp16 channels + a 16-byte pad). A ds_read_b128 is serviced 16 lanes at a time,
+// conflict-free when the 16 lanes hit 16 distinct 16-byte bank groups (mod 16).
+// The depthwise reads 16 consecutive output pixels: within a row 5 * dx is distinct
+// mod 16, and across the row wrap (lanes (r, x) and (r + 1, x'), x' - x in
+// [-(TX - 1), 15 - TX]) the pitch RP must avoid RP + 5 (x' - x) == 0 mod 16, i.e.
+// RP == 5 * TX mod 16 (stride 1). The unpadded pitch 5 * TIW put two lanes of every
+// row-wrapping group on one bank group (2-way conflicts on every depthwise read).
+__host__ __device__ inline int e_pitch(int TX, int TIW, int stride) {
+  int rp = 5 * TIW;
+  if (stride == 1)
+    while ((rp - 5 * TX) % 16 != 0) ++rp;
+  return rp;
+}
+
+__host__ __device__ inline PLayout playout(int CinP, int hidP, int CoutP, int in_groups, int e_bytes) {
   PLayout l;
   int o = 0;
   l.we = o; o += hidP * (CinP + 8) * 2;
@@ -58,7 +73,7 @@ __host__ __device__ inline PLayout playout(int CinP, int hidP, int CoutP, int in
   l.bp = o; o += CoutP * 4;
   o = (o + 15) & ~15;
   l.X = o; o += in_groups * 16 * (CinP + 8) * 2;
-  l.E = o; o += in_groups * 16 * 40 * 2;
+  l.E = o; o += e_bytes > in_groups * 16 * 40 * 2 ? e_bytes : in_groups * 16 * 40 * 2;
   l.total = o;
   return l;
 }
@@ -74,7 +89,8 @@ __global__ __launch_bounds__(64 * kPNW) void fused_ir_persist_kernel(PIRArgs a) 
   const int in_px = TIH * TIW;
   const int in_groups = (in_px + 15) / 16;
   const int hidP = a.hidP, WPS = hidP + 8;
-  const PLayout L = playout(CinP, hidP, a.CoutP, in_groups);
+  const int RPE = e_pitch(a.TX, TIW, s) * 8;  // E row pitch in fp16 elements
+  const PLayout L = playout(CinP, hidP, a.CoutP, in_groups, TIH * RPE * 2 + 256);
   bf16* sWe = reinterpret_cast<bf16*>(smem + L.we);
   f16* sWp = reinterpret_cast<f16*>(smem + L.wp);
   f16* sWd = reinterpret_cast<f16*>(smem + L.wd);
@@ -160,9 +176,15 @@ __global__ __launch_bounds__(64 * kPNW) void fused_ir_persist_kernel(PIRArgs a) 
     opy[g] = p / a.TX;
     opx[g] = p - opy[g] * a.TX;
     pin[g] = p < a.TY * a.TX;
-    pofs[g] = pin[g] ? (opy[g] * s * TIW + opx[g] * s) * ES : 0;
+    pofs[g] = pin[g] ? opy[g] * s * RPE + opx[g] * s * ES : 0;
   }
-  const int dw_row = TIW * dl * ES, dw_col = dl * ES;  // tap strides in E (elements)
+  const int dw_row = dl * RPE, dw_col = dl * ES;  // tap strides in E (elements)
+  int geo[MAXG];  // E element offset of each expansion group's halo pixel
+#pragma unroll
+  for (int k = 0; k < MAXG; ++k) {
+    const int ty = gyx[k] >> 16, tx = gyx[k] & 0xffff;
+    geo[k] = ty < 0x7fff ? ty * RPE + tx * ES : TIH * RPE;  // padding lanes: scratch slack past E
+  }
 
   const f16x8 h0 = {0, 0, 0, 0, 0, 0, 0, 0}, h6 = {6, 6, 6, 6, 6, 6, 6, 6};
   for (; tile < a.ntiles; tile += gridDim.x) {
@@ -212,7 +234,7 @@ __global__ __launch_bounds__(64 * kPNW) void fused_ir_persist_kernel(PIRArgs a) 
           f16x4 o = {(f16)e[0], (f16)e[1], (f16)e[2], (f16)e[3]};
           o = __builtin_elementwise_min(__builtin_elementwise_max(o, h0.lo), h6.lo);
           if (!in_img) o = h0.lo;  // zero padding applies to the expanded tensor
-          *reinterpret_cast<f16x4*>(E + gip[kg] * ES + sub * 16 + kq * 4) = o;
+          *reinterpret_cast<f16x4*>(E + geo[kg] + sub * 16 + kq * 4) = o;
         }
       }
       __syncthreads();
@@ -312,7 +334,8 @@ size_t fused_ir_persist_lds(int CinP, int hidP, int Cout, int stride, int dil, i
   const int CoutP = (Cout + 15) / 16 * 16;
   if ((size_t)in_groups * 16 * (CinP / 8) > (size_t)kPXPF * 64 * kPNW) return 0;  // prefetch registers
   if (in_groups > kPMaxG * kPNW) return 0;                                       // expansion groups per wave
-  return (size_t)playout(CinP, hidP, CoutP, in_groups).total;
+  const int RPE = e_pitch(TX, TIW, stride) * 8;
+  return (size_t)playout(CinP, hidP, CoutP, in_groups, TIH * RPE * 2 + 256).total;
 }
 
 void fused_ir_persist(const FusedIRParams& p, hipStream_t st) {
