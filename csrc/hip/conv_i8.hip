@@ -29,6 +29,102 @@ struct I8Args {
 
 __device__ __forceinline__ i32x4v ld16(const int8_t* p) { return *reinterpret_cast<const i32x4v*>(p); }
 
+// Transposing epilogue (NT == 4: a wave's 64 output channels): the MFMA C layout
+// gives a lane 4 channels of one pixel per 16-channel subtile, so a direct store is
+// 4 bytes per lane at a Cout stride and the int8 residual is read byte by byte.
+// Per 16-pixel group the wave stages its int32 accumulators in LDS ([16 px][64 ch],
+// 272-byte row pitch: both the writes and the reads hit 16 distinct bank groups per
+// 16 lanes), reads them back as [pixel][16 consecutive channels] per lane and runs
+// the epilogue on 16-byte vectors: float4 scale / bias, one 16-byte residual load,
+// one 16-byte int8 (or 2 x 16-byte bf16) store.
+constexpr int kEpPitch = 68;  // ints per staged pixel row (64 + 4 pad)
+
+template <int MT>
+__device__ __forceinline__ void i8_epilogue_lds(const I8Args& a, const i32x4v (&acc)[MT][4],
+                                                int mbase, int nbase, int* ep, int lane) {
+  const int M = a.B * a.OH * a.OW;
+  const int r16 = lane & 15, kq = lane >> 4;
+  const int px = lane >> 2, cb = (lane & 3) * 16;
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      *reinterpret_cast<i32x4v*>(ep + r16 * kEpPitch + j * 16 + kq * 4) = acc[i][j];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    i32x4v v[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = *reinterpret_cast<const i32x4v*>(ep + px * kEpPitch + cb + c * 4);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the next group rewrites ep
+    const int m = mbase + i * 16 + px;
+    const int n = nbase + cb;
+    if (m >= M || n >= a.Cout) continue;
+    const int b = m / (a.OH * a.OW);
+    float f[16];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) f[c * 4 + q] = (float)v[c][q];
+    if (n + 16 <= a.Cout && (a.Cout & 15) == 0) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float4 sc = *reinterpret_cast<const float4*>(a.scale + n + c * 4);
+        const float4 bi = *reinterpret_cast<const float4*>(a.bias + n + c * 4);
+        f[c * 4 + 0] = f[c * 4 + 0] * sc.x + bi.x; f[c * 4 + 1] = f[c * 4 + 1] * sc.y + bi.y;
+        f[c * 4 + 2] = f[c * 4 + 2] * sc.z + bi.z; f[c * 4 + 3] = f[c * 4 + 3] * sc.w + bi.w;
+        if (a.img_bias) {
+          const float4 ib = *reinterpret_cast<const float4*>(a.img_bias + (size_t)b * a.Cout + n + c * 4);
+          f[c * 4 + 0] += ib.x; f[c * 4 + 1] += ib.y; f[c * 4 + 2] += ib.z; f[c * 4 + 3] += ib.w;
+        }
+      }
+      if (a.res) {
+        const i32x4v rv = *reinterpret_cast<const i32x4v*>(a.res + (size_t)m * a.Cout + n);
+        const signed char* rb = reinterpret_cast<const signed char*>(&rv);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) f[q] += (float)rb[q] * a.res_scale;
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) f[q] = apply_act(f[q], a.act);
+      const size_t o = (size_t)m * a.ldo + a.co_off + n;
+      if (a.out_mode == 0) {
+        i32x4v pk;
+        signed char* pb = reinterpret_cast<signed char*>(&pk);
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+          pb[q] = (signed char)fminf(fmaxf(rintf(f[q] * a.inv_out_scale), -127.f), 127.f);
+        int8_t* op = static_cast<int8_t*>(a.out) + o;
+        if (((a.ldo | a.co_off) & 15) == 0) {
+          *reinterpret_cast<i32x4v*>(op) = pk;
+        } else {
+          for (int q = 0; q < 16; ++q) op[q] = pb[q];
+        }
+      } else {
+        bf16* op = static_cast<bf16*>(a.out) + o;
+        bf16x8 o0, o1;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) { o0[q] = (bf16)f[q]; o1[q] = (bf16)f[q + 8]; }
+        if (((a.ldo | a.co_off) & 7) == 0) {
+          *reinterpret_cast<bf16x8*>(op) = o0;
+          *reinterpret_cast<bf16x8*>(op + 8) = o1;
+        } else {
+          for (int q = 0; q < 8; ++q) { op[q] = o0[q]; op[q + 8] = o1[q]; }
+        }
+      }
+    } else {  // channel tail (e.g. the 19-class logits)
+      for (int q = 0; q < 16 && n + q < a.Cout; ++q) {
+        float x = f[q] * a.scale[n + q] + a.bias[n + q];
+        if (a.img_bias) x += a.img_bias[(size_t)b * a.Cout + n + q];
+        if (a.res) x += (float)a.res[(size_t)m * a.Cout + n + q] * a.res_scale;
+        x = apply_act(x, a.act);
+        const size_t o = (size_t)m * a.ldo + a.co_off + n + q;
+        if (a.out_mode == 0)
+          static_cast<int8_t*>(a.out)[o] = (signed char)fminf(fmaxf(rintf(x * a.inv_out_scale), -127.f), 127.f);
+        else
+          static_cast<bf16*>(a.out)[o] = (bf16)x;
+      }
+    }
+  }
+}
+
 template <int MT, int NT>
 __global__ __launch_bounds__(256) void conv_i8_kernel(I8Args a) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -92,6 +188,11 @@ __global__ __launch_bounds__(256) void conv_i8_kernel(I8Args a) {
         for (int j = 0; j < NT; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[j], bfr[i], acc[i][j], 0, 0, 0);
     }
+  }
+  if constexpr (NT == 4) {
+    __shared__ __attribute__((aligned(16))) int ep_all[4 * 16 * kEpPitch];
+    i8_epilogue_lds<MT>(a, acc, pix0, ch0, ep_all + wid * 16 * kEpPitch, lane);
+    return;
   }
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
@@ -277,42 +378,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_i8_glds_kernel(I8Args a) {
     }
   }
 
-#pragma unroll
-  for (int i = 0; i < MT; ++i) {
-    const int m = m0 + wm * 16 * MT + i * 16 + r16;
-    if (m >= M) continue;
-    const int b = m / (a.OH * a.OW);
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const int n = n0 + wn * 16 * NT + j * 16 + kq * 4;
-      if (n >= a.Cout) continue;
-      float v[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (n + q >= a.Cout) { v[q] = 0.f; continue; }
-        v[q] = (float)acc[i][j][q] * a.scale[n + q] + a.bias[n + q];
-        if (a.img_bias) v[q] += a.img_bias[(long long)b * a.Cout + n + q];
-        if (a.res) v[q] += (float)a.res[(long long)m * a.Cout + n + q] * a.res_scale;
-        v[q] = apply_act(v[q], a.act);
-      }
-      const long long o = (long long)m * a.ldo + a.co_off + n;
-      if (a.out_mode == 0) {
-        int8_t* op = static_cast<int8_t*>(a.out) + o;
-        signed char qv[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          qv[q] = (signed char)fminf(fmaxf(rintf(v[q] * a.inv_out_scale), -127.f), 127.f);
-        if (n + 3 < a.Cout && ((a.ldo | a.co_off) & 3) == 0) {
-          *reinterpret_cast<char4*>(op) = make_char4(qv[0], qv[1], qv[2], qv[3]);
-        } else {
-          for (int q = 0; q < 4; ++q) if (n + q < a.Cout) op[q] = qv[q];
-        }
-      } else {
-        bf16* op = static_cast<bf16*>(a.out) + o;
-        for (int q = 0; q < 4; ++q) if (n + q < a.Cout) op[q] = (bf16)v[q];
-      }
-    }
-  }
+  static_assert(NT == 4, "conv_i8_glds: the LDS epilogue stages 64-channel wave tiles");
+  __syncthreads();  // every wave is done reading the last stage: reuse it for the epilogue
+  i8_epilogue_lds<MT>(a, acc, m0 + wm * 16 * MT, n0 + wn * 16 * NT,
+                      reinterpret_cast<int*>(smem) + wid * 16 * kEpPitch, lane);
 }
 
 template <int MT, int NT, int WM, int WN>
