@@ -146,6 +146,14 @@ PYBIND11_MODULE(_hip, m) {
                        IH, IW, C, OH, OW, stride, dil, act, S(stream));
         });
 
+  m.def("stem_mfma",
+        [](uintptr_t frames, uintptr_t lut_x, uintptr_t lut_y, uintptr_t w, uintptr_t bias,
+           uintptr_t out, int B, int Hc, int Wc, int H, int W, int OH, int OW, int Cout, int K,
+           int stride, int act, float out_inv_scale, int TY, int TX, uintptr_t stream) {
+          stem_mfma(P<const uint8_t>(frames), P<const int32_t>(lut_x), P<const int32_t>(lut_y),
+                    P<const bf16>(w), P<const float>(bias), P<void>(out), B, Hc, Wc, H, W, OH, OW,
+                    Cout, K, stride, act, out_inv_scale, TY, TX, S(stream));
+        });
   m.def("stem_conv",
         [](uintptr_t frames, uintptr_t lut_x, uintptr_t lut_y, uintptr_t w, uintptr_t bias,
            uintptr_t out, int B, int Hc, int Wc, int H, int W, int OH, int OW, int Cout, int K,

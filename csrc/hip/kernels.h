@@ -173,6 +173,11 @@ void depthwise3x3(const bf16* in, const float* w, const float* bias, bf16* out, 
 // x/127.5 - 1 -> KxK stride-s conv (pad K/2) 3 -> Cout, bias + act, NHWC bf16.
 // w: [K*K*3, Cout] fp32 (tap-major, then input channel).
 // out_inv_scale > 0: int8 output round(v * out_inv_scale) (int8 pipelines).
+// Stem conv on MFMA (TY x TX output tiles): w bf16 [Cout][ceil(K*K/4)*16], K = tap*4 + c.
+void stem_mfma(const uint8_t* frames, const int32_t* lut_x, const int32_t* lut_y, const bf16* w,
+               const float* bias, void* out, int B, int Hc, int Wc, int H, int W, int OH, int OW,
+               int Cout, int K, int stride, int act, float out_inv_scale, int TY, int TX,
+               hipStream_t s);
 void stem_conv(const uint8_t* frames, const int32_t* lut_x, const int32_t* lut_y, const float* w,
                const float* bias, void* out, int B, int Hc, int Wc, int H, int W, int OH, int OW,
                int Cout, int K, int stride, int act, hipStream_t s, float out_inv_scale = 0.f);

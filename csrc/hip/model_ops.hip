@@ -245,6 +245,136 @@ void stem_conv(const uint8_t* frames, const int32_t* lut_x, const int32_t* lut_y
   check_launch("stem_conv");
 }
 
+// ---------------------------------------------------------------- MFMA stem
+// The same conv on v_mfma_f32_16x16x16_bf16 (the dense stem of DeepLabv3-ResNet50:
+// 7x7 s2, 3 -> 64 at 513^2 per frame): a workgroup owns a TY x TX output tile,
+// gathers the letterboxed input region under it ONCE into LDS as bf16 RGB0 pixels
+// (8 bytes: the stem_block0 layout), and every 16 output pixels x 16 channels are
+// KG MFMAs over K = taps x 4 channels (lane kq of MFMA m holds tap 4m + kq: one
+// 8-byte LDS read). The per-lane kernel above re-gathers 49 camera pixels (LUTs +
+// 3 byte loads each) for every output pixel and runs 9.4k fp32 FMAs per pixel.
+typedef short s16x4m __attribute__((ext_vector_type(4)));
+
+struct SMArgs {
+  const uint8_t* frames; const int32_t* lut_x; const int32_t* lut_y;
+  const bf16* w;      // [Cout][KG * 16], K = tap * 4 + c (c = 3 and taps >= K*K zero)
+  const float* bias;  // [Cout]
+  void* out;
+  int B, Hc, Wc, H, W, OH, OW, K, stride, act, TY, TX, tiles_y, tiles_x;
+  float out_inv_scale;  // > 0: int8 output
+};
+
+template <int NSUB, int KG, int GPW>
+__global__ __launch_bounds__(256) void stem_mfma_kernel(SMArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* IN = reinterpret_cast<bf16*>(smem);
+  const int IHT = (a.TY - 1) * a.stride + a.K, IWT = (a.TX - 1) * a.stride + a.K;
+  const int ntile = a.tiles_y * a.tiles_x;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = bid / ntile, t = bid % ntile;
+  const int oy0 = (t / a.tiles_x) * a.TY, ox0 = (t % a.tiles_x) * a.TX;
+  const int iy0 = oy0 * a.stride - a.K / 2, ix0 = ox0 * a.stride - a.K / 2;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+  const float inv_iwt = 1.f / IWT, inv_tx = 1.f / a.TX;
+  const uint8_t* fb = a.frames + (size_t)b * a.Hc * a.Wc * 3;
+  for (int i = tid; i < IHT * IWT; i += 256) {
+    const int ry = (int)(((float)i + 0.5f) * inv_iwt);
+    const int y = iy0 + ry, x = ix0 + (i - ry * IWT);
+    float rgb[3] = {0.f, 0.f, 0.f};  // conv zero padding outside the model input
+    if (y >= 0 && y < a.H && x >= 0 && x < a.W) {
+      const int sy = a.lut_y[y], sx = a.lut_x[x];
+      if (sy >= 0 && sx >= 0) {
+        const uint8_t* px = fb + ((size_t)sy * a.Wc + sx) * 3;
+        rgb[0] = px[2] * (1.f / 127.5f) - 1.f;  // BGR -> RGB
+        rgb[1] = px[1] * (1.f / 127.5f) - 1.f;
+        rgb[2] = px[0] * (1.f / 127.5f) - 1.f;
+      } else {
+        rgb[0] = rgb[1] = rgb[2] = -1.f;  // letterbox padding: uint8 0 -> -1
+      }
+    }
+    const bf16x4 v = {(bf16)rgb[0], (bf16)rgb[1], (bf16)rgb[2], (bf16)0.f};
+    *reinterpret_cast<bf16x4*>(IN + (size_t)i * 4) = v;
+  }
+  s16x4m wf[NSUB][KG];
+  f32x4 bs[NSUB];
+#pragma unroll
+  for (int sub = 0; sub < NSUB; ++sub) {
+#pragma unroll
+    for (int m = 0; m < KG; ++m)
+      wf[sub][m] = *reinterpret_cast<const s16x4m*>(a.w + (size_t)(sub * 16 + r16) * (KG * 16) + m * 16 + kq * 4);
+    bs[sub] = *reinterpret_cast<const f32x4*>(a.bias + sub * 16 + kq * 4);
+  }
+  int toff[KG];
+#pragma unroll
+  for (int m = 0; m < KG; ++m) {
+    const int tp = m * 4 + kq;
+    toff[m] = tp < a.K * a.K ? ((tp / a.K) * IWT + tp % a.K) * 4 : -1;
+  }
+  __syncthreads();
+  const s16x4m zs = {0, 0, 0, 0};
+  const int Cout = NSUB * 16;
+#pragma unroll
+  for (int g = 0; g < GPW; ++g) {
+    const int p = (wid * GPW + g) * 16 + r16;
+    const int py = (int)(((float)p + 0.5f) * inv_tx), px = p - py * a.TX;
+    const int oy = oy0 + py, ox = ox0 + px;
+    const bool valid = p < a.TY * a.TX && oy < a.OH && ox < a.OW;
+    const int base = valid ? (py * a.stride * IWT + px * a.stride) * 4 : 0;
+    s16x4m xf[KG];
+#pragma unroll
+    for (int m = 0; m < KG; ++m)
+      xf[m] = toff[m] >= 0 ? *reinterpret_cast<const s16x4m*>(IN + base + toff[m]) : zs;
+    const size_t pix = ((size_t)b * a.OH + oy) * a.OW + ox;
+#pragma unroll
+    for (int sub = 0; sub < NSUB; ++sub) {
+      f32x4 acc = bs[sub];
+#pragma unroll
+      for (int m = 0; m < KG; ++m) acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wf[sub][m], xf[m], acc, 0, 0, 0);
+      if (!valid) continue;
+      const int n = sub * 16 + kq * 4;
+      if (a.out_inv_scale > 0.f) {
+        char4 o;
+        o.x = (signed char)fminf(fmaxf(rintf(apply_act(acc[0], a.act) * a.out_inv_scale), -127.f), 127.f);
+        o.y = (signed char)fminf(fmaxf(rintf(apply_act(acc[1], a.act) * a.out_inv_scale), -127.f), 127.f);
+        o.z = (signed char)fminf(fmaxf(rintf(apply_act(acc[2], a.act) * a.out_inv_scale), -127.f), 127.f);
+        o.w = (signed char)fminf(fmaxf(rintf(apply_act(acc[3], a.act) * a.out_inv_scale), -127.f), 127.f);
+        *reinterpret_cast<char4*>(static_cast<int8_t*>(a.out) + pix * Cout + n) = o;
+      } else {
+        bf16x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = (bf16)apply_act(acc[q], a.act);
+        *reinterpret_cast<bf16x4*>(static_cast<bf16*>(a.out) + pix * Cout + n) = o;
+      }
+    }
+  }
+}
+
+void stem_mfma(const uint8_t* frames, const int32_t* lut_x, const int32_t* lut_y, const bf16* w,
+               const float* bias, void* out, int B, int Hc, int Wc, int H, int W, int OH, int OW,
+               int Cout, int K, int stride, int act, float out_inv_scale, int TY, int TX,
+               hipStream_t s) {
+  if (TY < 1 || TX < 1 || TY * TX > 256 || TX > 120) throw std::invalid_argument("stem_mfma: bad tile");
+  const int IHT = (TY - 1) * stride + K, IWT = (TX - 1) * stride + K;
+  const size_t lds = (size_t)IHT * IWT * 8;
+  if (lds > 64 * 1024) throw std::invalid_argument("stem_mfma: tile too large");
+  SMArgs a{frames, lut_x, lut_y, w, bias, out, B, Hc, Wc, H, W, OH, OW, K, stride, act, TY, TX,
+           cdiv(OH, TY), cdiv(OW, TX), out_inv_scale};
+  const int grid = B * a.tiles_y * a.tiles_x;
+  const int groups = (TY * TX + 15) / 16;
+  const int kg = (K * K + 3) / 4;
+#define SM(NS, KGV, G) hipLaunchKernelGGL((stem_mfma_kernel<NS, KGV, G>), dim3(grid), dim3(256), lds, s, a)
+  if (Cout == 64 && kg == 13) {
+    if (groups <= 4) SM(4, 13, 1); else if (groups <= 8) SM(4, 13, 2); else SM(4, 13, 4);
+  } else if (Cout == 32 && kg == 3) {
+    if (groups <= 4) SM(2, 3, 1); else if (groups <= 8) SM(2, 3, 2); else SM(2, 3, 4);
+  } else {
+    throw std::invalid_argument("stem_mfma: (Cout, K) must be (64, 7) or (32, 3)");
+  }
+#undef SM
+  check_launch("stem_mfma");
+}
+
 // ---------------------------------------------------------------- max pool
 __global__ void maxpool_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, int B, int IH,
                                int IW, int C, int OH, int OW) {

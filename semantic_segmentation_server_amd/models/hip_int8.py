@@ -107,9 +107,20 @@ class HipDeepLabInt8:
         k, st, c = self.stem_meta
         OH, OW = conv_out_hw(H, W, k, st, 1)
         x = buf("stem", B, OH, OW, c)
-        ops.append(lambda frames, lx, ly, x=x, OH=OH, OW=OW, c=c: K.stem_conv(
+        from .hip_model import Choice
+        stem_variants = [("fp32", [lambda frames, lx, ly, x=x, OH=OH, OW=OW, c=c: K.stem_conv(
             frames, lx, ly, self.stem_w, self.stem_b, x, H=H, W=W, OH=OH, OW=OW, Cout=c, k=k,
-            stride=st, act="relu", out_scale=S["stem"]))
+            stride=st, act="relu", out_scale=S["stem"])])]
+        if (c, k) in ((64, 7), (32, 3)):
+            # the dense stem on bf16 MFMA (int8 out): one LDS-gathered input tile per workgroup
+            wpk = K.pack_stem_mfma(self.stem_w, k, c)
+            bufs["stem_wpk"] = wpk
+            for tile in ((8, 16), (16, 16), (4, 32)):
+                stem_variants.append((f"mfma{tile[0]}x{tile[1]}", [
+                    lambda frames, lx, ly, x=x, OH=OH, OW=OW, c=c, tile=tile, wpk=wpk: K.stem_mfma(
+                        frames, lx, ly, wpk, self.stem_b, x, H=H, W=W, OH=OH, OW=OW, Cout=c, k=k,
+                        stride=st, act="relu", out_scale=S["stem"], tile=tile)]))
+        ops.append(Choice("stem", stem_variants))
         PH, PW = conv_out_hw(OH, OW, 3, 2, 1)
         y = buf("pool0", B, PH, PW, c)
         ops.append(lambda *_, x=x, y=y, OH=OH, OW=OW, PH=PH, PW=PW, c=c: K.maxpool3x3s2_i8(

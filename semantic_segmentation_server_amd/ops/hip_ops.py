@@ -580,6 +580,39 @@ def stem_conv(frames, lut_x, lut_y, w, bias, out, *, H, W, OH, OW, Cout, k, stri
     return out
 
 
+def pack_stem_mfma(w: torch.Tensor, k: int, Cout: int) -> torch.Tensor:
+    """stem_conv weights [k*k*3, Cout] fp32 -> stem_mfma's bf16 [Cout][ceil(k*k/4)*16]
+    (K index = tap * 4 + channel; the 4th channel and the padding taps are zero)."""
+    kg = -(-k * k // 4)
+    wp = torch.zeros(Cout, kg * 4, 4, dtype=torch.float32, device=w.device)
+    wp[:, :k * k, :3] = w.reshape(k * k, 3, Cout).permute(2, 0, 1)
+    return wp.reshape(Cout, kg * 16).to(torch.bfloat16).contiguous()
+
+
+def stem_mfma(frames, lut_x, lut_y, wpk, bias, out, *, H, W, OH, OW, Cout, k, stride, act,
+              out_scale=None, tile=(8, 16)):
+    """stem_conv on MFMA (TY x TX output tiles); wpk from ``pack_stem_mfma``."""
+    B, Hc, Wc, C3 = frames.shape
+    if C3 != 3 or (Cout, k) not in ((64, 7), (32, 3)):
+        raise ValueError("stem_mfma: (Cout, k) must be (64, 7) or (32, 3)")
+    ty, tx = tile
+    if not (ty >= 1 and 1 <= tx <= 120 and ty * tx <= 256):
+        raise ValueError("stem_mfma: tile must hold <= 256 pixels")
+    if ((ty - 1) * stride + k) * ((tx - 1) * stride + k) * 8 > 64 * 1024:
+        raise ValueError("stem_mfma: tile too large")
+    _chk(frames, torch.uint8, "frames")
+    _chk(lut_x, torch.int32, "lut_x", W)
+    _chk(lut_y, torch.int32, "lut_y", H)
+    _chk(wpk, torch.bfloat16, "wpk", Cout * (-(-k * k // 4)) * 16)
+    _chk(bias, torch.float32, "bias", Cout)
+    _chk(out, torch.int8 if out_scale else torch.bfloat16, "out", B * OH * OW * Cout)
+    _hip_mod().stem_mfma(_ptr(frames), _ptr(lut_x), _ptr(lut_y), _ptr(wpk), _ptr(bias), _ptr(out), B,
+                         Hc, Wc, H, W, OH, OW, Cout, k, stride, ACT[act],
+                         1.0 / out_scale if out_scale else 0.0, ty, tx, _stream())
+    _dbg('stem_mfma')
+    return out
+
+
 def conv_i8(x, w8, scale, bias, out, *, B, IH, IW, Cin, OH, OW, Cout, k=1, stride=1, dil=1,
             ldo=None, co_off=0, act=None, res=None, res_scale=0.0, img_bias=None,
             out_scale=None, variant=0) -> torch.Tensor:

@@ -276,11 +276,28 @@ def test_stem_fused_preprocess(cam, k, cout):
     ref = F.relu6(F.conv2d(x, w, b, 2, k // 2))
     OH, OW = ref.shape[-2:]
     out = torch.empty(2, OH, OW, cout, dtype=torch.bfloat16, device=DEV)
+    wk = w.permute(2, 3, 1, 0).reshape(-1, cout).contiguous().to(DEV)
     K.stem_conv(frames.to(DEV), torch.tensor(lx, device=DEV), torch.tensor(ly, device=DEV),
-                w.permute(2, 3, 1, 0).reshape(-1, cout).contiguous().to(DEV), b.to(DEV), out, H=H,
-                W=W, OH=OH, OW=OW, Cout=cout, k=k, stride=2, act="relu6")
+                wk, b.to(DEV), out, H=H, W=W, OH=OH, OW=OW, Cout=cout, k=k, stride=2, act="relu6")
     torch.cuda.synchronize()
     assert _rel(_nchw(out).cpu(), ref) < 1e-2
+    # MFMA stem (bf16 operands): same conv, several tile shapes, bf16 and int8 outputs
+    wpk = K.pack_stem_mfma(wk, k, cout)
+    for tile in ((8, 16), (16, 16), (3, 7)):
+        o2 = torch.full((2, OH, OW, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
+        K.stem_mfma(frames.to(DEV), torch.tensor(lx, device=DEV), torch.tensor(ly, device=DEV), wpk,
+                    b.to(DEV), o2, H=H, W=W, OH=OH, OW=OW, Cout=cout, k=k, stride=2, act="relu6",
+                    tile=tile)
+        torch.cuda.synchronize()
+        assert torch.isfinite(o2.float()).all()
+        assert _rel(_nchw(o2).cpu(), ref) < 2e-2, tile
+    o8 = torch.empty(2, OH, OW, cout, dtype=torch.int8, device=DEV)
+    K.stem_mfma(frames.to(DEV), torch.tensor(lx, device=DEV), torch.tensor(ly, device=DEV), wpk,
+                b.to(DEV), o8, H=H, W=W, OH=OH, OW=OW, Cout=cout, k=k, stride=2, act="relu6",
+                out_scale=0.05)
+    torch.cuda.synchronize()
+    exp = torch.clamp(torch.round(ref / 0.05), -127, 127)
+    assert (_nchw(o8).cpu().float() - exp).abs().float().mean() < 0.5
 
 
 def test_maxpool_gap_matvec():
