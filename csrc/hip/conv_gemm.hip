@@ -478,12 +478,20 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 // One BM x BN output tile (tile index bid in row-major (m-tile, n-tile) order) of
 // the LDS-DMA conv GEMM; shared by the single-conv kernel and the grouped kernel.
-template <int MT, int NT, int ST, int WM, int WN>
+// BK: K depth of one stage (64: 128-byte rows, 8 per glds; 32: 64-byte rows, 16 per
+// glds). BK = 32 halves each stage, so the same LDS holds twice the stages: with
+// ST = 4 three stages of loads stay in flight across every barrier (the deep-K
+// ASPP tiles run at one workgroup per CU, where one stage of lookahead leaves the
+// L2/MALL latency exposed).
+template <int MT, int NT, int ST, int WM, int WN, int BK = 64>
 __device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char* smem) {
   constexpr int NW = WM * WN;                            // waves: WM (pixels) x WN (channels)
-  constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN, ROWB = 128;  // BK = 64 bf16 per stage row
-  constexpr int GA = BM / (8 * NW), GB = BN / (8 * NW);  // glds per thread per stage
-  static_assert(GA * 8 * NW == BM && GB * 8 * NW == BN, "tile rows must split over the waves");
+  constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN, ROWB = BK * 2;  // BK bf16 per stage row
+  constexpr int CPR = ROWB / 16, RPG = 1024 / ROWB;      // 16-B chunks per row, rows per glds
+  constexpr int KS = BK / 32;                            // MFMA k-steps per stage
+  static_assert(BK == 64 || BK == 32, "BK 64 or 32");
+  constexpr int GA = BM / (RPG * NW), GB = BN / (RPG * NW);  // glds per thread per stage
+  static_assert(GA * RPG * NW == BM && GB * RPG * NW == BN, "tile rows must split over the waves");
   constexpr int SB = (BM + BN) * ROWB;
   constexpr int VM_INFLIGHT = (ST - 2) * (GA + GB);
   int* s_tap = reinterpret_cast<int*>(smem + ST * SB);
@@ -500,15 +508,15 @@ __device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char
   const int tn = bid % tiles_n, tm = bid / tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int taps = a.KH * a.KW;
-  const int grow = lane >> 3;        // row inside the 8-row group of one glds
-  const int lc = (lane & 7) ^ grow;  // logical K-chunk this lane fetches
+  const int grow = lane / CPR;                    // row inside the RPG-row group of one glds
+  const int lc = (lane % CPR) ^ (grow % CPR);     // logical K-chunk this lane fetches
 
   int ay[GA], ax[GA], aoff[GA];
   bool av[GA];
   int tapbits = 0;
 #pragma unroll
   for (int i = 0; i < GA; ++i) {
-    const int m = m0 + wid * (BM / NW) + i * 8 + grow;
+    const int m = m0 + wid * (BM / NW) + i * RPG + grow;
     const int pm = m < M ? (a.perm ? a.perm[m] : m) : -1;
     av[i] = pm >= 0;
     const int mm = av[i] ? pm : 0;
@@ -528,7 +536,7 @@ __device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char
   bool bv[GB];
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
-    const int n = n0 + wid * (BN / NW) + j * 8 + grow;
+    const int n = n0 + wid * (BN / NW) + j * RPG + grow;
     bv[j] = n < a.Cout;
     boff[j] = (bv[j] ? n : 0) * taps * a.Cin;
   }
@@ -541,14 +549,14 @@ __device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char
   int ntap = 0;
   for (int t = 0; t < taps; ++t)
     if ((tapmask >> t) & 1) { tl |= (unsigned long long)t << (4 * ntap); ++ntap; }
-  const int cch = cdiv_dev(a.Cin, 64);
+  const int cch = cdiv_dev(a.Cin, BK);
   const int total = ntap * cch;
 
   int is_tap = 0, is_c = 0;  // issue cursor
   auto issue = [&](int stage) {
     const int t = (int)((tl >> (4 * is_tap)) & 15);
     const int dy = (t / a.KW - a.KH / 2) * a.dil, dx = (t % a.KW - a.KW / 2) * a.dil;
-    const int c = is_c * 64 + lc * 8;
+    const int c = is_c * BK + lc * 8;
     const bool cok = c < a.Cin;
     const int doff = (dy * a.IW + dx) * a.Cin + c;
     char* sA = smem + stage * SB;
@@ -557,14 +565,14 @@ __device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char
       const int iy = ay[i] + dy, ix = ax[i] + dx;
       const bool ok = av[i] && cok && iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW;
       const void* src = ok ? (const void*)(a.in + aoff[i] + doff) : (const void*)g_zero_page;
-      __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(sA + (wid * (BM / NW) + i * 8) * ROWB), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(sA + (wid * (BM / NW) + i * RPG) * ROWB), 16, 0, 0);
     }
     char* sB = sA + BM * ROWB;
     const int wofs = t * a.Cin + c;
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
       const void* src = (bv[j] && cok) ? (const void*)(a.w + boff[j] + wofs) : (const void*)g_zero_page;
-      __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(sB + (wid * (BN / NW) + j * 8) * ROWB), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(sB + (wid * (BN / NW) + j * RPG) * ROWB), 16, 0, 0);
     }
     if (++is_c == cch) { is_c = 0; ++is_tap; }
   };
@@ -588,24 +596,28 @@ __device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char
     const char* sA = smem + (k % ST) * SB;
     const char* sB = sA + BM * ROWB;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < KS; ++ks) {
       const int kc = ks * 4 + kq;
       bf16x8 bfr[MT], afr[NT];
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         const int r = wm * 16 * MT + i * 16 + r16;
-        bfr[i] = *reinterpret_cast<const bf16x8*>(sA + r * ROWB + ((kc ^ (r & 7)) << 4));
+        bfr[i] = *reinterpret_cast<const bf16x8*>(sA + r * ROWB + ((kc ^ (r % CPR)) << 4));
       }
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         const int n = wn * 16 * NT + j * 16 + r16;
-        afr[j] = *reinterpret_cast<const bf16x8*>(sB + n * ROWB + ((kc ^ (n & 7)) << 4));
+        afr[j] = *reinterpret_cast<const bf16x8*>(sB + n * ROWB + ((kc ^ (n % CPR)) << 4));
       }
+      // T5: raise this wave's issue priority over the MFMA cluster, so the SIMD's
+      // other wave (2 per SIMD at 8 waves) does not interleave its LDS reads into it
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[j], bfr[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
     }
   }
 
@@ -668,31 +680,32 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(ConvArgs a) {
 // tiles by live-tap work, heaviest first (LPT), so the per-branch grids that left
 // half the CUs idle (137 256x256 tiles of a 34848 x 256 GEMM on 256 CUs) become
 // one balanced grid with no per-branch tail.
-template <int MT, int NT, int ST, int WM = 2, int WN = 2>
+template <int MT, int NT, int ST, int WM = 2, int WN = 2, int BK = 64>
 __global__ __launch_bounds__(64 * WM * WN) void conv_glds_group_kernel(ConvGroupArgs ga) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int e = __builtin_amdgcn_readfirstlane(ga.order[blockIdx.x]);
   const int t = e & 0xffffff;
   switch (e >> 24) {  // constant indices: each arm reads its ConvArgs straight from kernarg
-    case 0: glds_tile<MT, NT, ST, WM, WN>(ga.g[0], t, smem); break;
-    case 1: glds_tile<MT, NT, ST, WM, WN>(ga.g[1], t, smem); break;
-    case 2: glds_tile<MT, NT, ST, WM, WN>(ga.g[2], t, smem); break;
-    default: glds_tile<MT, NT, ST, WM, WN>(ga.g[3], t, smem); break;
+    case 0: glds_tile<MT, NT, ST, WM, WN, BK>(ga.g[0], t, smem); break;
+    case 1: glds_tile<MT, NT, ST, WM, WN, BK>(ga.g[1], t, smem); break;
+    case 2: glds_tile<MT, NT, ST, WM, WN, BK>(ga.g[2], t, smem); break;
+    default: glds_tile<MT, NT, ST, WM, WN, BK>(ga.g[3], t, smem); break;
   }
 }
 
-template <int MT, int NT, int ST, int WM = 2, int WN = 2>
+template <int MT, int NT, int ST, int WM = 2, int WN = 2, int BK = 64>
 static void launch_conv_glds_group(const ConvGroupArgs& ga, int nblocks, hipStream_t s) {
   constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN;
-  const size_t lds = (size_t)ST * (BM + BN) * 128 + 16;
+  const size_t lds = (size_t)ST * (BM + BN) * BK * 2 + 16;
+  static_assert((size_t)ST * (BM + BN) * BK * 2 + 16 <= 160 * 1024, "LDS ring too large");
   static bool attr_set = false;
   if (!attr_set) {
-    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_glds_group_kernel<MT, NT, ST, WM, WN>),
+    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_glds_group_kernel<MT, NT, ST, WM, WN, BK>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
           "conv_glds_group attr");
     attr_set = true;
   }
-  hipLaunchKernelGGL((conv_glds_group_kernel<MT, NT, ST, WM, WN>), dim3(nblocks),
+  hipLaunchKernelGGL((conv_glds_group_kernel<MT, NT, ST, WM, WN, BK>), dim3(nblocks),
                      dim3(64 * WM * WN), lds, s, ga);
   check_launch("conv_glds_group");
 }
@@ -871,7 +884,11 @@ void conv_gemm_grouped(const ConvParams* ps, int n, const int* order, int nblock
     case 8: launch_conv_glds_group<4, 4, 3, 2, 4>(ga, nblocks, s); break;   // 128 x 256, 3 stages
     case 10: launch_conv_glds_group<4, 4, 4, 2, 2>(ga, nblocks, s); break;  // 128 x 128, 4 stages
     case 11: launch_conv_glds_group<4, 4, 2, 2, 2>(ga, nblocks, s); break;  // 128 x 128, 2 stages
-    default: throw std::invalid_argument("conv_gemm_grouped: variant must be 5, 6, 8, 10 or 11");
+    // 32-deep stages, 3 in flight
+    case 12: launch_conv_glds_group<8, 4, 4, 2, 4, 32>(ga, nblocks, s); break;  // 256 x 256
+    case 13: launch_conv_glds_group<4, 4, 4, 2, 4, 32>(ga, nblocks, s); break;  // 128 x 256
+    case 14: launch_conv_glds_group<8, 4, 3, 2, 4, 32>(ga, nblocks, s); break;  // 256 x 256, 3 stages
+    default: throw std::invalid_argument("conv_gemm_grouped: variant must be 5, 6, 8, 10-14");
   }
 }
 

@@ -316,7 +316,7 @@ class HipDeepLab:
             # (conv_gemm_grouped) against the per-branch launches above
             seq = ("separate", ops[aspp_at:])
             grouped = []
-            for gv in (5, 6, 8, 11):
+            for gv in (5, 6, 8, 11, 12, 13, 14):
                 BM = K.GROUP_TILE[gv][0]
                 convs = [dict(x=x, w=b0w, bias=b0b, out=cat, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w,
                               Cout=A, k=1, dil=1, ldo=self.cat_c, co_off=0, act="relu")]
