@@ -26,6 +26,7 @@ class DistContext:
     local_rank: int = 0
     device: torch.device = torch.device("cpu")
     backend: Optional[str] = None
+    cpu_group: Optional[object] = None  # gloo group for host-memory collectives (None: default group)
 
     @property
     def is_root(self) -> bool:
@@ -36,27 +37,44 @@ class DistContext:
         return self.backend is not None
 
 
-def init(backend: Optional[str] = None, timeout_s: float = 300.0) -> DistContext:
-    """Initialise from env. Single process (no WORLD_SIZE) -> no process group."""
+def init(backend: Optional[str] = None, timeout_s: float = 300.0,
+         device: str = "auto") -> DistContext:
+    """Initialise from env. Single process (no WORLD_SIZE) -> no process group.
+
+    ``device``: "auto" (the local GPU unless ``backend`` is gloo), "cuda" (the local
+    GPU whatever the backend: a gloo group driving GPU ranks) or "cpu".
+    ``backend`` (or env SSA_PG_BACKEND): "nccl" (RCCL) or "gloo". The GPU data path
+    only needs RCCL for the frame scatter / device record gather; the default serving
+    and bench path gathers host records over gloo (see DataParallelPipeline)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
-    use_cuda = torch.cuda.is_available() and backend != "gloo"
+    backend = backend or os.environ.get("SSA_PG_BACKEND") or None
+    if device == "auto":
+        use_cuda = torch.cuda.is_available() and backend != "gloo"
+    else:
+        use_cuda = device == "cuda"
     if use_cuda:
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     else:
         device = torch.device("cpu")
-    if world == 1:
+    if world == 1 and os.environ.get("SSA_FORCE_PG", "0") != "1":
         return DistContext(0, 1, 0, device, None)
+    # SSA_FORCE_PG=1: a real (world-size 1) process group, so the single-GPU box can
+    # rehearse the collective path of the multi-GPU run (RCCL streams, gathers)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29561")
     backend = backend or ("nccl" if use_cuda else "gloo")
     kw = {}
     if backend == "nccl":
         kw["device_id"] = device
     dist.init_process_group(backend, rank=rank, world_size=world,
                             timeout=datetime.timedelta(seconds=timeout_s), **kw)
-    return DistContext(rank, world, local, device, backend)
+    # host-memory collectives (the per-step record gather) go over gloo, so the step
+    # loop never enqueues an RCCL kernel beside the compute graphs
+    cpu_group = dist.new_group(backend="gloo") if backend == "nccl" else None
+    return DistContext(rank, world, local, device, backend, cpu_group)
 
 
 def barrier(ctx: DistContext) -> None:

@@ -48,7 +48,14 @@ class DistributedServer:
     def __init__(self, cfg: Config, ctx: Optional[D.DistContext] = None,
                  max_steps: Optional[int] = None):
         self.cfg = cfg
-        self.ctx = ctx or D.init(timeout_s=cfg.rank_timeout)
+        # RCCL only for the rank-0 frame scatter; otherwise a gloo group (records are
+        # gathered from pinned host memory, and an initialised RCCL communicator alone
+        # cost 23% of single-GPU throughput on MI355X -- see bench.py --pg)
+        pg = "nccl" if cfg.ingest == "scatter" else "gloo"
+        import torch
+        self.ctx = ctx or D.init(pg, timeout_s=cfg.rank_timeout,
+                                 device="cuda" if torch.cuda.is_available() and cfg.device != "cpu"
+                                 else "auto")
         self.run_ctx = self.ctx  # == ctx until degraded to rank 0 alone
         self.degraded = False
         self.max_steps = max_steps

@@ -45,7 +45,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, ingest, q, lag=0):
+def _worker(rank, world, port, ingest, q, lag=0, gather="host"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     from semantic_segmentation_server_amd.parallel import dist as D
@@ -54,7 +54,7 @@ def _worker(rank, world, port, ingest, q, lag=0):
     ctx = D.init("gloo")
     B = 2
     hub = ResultHub(world) if ctx.is_root else None
-    pipe = DataParallelPipeline(ctx, FakeEngine(), 8, 6, B, ingest, hub, lag=lag)
+    pipe = DataParallelPipeline(ctx, FakeEngine(), 8, 6, B, ingest, hub, lag=lag, gather=gather)
     if ingest == "scatter":
         nb = B * world if ctx.is_root else B
         frames = torch.zeros(nb, 6, 8, 3, dtype=torch.uint8)
@@ -81,13 +81,16 @@ def _worker(rank, world, port, ingest, q, lag=0):
     D.destroy(ctx)
 
 
-@pytest.mark.parametrize("world,ingest,lag", [(2, "local", 0), (2, "scatter", 0), (3, "scatter", 0),
-                                              (2, "local", 1), (2, "scatter", 1)])
-def test_dp_gather_and_scatter(world, ingest, lag):
+@pytest.mark.parametrize("world,ingest,lag,gather", [
+    (2, "local", 0, "host"), (2, "scatter", 0, "host"), (3, "scatter", 0, "host"),
+    (2, "local", 1, "host"), (2, "scatter", 1, "host"), (2, "local", 1, "rccl"),
+    (3, "scatter", 0, "rccl")])
+def test_dp_gather_and_scatter(world, ingest, lag, gather):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, ingest, q, lag)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, ingest, q, lag, gather))
+             for r in range(world)]
     for p in procs:
         p.start()
     cx, streams, tmax, depth = q.get(timeout=120)
