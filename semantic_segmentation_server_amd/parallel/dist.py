@@ -67,7 +67,11 @@ def init(backend: Optional[str] = None, timeout_s: float = 300.0,
     os.environ.setdefault("MASTER_PORT", "29561")
     backend = backend or ("nccl" if use_cuda else "gloo")
     kw = {}
-    if backend == "nccl":
+    if backend == "nccl" and os.environ.get("SSA_NCCL_EAGER", "0") == "1":
+        # eager communicator init. Off by default: HIP maps streams onto 4 hardware
+        # queues in creation order, and RCCL's streams created before the engine's shift
+        # the compute / result / copy streams onto a worse mapping (world-size-1 rehearsal:
+        # 17.6k frames/s eager vs 21.4k lazy, where the first collective creates them)
         kw["device_id"] = device
     dist.init_process_group(backend, rank=rank, world_size=world,
                             timeout=datetime.timedelta(seconds=timeout_s), **kw)
