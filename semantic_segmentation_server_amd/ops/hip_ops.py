@@ -157,22 +157,44 @@ def _tile_taps(B: int, H: int, W: int, k: int, dil: int, BM: int,
     return sum(((tile >> t) & 1) for t in range(k * k))
 
 
-def grouped_tile_order(convs: List[dict], variant: int, device=None) -> torch.Tensor:
+def grouped_tile_order(convs: List[dict], variant: int, device=None, xcds: int = 1) -> torch.Tensor:
     """Block -> tile table of ``conv_gemm_grouped``: every tile of every conv as
     (group << 24) | tile, heaviest first (work = live taps x 64-channel K chunks;
-    longest-processing-time order, so the short 1x1 / edge tiles fill the tail)."""
+    longest-processing-time order, so the short 1x1 / edge tiles fill the tail).
+
+    ``xcds > 1`` (8 on MI355X): block i runs on XCD i % xcds, so each XCD gets one
+    contiguous run of every conv's row tiles (LPT order inside it) -- a dilated
+    tile's shifted-tap rows belong to its neighbour tiles, which then sit in the
+    same XCD's L2 instead of being fetched from MALL by all eight."""
     BM, BN = GROUP_TILE[variant]
-    ent, cost = [], []
+    ent, cost, part = [], [], []
     for g, c in enumerate(convs):
         tn = -(-c["Cout"] // BN)
         taps = _tile_taps(c["B"], c["OH"], c["OW"], c["k"], c["dil"], BM, c.get("perm"))
         kch = -(-c["Cin"] // 64)
-        for tm in range(taps.numel()):
+        ntm = taps.numel()
+        for tm in range(ntm):
             for n in range(tn):
                 ent.append((g << 24) | (tm * tn + n))
                 cost.append(int(taps[tm]) * kch)
-    idx = sorted(range(len(ent)), key=lambda i: (-cost[i], i))
-    return torch.tensor([ent[i] for i in idx], dtype=torch.int32).to(device).contiguous()
+                part.append(min(xcds - 1, tm * xcds // max(1, ntm)))
+    if xcds <= 1:
+        idx = sorted(range(len(ent)), key=lambda i: (-cost[i], i))
+        return torch.tensor([ent[i] for i in idx], dtype=torch.int32).to(device).contiguous()
+    lists = [sorted((i for i in range(len(ent)) if part[i] == x), key=lambda i: (-cost[i], i))
+             for x in range(xcds)]
+    out, j = [], 0
+    while any(j < len(lst) for lst in lists):
+        for x in range(xcds):  # position 8j + x runs on XCD x
+            if j < len(lists[x]):
+                out.append(ent[lists[x][j]])
+            else:  # this XCD's run is exhausted: lend the slot to the longest remaining run
+                donor = max(range(xcds), key=lambda y: len(lists[y]) - j)
+                if len(lists[donor]) > j + 1:
+                    out.append(ent[lists[donor].pop()])
+        j += 1
+    assert sorted(out) == sorted(ent)
+    return torch.tensor(out, dtype=torch.int32).to(device).contiguous()
 
 
 def conv_gemm_grouped(convs: List[dict], order: torch.Tensor, variant: int = 5) -> None:
