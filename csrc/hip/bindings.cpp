@@ -86,6 +86,7 @@ PYBIND11_MODULE(_hip, m) {
           p.dil = dil; p.TY = TY; p.TX = TX;
           p.wd_h = P<const void>(wd_h); p.bd_h = P<const void>(bd_h); p.wp_h = P<const void>(wp_h);
           p.trace = P<long long>(trace);
+          p.nw = persist == 2 ? 8 : 4;
           if (persist) fused_ir_persist(p, S(stream));
           else fused_inverted_residual(p, S(stream));
         },
@@ -96,7 +97,8 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("TY") = 0, py::arg("TX") = 0, py::arg("wd_h") = 0, py::arg("bd_h") = 0,
         py::arg("wp_h") = 0, py::arg("trace") = 0, py::arg("persist") = 0);
   m.def("fused_ir_tile_lds", &fused_ir_tile_lds);
-  m.def("fused_ir_persist_lds", &fused_ir_persist_lds);
+  m.def("fused_ir_persist_lds", &fused_ir_persist_lds, py::arg("CinP"), py::arg("hidP"), py::arg("Cout"),
+        py::arg("stride"), py::arg("dil"), py::arg("TY"), py::arg("TX"), py::arg("nw") = 4);
   m.def("stem_block0",
         [](uintptr_t frames, uintptr_t lx, uintptr_t ly, uintptr_t ws, uintptr_t bs, uintptr_t wd,
            uintptr_t bd, uintptr_t wp, uintptr_t bp, uintptr_t out, int B, int Hc, int Wc, int H,

@@ -78,9 +78,9 @@ __host__ __device__ inline PLayout playout(int CinP, int hidP, int CoutP, int in
   return l;
 }
 
-template <int NSUB, int KS, int GPW>
-__global__ __launch_bounds__(64 * kPNW) void fused_ir_persist_kernel(PIRArgs a) {
-  constexpr int NT = 64 * kPNW;
+template <int NSUB, int KS, int GPW, int NW>
+__global__ __launch_bounds__(64 * NW) void fused_ir_persist_kernel(PIRArgs a) {
+  constexpr int NT = 64 * NW;
   constexpr int CinP = KS * 32;
   constexpr int XS = CinP + 8, ES = 40, WES = CinP + 8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -162,12 +162,12 @@ __global__ __launch_bounds__(64 * kPNW) void fused_ir_persist_kernel(PIRArgs a) 
   int gip[MAXG], gyx[MAXG];    // halo pixel index; (ty << 16 | tx), ty = 0x7fff for padding lanes
 #pragma unroll
   for (int k = 0; k < MAXG; ++k) {
-    const int ip = (wid + k * kPNW) * 16 + r16;
+    const int ip = (wid + k * NW) * 16 + r16;
     const int ty = ip / TIW;
     gip[k] = ip;
     gyx[k] = ((ip < in_px ? ty : 0x7fff) << 16) | (ip - ty * TIW);
   }
-  const int ngroups_w = (in_groups - wid + kPNW - 1) / kPNW;  // expansion groups this wave owns
+  const int ngroups_w = (in_groups - wid + NW - 1) / NW;  // expansion groups this wave owns
   int pofs[GPW], opy[GPW], opx[GPW];
   bool pin[GPW];
 #pragma unroll
@@ -303,11 +303,11 @@ __global__ __launch_bounds__(64 * kPNW) void fused_ir_persist_kernel(PIRArgs a) 
   }
 }
 
-template <int NSUB, int KS, int GPW>
+template <int NSUB, int KS, int GPW, int NW>
 void launch_persist(const PIRArgs& a, size_t lds, hipStream_t st) {
   static int ncu = 0;
   if (ncu == 0) {
-    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_ir_persist_kernel<NSUB, KS, GPW>),
+    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_ir_persist_kernel<NSUB, KS, GPW, NW>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
           "fused_ir_persist attr");
     int dev = 0;
@@ -318,22 +318,24 @@ void launch_persist(const PIRArgs& a, size_t lds, hipStream_t st) {
   // host work and keeps graph capture valid: nothing here touches the stream)
   int occ = 0;
   check(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ, reinterpret_cast<const void*>(&fused_ir_persist_kernel<NSUB, KS, GPW>), 64 * kPNW, lds),
+            &occ, reinterpret_cast<const void*>(&fused_ir_persist_kernel<NSUB, KS, GPW, NW>), 64 * NW, lds),
         "occupancy");
   occ = occ < 1 ? 1 : occ;
   const int grid = std::min(a.ntiles, ncu * occ);
-  hipLaunchKernelGGL((fused_ir_persist_kernel<NSUB, KS, GPW>), dim3(grid), dim3(64 * kPNW), lds, st, a);
+  hipLaunchKernelGGL((fused_ir_persist_kernel<NSUB, KS, GPW, NW>), dim3(grid), dim3(64 * NW), lds, st, a);
   check_launch("fused_ir_persist");
 }
 
 }  // namespace
 
-size_t fused_ir_persist_lds(int CinP, int hidP, int Cout, int stride, int dil, int TY, int TX) {
+size_t fused_ir_persist_lds(int CinP, int hidP, int Cout, int stride, int dil, int TY, int TX, int nw) {
+  if (nw != 4 && nw != 8) return 0;
   const int TIH = (TY - 1) * stride + 2 * dil + 1, TIW = (TX - 1) * stride + 2 * dil + 1;
   const int in_groups = (TIH * TIW + 15) / 16;
   const int CoutP = (Cout + 15) / 16 * 16;
-  if ((size_t)in_groups * 16 * (CinP / 8) > (size_t)kPXPF * 64 * kPNW) return 0;  // prefetch registers
-  if (in_groups > kPMaxG * kPNW) return 0;                                       // expansion groups per wave
+  if ((size_t)in_groups * 16 * (CinP / 8) > (size_t)kPXPF * 64 * nw) return 0;  // prefetch registers
+  if (in_groups > kPMaxG * nw) return 0;                                       // expansion groups per wave
+  if ((TY * TX + 15) / 16 > 2 * nw) return 0;                                  // output groups per wave
   const int RPE = e_pitch(TX, TIW, stride) * 8;
   return (size_t)playout(CinP, hidP, CoutP, in_groups, TIH * RPE * 2 + 256).total;
 }
@@ -344,9 +346,10 @@ void fused_ir_persist(const FusedIRParams& p, hipStream_t st) {
   if (p.Cin % 8 || p.hidP % 32 || p.CinP % 32 || p.CinP < p.Cin)
     throw std::invalid_argument("fused_ir_persist: bad channel padding");
   if (p.residual && (p.stride != 1 || p.Cin != p.Cout)) throw std::invalid_argument("fused_ir_persist: bad residual");
+  const int nw = p.nw == 8 ? 8 : 4;
   const int groups = (p.TY * p.TX + 15) / 16;
-  const int gpw = (groups + kPNW - 1) / kPNW;
-  const size_t lds = fused_ir_persist_lds(p.CinP, p.hidP, p.Cout, p.stride, p.dil, p.TY, p.TX);
+  const int gpw = (groups + nw - 1) / nw;
+  const size_t lds = fused_ir_persist_lds(p.CinP, p.hidP, p.Cout, p.stride, p.dil, p.TY, p.TX, nw);
   if (gpw > 2 || lds == 0 || lds > 160 * 1024) throw std::invalid_argument("fused_ir_persist: tile / weights too large");
   const int ty_n = cdiv(p.OH, p.TY), tx_n = cdiv(p.OW, p.TX);
   PIRArgs a{p.in, p.we, p.be, reinterpret_cast<const f16*>(p.wd_h), reinterpret_cast<const f16*>(p.bd_h),
@@ -354,10 +357,14 @@ void fused_ir_persist(const FusedIRParams& p, hipStream_t st) {
             p.Cout, (p.Cout + 15) / 16 * 16, p.OH, p.OW, p.stride, p.dil, p.residual, p.TY, p.TX, ty_n,
             tx_n, p.B * ty_n * tx_n};
   const int nsub = (p.Cout + 15) / 16, ks = p.CinP / 32;
-#define PIR(N, K)                                                                        \
-  if (nsub == N && ks == K) {                                                            \
-    if (gpw <= 1) launch_persist<N, K, 1>(a, lds, st); else launch_persist<N, K, 2>(a, lds, st); \
-    return;                                                                              \
+#define PIR(N, K)                                                                          \
+  if (nsub == N && ks == K) {                                                              \
+    if (nw == 8) {                                                                         \
+      if (gpw <= 1) launch_persist<N, K, 1, 8>(a, lds, st); else launch_persist<N, K, 2, 8>(a, lds, st); \
+    } else {                                                                               \
+      if (gpw <= 1) launch_persist<N, K, 1, 4>(a, lds, st); else launch_persist<N, K, 2, 4>(a, lds, st); \
+    }                                                                                      \
+    return;                                                                                \
   }
   PIR(2, 1) PIR(4, 1) PIR(4, 2) PIR(6, 2)
 #undef PIR

@@ -112,13 +112,14 @@ struct FusedIRParams {
   const void* bd_h = nullptr;
   const void* wp_h = nullptr;
   long long* trace = nullptr;  // debug timeline (128 slots), tile kernel only
+  int nw = 4;                  // fused_ir_persist: waves per workgroup (4 or 8)
 };
 void fused_inverted_residual(const FusedIRParams& p, hipStream_t s);
 // Persistent variant of the tile kernel (fused_ir_persist.hip): block weights staged
 // in LDS once per workgroup, next input tile prefetched; same params (TY/TX > 0).
 void fused_ir_persist(const FusedIRParams& p, hipStream_t s);
 // LDS bytes it needs (0: tile too large for the input-tile prefetch registers).
-size_t fused_ir_persist_lds(int CinP, int hidP, int Cout, int stride, int dil, int TY, int TX);
+size_t fused_ir_persist_lds(int CinP, int hidP, int Cout, int stride, int dil, int TY, int TX, int nw = 4);
 // Fused stem (3x3 s2, 3 -> 32, relu6, letterbox gather) + MobileNetV2 block 0
 // (dw 3x3 on 32 ch + relu6, project 32 -> 16); weights: ws [32][32] bf16 with
 // K = (ky*3+kx)*3 + c (RGB), bs [32] f32, wd [9][32] f16, bd [32] f16, wp [16][32] f16, bp [16].

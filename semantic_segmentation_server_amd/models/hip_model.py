@@ -48,7 +48,7 @@ def _pack_dw(layer: ConvBNAct, dev) -> Tuple[torch.Tensor, torch.Tensor]:
             b.contiguous().to(dev, torch.float32))
 
 
-_TILES = [(8, 16), (4, 16), (11, 11), (5, 11), (8, 13), (5, 13)]
+_TILES = [(8, 16), (4, 16), (11, 11), (5, 11), (8, 13), (5, 13), (16, 16), (11, 22)]
 
 
 def _tile_candidates(OH: int, OW: int, CinP: int, stride: int, dil: int,
@@ -494,15 +494,16 @@ class HipDeepLab:
             shape = (-(-s.cout // 16), fp["CinP"] // 32)
             if fp["we"] is not None and shape in K.FUSED_PERSIST_SHAPES:
                 for tile in _TILES:
-                    lds = K.fused_ir_persist_lds(fp["CinP"], fp["hidP"], s.cout, s.stride,
-                                                 s.dilation, *tile)
-                    covered = -(-OH // tile[0]) * tile[0] * -(-OW // tile[1]) * tile[1]
-                    if (0 < lds <= 80 * 1024 and -(-tile[0] * tile[1] // 16) <= 8
-                            and covered <= 1.25 * OH * OW):
-                        variants.insert(0, (f"persist{tile[0]}x{tile[1]}", [
-                            lambda *_, x=inp, out=out, h=h, w=w, OH=OH, OW=OW, tile=tile: K.fused_ir(
-                                x, fp, out, B=B, IH=h, IW=w, OH=OH, OW=OW, tile=tile,
-                                persist=True)]))
+                    for nw in (4, 8):
+                        lds = K.fused_ir_persist_lds(fp["CinP"], fp["hidP"], s.cout, s.stride,
+                                                     s.dilation, *tile, nw)
+                        covered = -(-OH // tile[0]) * tile[0] * -(-OW // tile[1]) * tile[1]
+                        if (0 < lds <= 80 * 1024 and -(-tile[0] * tile[1] // 16) <= 2 * nw
+                                and covered <= 1.25 * OH * OW):
+                            variants.insert(0, (f"persist{tile[0]}x{tile[1]}" + ("w8" if nw == 8 else ""), [
+                                lambda *_, x=inp, out=out, h=h, w=w, OH=OH, OW=OW, tile=tile, nw=nw:
+                                K.fused_ir(x, fp, out, B=B, IH=h, IW=w, OH=OH, OW=OW, tile=tile,
+                                           persist=8 if nw == 8 else True)]))
         if "fused" in blk:
             fp = blk["fused"]
             variants.insert(0, ("fused", [lambda *_, x=inp, out=out, h=h, w=w, OH=OH, OW=OW:

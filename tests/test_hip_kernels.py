@@ -651,8 +651,10 @@ def test_stem_block0_fused(cam, H, tile):
     (24, 24, 1, 1, 41, (11, 11)),    # block 2 shape: residual, Cin 24 -> CinP 32
     (32, 32, 1, 1, 30, (8, 13)),     # blocks 4/5, partial edge tiles
     (32, 16, 1, 1, 37, (8, 16)),     # block 0: no expansion (t = 1)
+    (24, 24, 1, 1, 41, (16, 16)),    # 8-wave persistent tiles
+    (32, 32, 1, 1, 30, (11, 22)),
 ])
-@pytest.mark.parametrize("persist", [False, True])
+@pytest.mark.parametrize("persist", [False, True, 8])
 def test_fused_ir_tile(cin, cout, stride, dil, H, tile, persist):
     from semantic_segmentation_server_amd.models.layers import init_random
     from semantic_segmentation_server_amd.models.mobilenetv2 import InvertedResidual, IRSpec
@@ -680,9 +682,12 @@ def test_fused_ir_tile(cin, cout, stride, dil, H, tile, persist):
     packed = K.pack_fused_ir(ew, eb, dwf[:, 0], dbf, pwf[:, :, 0, 0], pbf, Cin=cin,
                              hid=spec.hidden, Cout=cout, stride=stride, residual=spec.residual,
                              device=DEV, dil=dil)
+    if -(-tile[0] * tile[1] // 16) > 8 and persist is not 8:
+        pytest.skip("tiles over 128 pixels: 8-wave persistent kernel only")
     if persist:
         shape = (-(-cout // 16), packed["CinP"] // 32)
-        lds = K.fused_ir_persist_lds(packed["CinP"], packed["hidP"], cout, stride, dil, *tile)
+        lds = K.fused_ir_persist_lds(packed["CinP"], packed["hidP"], cout, stride, dil, *tile,
+                                     8 if persist is 8 else 4)
         if ew is None or shape not in K.FUSED_PERSIST_SHAPES or not 0 < lds <= 160 * 1024:
             pytest.skip("no persistent instantiation for this block shape")
     out = torch.full((B, OH, OW, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
