@@ -636,15 +636,23 @@ __global__ __launch_bounds__(256) void upsample_argmax_interval_kernel(
     }
   }
   uint8_t* op = labels + ((size_t)b * H + Y) * W;
+  // argmax as a max over index-tagged scores: the low 5 mantissa bits of each score
+  // are replaced by 31 - k, so one max per class (v_max3: two classes per
+  // instruction) carries the winning index along; a tie goes to the lower class as
+  // with a strict compare (for positive scores), and two classes closer than 2^-18
+  // relative may swap (the tests check argmax agreement with torch). Replaces a
+  // compare + two selects per class in this VALU-bound loop.
   auto argmax_at = [&](float lx1) {
     float best = -3.0e38f;
-    int arg = 0;
 #pragma unroll
-    for (int k = 0; k < KP; ++k) {
-      const float v = v0[k] + lx1 * dv[k];
-      if (k < K && v > best) { best = v; arg = k; }
+    for (int k = 0; k < KP; k += 2) {
+      const float va = v0[k] + lx1 * dv[k], vb = v0[k + 1] + lx1 * dv[k + 1];
+      const float ta = __uint_as_float((__float_as_uint(va) & ~31u) | (unsigned)(31 - k));
+      const float tb = __uint_as_float((__float_as_uint(vb) & ~31u) | (unsigned)(30 - k));
+      if (k + 1 < K) best = fmaxf(best, fmaxf(ta, tb));
+      else if (k < K) best = fmaxf(best, ta);
     }
-    return arg;
+    return 31 - (int)(__float_as_uint(best) & 31u);
   };
   // pixels of this interval: X in [xs, xe)
   int xe = xs;
