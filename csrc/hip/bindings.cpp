@@ -248,8 +248,9 @@ PYBIND11_MODULE(_hip, m) {
   });
 
   m.def("upsample_argmax", [](uintptr_t logits, uintptr_t labels, int B, int h, int w, int K,
-                              int ldk, int H, int W, uintptr_t stream) {
-    upsample_argmax(P<const bf16>(logits), P<uint8_t>(labels), B, h, w, K, ldk, H, W, S(stream));
+                              int ldk, int H, int W, uintptr_t stream, int variant) {
+    upsample_argmax(P<const bf16>(logits), P<uint8_t>(labels), B, h, w, K, ldk, H, W, S(stream),
+                    variant);
   });
 
   m.def("post_workspace_bytes", &post_workspace_bytes);

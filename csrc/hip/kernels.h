@@ -201,8 +201,10 @@ void matvec(const float* x, const float* w, const float* bias, float* out, int B
 
 // Bilinear (align_corners=True) upsample of NHWC bf16 logits [B, h, w, ldk]
 // (first K channels valid) to H x W, then per-pixel argmax -> uint8 [B, H, W].
+// variant: 0 default, 1-4 interval kernels (per-lane / row-block x compare / tagged
+// argmax), 5 the direct kernel (see model_ops.hip).
 void upsample_argmax(const bf16* logits, uint8_t* labels, int B, int h, int w, int K, int ldk,
-                     int H, int W, hipStream_t s);
+                     int H, int W, hipStream_t s, int variant = 0);
 
 // ---- post-processing (postprocess.hip) -------------------------------------
 struct PostParams {

@@ -599,7 +599,110 @@ __global__ __launch_bounds__(256) void upsample_argmax_kernel(const bf16* __rest
 // Interpolant v = v_j + lx1 * (v_{j+1} - v_j) with v_c = ly0 * L[y0][c] + ly1 * L[y1][c]:
 // the same bilinear value as torch's align_corners=True in another rounding order
 // (the tests check argmax agreement).
-template <int KP, int PXMAX>
+// Per-lane state of the separable interval upsample: the two vertically interpolated
+// source columns j, j+1 (fp32, as v0 and dv = v1 - v0) of one output row, and the
+// output pixels [xs, xe) whose left source column is j.
+template <int KP>
+struct Interval {
+  float v0[KP], dv[KP];
+  int xs, xe;
+  float sw;
+  int j, w;
+
+  __device__ void load(const bf16* __restrict__ logits, int b, int Y, int jj, int h, int ww, int H,
+                       int W, int ldk) {
+    j = jj;
+    w = ww;
+    const float sh = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
+    sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
+    const float fy = sh * (float)Y;
+    const int y0 = (int)fy;
+    const int yp = y0 < h - 1 ? 1 : 0;
+    const float ly1 = fy - (float)y0, ly0 = 1.f - ly1;
+    // first output column whose left source column is j (exact fp32 formula, then fix-up)
+    xs = sw > 0.f ? (int)((float)j / sw) - 1 : 0;
+    if (xs < 0) xs = 0;
+    while (xs > 0 && (int)(sw * (float)xs) >= j) --xs;
+    while (xs < W && (int)(sw * (float)xs) < j) ++xs;
+    xe = xs;
+    for (int e = 0; e < 32; ++e) {
+      const int X = xs + e;
+      if (X >= W || (int)(sw * (float)X) != j) break;
+      xe = X + 1;
+    }
+    const int j1 = j < w - 1 ? j + 1 : j;
+    const bf16* r0 = logits + ((size_t)(b * h + y0) * w) * ldk;
+    const bf16* r1 = r0 + (size_t)yp * w * ldk;
+#pragma unroll
+    for (int k8 = 0; k8 < KP; k8 += 8) {
+      const bf16x8 a0 = ld8(r0 + (size_t)j * ldk + k8), a1 = ld8(r1 + (size_t)j * ldk + k8);
+      const bf16x8 c0 = ld8(r0 + (size_t)j1 * ldk + k8), c1 = ld8(r1 + (size_t)j1 * ldk + k8);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float u = ly0 * (float)a0[q] + ly1 * (float)a1[q];
+        const float v = ly0 * (float)c0[q] + ly1 * (float)c1[q];
+        v0[k8 + q] = u;
+        dv[k8 + q] = v - u;
+      }
+    }
+  }
+
+  __device__ float lx(int X) const { return j < w - 1 ? sw * (float)X - (float)j : 0.f; }
+
+  // TAGGED: argmax as a max over index-tagged scores (the low 5 mantissa bits of each
+  // score replaced by 31 - k, one v_max per class instead of a compare + two selects;
+  // classes closer than 2^-18 relative may swap). Otherwise a strict-compare argmax
+  // (first maximum wins, as torch.argmax). Measured on MI355X (B=32, 33->513, K=21,
+  // scripts/bench_upsample.py): tagged 57.5 us vs compare 34.4 us per launch, so the
+  // tagged form is kept only as a benchmarked alternative.
+  template <bool TAGGED>
+  __device__ int argmax_at(float lx1, int K) const {
+    float best = -3.0e38f;
+    int arg = 0;
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+      const float v = v0[k] + lx1 * dv[k];
+      if (TAGGED) {
+        const float t = __uint_as_float((__float_as_uint(v) & ~31u) | (unsigned)(31 - k));
+        if (k < K) best = fmaxf(best, t);
+      } else {
+        if (k < K && v > best) { best = v; arg = k; }
+      }
+    }
+    return TAGGED ? 31 - (int)(__float_as_uint(best) & 31u) : arg;
+  }
+
+  // Along the interval every class score is LINEAR in lx1, and the max of linear
+  // functions is convex: when one class wins at both end pixels it wins at every
+  // pixel in between. The common case (smooth logits) then costs two argmaxes
+  // instead of one per pixel (up to 16).
+  template <bool TAGGED>
+  __device__ void emit(uint8_t* op, int K) const {
+    if (xe == xs) return;
+    const int a0 = argmax_at<TAGGED>(lx(xs), K);
+    const int a1 = xe - 1 > xs ? argmax_at<TAGGED>(lx(xe - 1), K) : a0;
+    if (a0 == a1) {
+      for (int X = xs; X < xe; ++X) op[X] = (uint8_t)a0;
+      return;
+    }
+    op[xs] = (uint8_t)a0;
+    op[xe - 1] = (uint8_t)a1;
+    for (int X = xs + 1; X < xe - 1; ++X) op[X] = (uint8_t)argmax_at<TAGGED>(lx(X), K);
+  }
+};
+
+// Separable interval variant (upsampling, K <= 32, ldk % 8 == 0): one lane = one
+// output row x one source interval [j, j+1], i.e. every output pixel X of the row
+// whose left source column (int)(sw * X) is j (16 of them at 33 -> 513). The lane
+// vertically interpolates its two source columns once (16-byte bf16 loads) into
+// fp32 registers (and their difference), after which each output pixel costs one
+// FMA + compare per class: no per-pixel gathers and no register selects (PMC on
+// the direct kernel: 4 x K scalar bf16 loads per pixel made it issue-bound).
+// Interpolant v = v_j + lx1 * (v_{j+1} - v_j) with v_c = ly0 * L[y0][c] + ly1 * L[y1][c]:
+// the same bilinear value as torch's align_corners=True in another rounding order
+// (the tests check argmax agreement). Labels are stored straight from the lane: up to
+// 16 byte stores per lane, 16 bytes apart across the wave.
+template <int KP, bool TAGGED>
 __global__ __launch_bounds__(256) void upsample_argmax_interval_kernel(
     const bf16* __restrict__ logits, uint8_t* __restrict__ labels, int B, int h, int w, int K,
     int ldk, int H, int W) {
@@ -608,95 +711,99 @@ __global__ __launch_bounds__(256) void upsample_argmax_interval_kernel(
   const int j = t % w;
   const int Y = (t / w) % H;
   const int b = t / (w * H);
-  const float sh = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
-  const float sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
-  const float fy = sh * (float)Y;
-  const int y0 = (int)fy;
-  const int yp = y0 < h - 1 ? 1 : 0;
-  const float ly1 = fy - (float)y0, ly0 = 1.f - ly1;
-  // first output column whose left source column is j (exact fp32 formula, then fix-up)
-  int xs = sw > 0.f ? (int)((float)j / sw) - 1 : 0;
-  if (xs < 0) xs = 0;
-  while (xs > 0 && (int)(sw * (float)xs) >= j) --xs;
-  while (xs < W && (int)(sw * (float)xs) < j) ++xs;
-  const int j1 = j < w - 1 ? j + 1 : j;
-  const bf16* r0 = logits + ((size_t)(b * h + y0) * w) * ldk;
-  const bf16* r1 = r0 + (size_t)yp * w * ldk;
-  float v0[KP], dv[KP];
-#pragma unroll
-  for (int k8 = 0; k8 < KP; k8 += 8) {
-    const bf16x8 a0 = ld8(r0 + (size_t)j * ldk + k8), a1 = ld8(r1 + (size_t)j * ldk + k8);
-    const bf16x8 c0 = ld8(r0 + (size_t)j1 * ldk + k8), c1 = ld8(r1 + (size_t)j1 * ldk + k8);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const float u = ly0 * (float)a0[q] + ly1 * (float)a1[q];
-      const float v = ly0 * (float)c0[q] + ly1 * (float)c1[q];
-      v0[k8 + q] = u;
-      dv[k8 + q] = v - u;
-    }
-  }
-  uint8_t* op = labels + ((size_t)b * H + Y) * W;
-  // argmax as a max over index-tagged scores: the low 5 mantissa bits of each score
-  // are replaced by 31 - k, so one max per class (v_max3: two classes per
-  // instruction) carries the winning index along; a tie goes to the lower class as
-  // with a strict compare (for positive scores), and two classes closer than 2^-18
-  // relative may swap (the tests check argmax agreement with torch). Replaces a
-  // compare + two selects per class in this VALU-bound loop.
-  auto argmax_at = [&](float lx1) {
-    float best = -3.0e38f;
-#pragma unroll
-    for (int k = 0; k < KP; k += 2) {
-      const float va = v0[k] + lx1 * dv[k], vb = v0[k + 1] + lx1 * dv[k + 1];
-      const float ta = __uint_as_float((__float_as_uint(va) & ~31u) | (unsigned)(31 - k));
-      const float tb = __uint_as_float((__float_as_uint(vb) & ~31u) | (unsigned)(30 - k));
-      if (k + 1 < K) best = fmaxf(best, fmaxf(ta, tb));
-      else if (k < K) best = fmaxf(best, ta);
-    }
-    return 31 - (int)(__float_as_uint(best) & 31u);
-  };
-  // pixels of this interval: X in [xs, xe)
-  int xe = xs;
-#pragma unroll
-  for (int e = 0; e < PXMAX; ++e) {
-    const int X = xs + e;
-    if (X >= W || (int)(sw * (float)X) != j) break;
-    xe = X + 1;
-  }
-  if (xe == xs) return;
-  // Along the interval every class score is LINEAR in lx1, and the max of linear
-  // functions is convex: when one class wins at both end pixels it wins at every
-  // pixel in between. The common case (smooth logits) then costs two argmaxes
-  // instead of one per pixel (up to 16).
-  const float lxa = j < w - 1 ? sw * (float)xs - (float)j : 0.f;
-  const float lxb = j < w - 1 ? sw * (float)(xe - 1) - (float)j : 0.f;
-  const int a0 = argmax_at(lxa);
-  const int a1 = xe - 1 > xs ? argmax_at(lxb) : a0;
-  if (a0 == a1) {
-    for (int X = xs; X < xe; ++X) op[X] = (uint8_t)a0;
-    return;
-  }
-  op[xs] = (uint8_t)a0;
-  op[xe - 1] = (uint8_t)a1;
-  for (int X = xs + 1; X < xe - 1; ++X) {
-    const float lx1 = j < w - 1 ? sw * (float)X - (float)j : 0.f;
-    op[X] = (uint8_t)argmax_at(lx1);
-  }
+  Interval<KP> iv;
+  iv.load(logits, b, Y, j, h, w, H, W, ldk);
+  iv.template emit<TAGGED>(labels + ((size_t)b * H + Y) * W, K);
 }
 
-void upsample_argmax(const bf16* logits, uint8_t* labels, int B, int h, int w, int K, int ldk,
-                     int H, int W, hipStream_t s) {
-  if (K > 256) throw std::invalid_argument("upsample_argmax: K > 256");
-  // interval path: at most PXMAX output pixels share a left source column
-  const float sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
-  if (K <= 32 && ldk % 8 == 0 && ldk >= ((K + 7) / 8) * 8 && w >= 2 && W > 1 && sw > 0.f &&
-      1.f / sw <= 30.f && (long long)B * H * w < (1LL << 31)) {
-    const long long total = (long long)B * H * w;
-    if (K <= 24)
-      hipLaunchKernelGGL((upsample_argmax_interval_kernel<24, 32>), dim3(cdiv(total, 256)), dim3(256),
-                         0, s, logits, labels, B, h, w, K, ldk, H, W);
+// Row-block variant: a workgroup owns R = 256 / w whole output rows (consecutive in the
+// B*H row space, so one contiguous R*W-byte run of the label buffer). Each lane
+// computes one interval as above into an LDS copy of the rows; the workgroup then
+// writes the run with coalesced dword stores (byte stores only for the unaligned head
+// and tail) instead of 16 scattered byte stores per lane. Measured on MI355X: 38.9 us
+// vs 34.4 us for the per-lane stores (the kernel is not store-bound; the 7-row blocks
+// leave 25 of 256 lanes idle and add a barrier), so the plan autotuner picks between
+// the two per shape.
+template <int KP, bool TAGGED>
+__global__ __launch_bounds__(256) void upsample_argmax_rows_kernel(
+    const bf16* __restrict__ logits, uint8_t* __restrict__ labels, int B, int h, int w, int K,
+    int ldk, int H, int W, int R) {
+  extern __shared__ uint8_t rows_lds[];
+  const int tid = threadIdx.x;
+  const long long g0 = (long long)blockIdx.x * R;  // first global row (b * H + Y)
+  const long long nrows = (long long)B * H;
+  const int nr = (int)(nrows - g0 < R ? nrows - g0 : R);
+  const int r = tid / w, j = tid % w;
+  if (r < nr) {
+    const long long g = g0 + r;
+    Interval<KP> iv;
+    iv.load(logits, (int)(g / H), (int)(g % H), j, h, w, H, W, ldk);
+    iv.template emit<TAGGED>(rows_lds + r * W, K);
+  }
+  __syncthreads();
+  const int n = nr * W;
+  uint8_t* out = labels + g0 * W;
+  const int head = (int)((4 - ((uintptr_t)out & 3)) & 3) < n ? (int)((4 - ((uintptr_t)out & 3)) & 3) : n;
+  if (tid < head) out[tid] = rows_lds[tid];
+  const int nd = (n - head) >> 2;
+  uint32_t* outd = reinterpret_cast<uint32_t*>(out + head);
+  for (int i = tid; i < nd; i += 256) {
+    const uint8_t* q = rows_lds + head + 4 * i;
+    outd[i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+  }
+  const int tail0 = head + 4 * nd;
+  if (tid < n - tail0) out[tail0 + tid] = rows_lds[tail0 + tid];
+}
+
+namespace {
+
+template <int KP>
+void launch_upsample_interval(int variant, const bf16* logits, uint8_t* labels, int B, int h,
+                              int w, int K, int ldk, int H, int W, hipStream_t s) {
+  const long long total = (long long)B * H * w;
+  if (variant == 1 || variant == 2) {
+    if (variant == 1)
+      hipLaunchKernelGGL((upsample_argmax_interval_kernel<KP, false>), dim3(cdiv(total, 256)),
+                         dim3(256), 0, s, logits, labels, B, h, w, K, ldk, H, W);
     else
-      hipLaunchKernelGGL((upsample_argmax_interval_kernel<32, 32>), dim3(cdiv(total, 256)), dim3(256),
-                         0, s, logits, labels, B, h, w, K, ldk, H, W);
+      hipLaunchKernelGGL((upsample_argmax_interval_kernel<KP, true>), dim3(cdiv(total, 256)),
+                         dim3(256), 0, s, logits, labels, B, h, w, K, ldk, H, W);
+    return;
+  }
+  const int R = 256 / w;
+  const long long nrows = (long long)B * H;
+  const size_t lds = (size_t)R * W;
+  if (variant == 3)
+    hipLaunchKernelGGL((upsample_argmax_rows_kernel<KP, false>), dim3(cdiv(nrows, R)), dim3(256),
+                       lds, s, logits, labels, B, h, w, K, ldk, H, W, R);
+  else
+    hipLaunchKernelGGL((upsample_argmax_rows_kernel<KP, true>), dim3(cdiv(nrows, R)), dim3(256),
+                       lds, s, logits, labels, B, h, w, K, ldk, H, W, R);
+}
+
+}  // namespace
+
+// variant: 0 = default (per-lane interval, strict-compare argmax), 1 = interval / compare,
+// 2 = interval / tagged max, 3 = row-block / compare, 4 = row-block / tagged max,
+// 5 = the direct (per-pixel gather) kernel. Variants 1-4 need the interval
+// preconditions; otherwise the direct kernel runs.
+void upsample_argmax(const bf16* logits, uint8_t* labels, int B, int h, int w, int K, int ldk,
+                     int H, int W, hipStream_t s, int variant) {
+  if (K > 256) throw std::invalid_argument("upsample_argmax: K > 256");
+  if (variant < 0 || variant > 5) throw std::invalid_argument("upsample_argmax: bad variant");
+  if (variant == 0) variant = 1;
+  // interval path: at most 32 output pixels share a left source column; the row-block
+  // variant needs a whole row of intervals in one workgroup and R * W bytes of LDS
+  const float sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
+  const bool interval = K <= 32 && ldk % 8 == 0 && ldk >= ((K + 7) / 8) * 8 && w >= 2 && W > 1 &&
+                        sw > 0.f && 1.f / sw <= 30.f && (long long)B * H * w < (1LL << 31);
+  if (interval && (variant == 3 || variant == 4) && (w > 256 || (256 / w) * W > 65536))
+    variant -= 2;
+  if (interval && variant != 5) {
+    if (K <= 24)
+      launch_upsample_interval<24>(variant, logits, labels, B, h, w, K, ldk, H, W, s);
+    else
+      launch_upsample_interval<32>(variant, logits, labels, B, h, w, K, ldk, H, W, s);
     check_launch("upsample_argmax interval");
     return;
   }

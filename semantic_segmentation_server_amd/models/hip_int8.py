@@ -161,7 +161,8 @@ class HipDeepLabInt8:
             Cout=self.num_classes, ldo=self.ldk, act=None))
         labels = buf("labels", B, H, W, dtype=torch.uint8)
         ops.append(lambda *_, h=h, w=w: K.upsample_argmax(
-            logits, labels, B=B, h=h, w=w, K=self.num_classes, ldk=self.ldk, H=H, W=W))
+            logits, labels, B=B, h=h, w=w, K=self.num_classes, ldk=self.ldk, H=H, W=W,
+            variant=K.UPSAMPLE_VARIANTS["lane"]))
         self._plans[key] = (ops, bufs)
         self._autotune(ops, B, Hc, Wc)
         return self._plans[key]

@@ -368,9 +368,11 @@ class HipDeepLab:
         labels = buf("labels", B, H, W, dtype=torch.uint8)
         # labels_out (segment's out=): write the label maps straight into a caller
         # buffer (the engine's per-slot maps) instead of the plan's static one
-        ops.append(lambda *_, h=h, w=w: K.upsample_argmax(
+        # upsample + argmax: row-block (LDS-staged, coalesced stores) or per-lane stores
+        ops.append(Choice("upsample", [(name, [lambda *_, h=h, w=w, v=K.UPSAMPLE_VARIANTS[name]:
+                                               K.upsample_argmax(
             logits, self._labels_out if self._labels_out is not None else labels, B=B, h=h, w=w,
-            K=self.num_classes, ldk=self.ldk, H=H, W=W))
+            K=self.num_classes, ldk=self.ldk, H=H, W=W, variant=v)]) for name in ("rows", "lane")]))
         self._plans[key] = (ops, bufs)
         self._autotune(ops, B, Hc, Wc)
         return self._plans[key]

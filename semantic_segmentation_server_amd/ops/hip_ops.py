@@ -717,12 +717,20 @@ def matvec(x, w, bias, out, *, B, N, K, act=None):
     return out
 
 
-def upsample_argmax(logits, labels, *, B, h, w, K, ldk, H, W):
+UPSAMPLE_VARIANTS = {"rows": 3, "rows_tag": 4, "lane": 1, "lane_tag": 2, "direct": 5}
+
+
+def upsample_argmax(logits, labels, *, B, h, w, K, ldk, H, W, variant: int = 0):
+    """Bilinear (align_corners) upsample of [B, h, w, ldk] logits + per-pixel argmax
+    into uint8 [B, H, W] labels. ``variant``: 0 default or a ``UPSAMPLE_VARIANTS`` id."""
     _chk(logits, torch.bfloat16, "logits", B * h * w * ldk)
     _chk(labels, torch.uint8, "labels", B * H * W)
     if K > ldk:
         raise ValueError("K > ldk")
-    _hip_mod().upsample_argmax(_ptr(logits), _ptr(labels), B, h, w, K, ldk, H, W, _stream())
+    if not 0 <= variant <= 5:
+        raise ValueError(f"bad upsample variant {variant}")
+    _hip_mod().upsample_argmax(_ptr(logits), _ptr(labels), B, h, w, K, ldk, H, W, _stream(),
+                               variant)
     _dbg('upsample_argmax')
     return labels
 

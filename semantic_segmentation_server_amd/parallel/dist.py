@@ -55,6 +55,10 @@ def init(backend: Optional[str] = None, timeout_s: float = 300.0,
     else:
         use_cuda = device == "cuda"
     if use_cuda:
+        if os.environ.get("SSA_SHARE_GPU", "0") == "1":
+            # rehearsal knob: several ranks on one GPU (a 1-GPU box running the
+            # multi-rank bench / server path over a gloo group); RCCL refuses this
+            local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     else:

@@ -322,8 +322,9 @@ def test_maxpool_gap_matvec():
     assert torch.allclose(mv.cpu(), F.relu(gref @ wm.t() + bm), atol=1e-3)
 
 
-@pytest.mark.parametrize("h,H,K", [(33, 513, 21), (65, 1025, 19), (9, 65, 21)])
-def test_upsample_argmax(h, H, K):
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("h,H,K", [(33, 513, 21), (65, 1025, 19), (9, 65, 21), (33, 257, 30)])
+def test_upsample_argmax(h, H, K, variant):
     from semantic_segmentation_server_amd.ops import reference_ops as R
     Kh = _hip()
     g = torch.Generator().manual_seed(7)
@@ -332,7 +333,8 @@ def test_upsample_argmax(h, H, K):
     logits = torch.randn(B, h, h, ldk, generator=g).to(torch.bfloat16)
     ref = R.upsample_argmax(_nchw(logits[..., :K]).float(), H, H)
     out = torch.empty(B, H, H, dtype=torch.uint8, device=DEV)
-    Kh.upsample_argmax(logits.to(DEV), out, B=B, h=h, w=h, K=K, ldk=ldk, H=H, W=H)
+    Kh.upsample_argmax(logits.to(DEV), out, B=B, h=h, w=h, K=K, ldk=ldk, H=H, W=H,
+                       variant=variant)
     torch.cuda.synchronize()
     agree = (out.cpu() == ref).float().mean().item()
     assert agree > 0.9999, agree
