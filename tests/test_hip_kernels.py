@@ -684,12 +684,12 @@ def test_fused_ir_tile(cin, cout, stride, dil, H, tile, persist):
     packed = K.pack_fused_ir(ew, eb, dwf[:, 0], dbf, pwf[:, :, 0, 0], pbf, Cin=cin,
                              hid=spec.hidden, Cout=cout, stride=stride, residual=spec.residual,
                              device=DEV, dil=dil)
-    if -(-tile[0] * tile[1] // 16) > 8 and persist is not 8:
+    if -(-tile[0] * tile[1] // 16) > 8 and persist != 8:
         pytest.skip("tiles over 128 pixels: 8-wave persistent kernel only")
     if persist:
         shape = (-(-cout // 16), packed["CinP"] // 32)
         lds = K.fused_ir_persist_lds(packed["CinP"], packed["hidP"], cout, stride, dil, *tile,
-                                     8 if persist is 8 else 4)
+                                     8 if persist == 8 else 4)
         if ew is None or shape not in K.FUSED_PERSIST_SHAPES or not 0 < lds <= 160 * 1024:
             pytest.skip("no persistent instantiation for this block shape")
     out = torch.full((B, OH, OW, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
