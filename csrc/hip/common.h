@@ -53,6 +53,56 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
 
 __host__ __device__ __forceinline__ int cdiv_dev(int a, int b) { return (a + b - 1) / b; }
 
+// Letterboxed camera pixels of an IHT x IWT model-input window at (iy0, ix0) ->
+// LDS as normalised bf16 RGB0 (x / 127.5 - 1, BGR -> RGB; -1 for letterbox
+// padding, 0 outside the H x W model input = conv zero padding). Model pixel
+// (y, x) is camera pixel (lut_y[y], lut_x[x]), -1 = padding. Each pixel is a
+// dependent chain (LUT load -> pixel load) and the stems are latency-bound here,
+// so every lane batches GU pixels: all LUT loads, then all pixel loads, then all
+// LDS stores (GU chains in flight instead of one).
+template <int GU, int NT>
+__device__ __forceinline__ void gather_letterbox_rgb0(bf16* IN, const uint8_t* fb, const int32_t* lut_x,
+                                                      const int32_t* lut_y, int Wc, int H, int W, int iy0,
+                                                      int ix0, int IHT, int IWT, int tid) {
+  const int n_in = IHT * IWT;
+  const float inv_iwt = 1.f / IWT;
+  for (int i0 = tid; i0 < n_in; i0 += NT * GU) {
+    int sidx[GU];  // >= 0: camera byte offset; -1: letterbox padding; -2: conv zero padding
+#pragma unroll
+    for (int u = 0; u < GU; ++u) {
+      const int i = i0 + u * NT;
+      const int ry = (int)(((float)i + 0.5f) * inv_iwt);  // i / IWT (i < 2^14)
+      const int y = iy0 + ry, x = ix0 + (i - ry * IWT);
+      sidx[u] = -2;
+      if (i < n_in && y >= 0 && y < H && x >= 0 && x < W) {
+        const int sy = lut_y[y], sx = lut_x[x];
+        sidx[u] = (sy >= 0 && sx >= 0) ? (sy * Wc + sx) * 3 : -1;
+      }
+    }
+    uint8_t pb[GU][3];
+#pragma unroll
+    for (int u = 0; u < GU; ++u) {
+      const uint8_t* px = fb + (sidx[u] >= 0 ? sidx[u] : 0);
+      pb[u][0] = px[0]; pb[u][1] = px[1]; pb[u][2] = px[2];
+    }
+#pragma unroll
+    for (int u = 0; u < GU; ++u) {
+      const int i = i0 + u * NT;
+      if (i >= n_in) break;
+      float rgb[3] = {0.f, 0.f, 0.f};
+      if (sidx[u] >= 0) {
+        rgb[0] = pb[u][2] * (1.f / 127.5f) - 1.f;
+        rgb[1] = pb[u][1] * (1.f / 127.5f) - 1.f;
+        rgb[2] = pb[u][0] * (1.f / 127.5f) - 1.f;
+      } else if (sidx[u] == -1) {
+        rgb[0] = rgb[1] = rgb[2] = -1.f;
+      }
+      const bf16x4 v = {(bf16)rgb[0], (bf16)rgb[1], (bf16)rgb[2], (bf16)0.f};
+      *reinterpret_cast<bf16x4*>(IN + (size_t)i * 4) = v;
+    }
+  }
+}
+
 inline void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }

@@ -487,50 +487,10 @@ __global__ __launch_bounds__(256) void stem_block0_kernel(SB0Args a) {
   const int iy0 = 2 * sy0 - 1, ix0 = 2 * sx0 - 1;   // input region origin
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int r16 = lane & 15, kq = lane >> 4;
-  const float inv_iwt = 1.f / IWT, inv_swt = 1.f / SWT, inv_tx = 1.f / a.TX;
+  const float inv_swt = 1.f / SWT, inv_tx = 1.f / a.TX;
 
   const uint8_t* fb = a.frames + (size_t)b * a.Hc * a.Wc * 3;
-  // The gather is a dependent chain (LUT load -> pixel load) per input pixel; the
-  // workgroup is latency-bound here, so GU pixels per lane are gathered as one batch:
-  // all LUT loads, then all pixel loads, then all LDS stores (GU chains in flight
-  // instead of one).
-  constexpr int GU = 6;
-  const int n_in = IHT * IWT;
-  for (int i0 = tid; i0 < n_in; i0 += 256 * GU) {
-    int sidx[GU];  // >= 0: camera pixel offset; -1: letterbox padding; -2: conv zero padding
-#pragma unroll
-    for (int u = 0; u < GU; ++u) {
-      const int i = i0 + u * 256;
-      const int ry = sdiv(i, inv_iwt);
-      const int y = iy0 + ry, x = ix0 + (i - ry * IWT);
-      sidx[u] = -2;
-      if (i < n_in && y >= 0 && y < a.H && x >= 0 && x < a.W) {
-        const int sy = a.lut_y[y], sx = a.lut_x[x];
-        sidx[u] = (sy >= 0 && sx >= 0) ? (sy * a.Wc + sx) * 3 : -1;
-      }
-    }
-    uint8_t pb[GU][3];
-#pragma unroll
-    for (int u = 0; u < GU; ++u) {
-      const uint8_t* px = fb + (sidx[u] >= 0 ? sidx[u] : 0);
-      pb[u][0] = px[0]; pb[u][1] = px[1]; pb[u][2] = px[2];
-    }
-#pragma unroll
-    for (int u = 0; u < GU; ++u) {
-      const int i = i0 + u * 256;
-      if (i >= n_in) break;
-      float rgb[3] = {0.f, 0.f, 0.f};  // conv zero padding outside the model input
-      if (sidx[u] >= 0) {
-        rgb[0] = pb[u][2] * (1.f / 127.5f) - 1.f;  // BGR -> RGB
-        rgb[1] = pb[u][1] * (1.f / 127.5f) - 1.f;
-        rgb[2] = pb[u][0] * (1.f / 127.5f) - 1.f;
-      } else if (sidx[u] == -1) {
-        rgb[0] = rgb[1] = rgb[2] = -1.f;  // letterbox padding: uint8 0 -> -1
-      }
-      bf16x4 v = {(bf16)rgb[0], (bf16)rgb[1], (bf16)rgb[2], (bf16)0.f};
-      *reinterpret_cast<bf16x4*>(IN + (size_t)i * 4) = v;
-    }
-  }
+  gather_letterbox_rgb0<6, 256>(IN, fb, a.lut_x, a.lut_y, a.Wc, a.H, a.W, iy0, ix0, IHT, IWT, tid);
   // Stem conv on v_mfma_f32_16x16x16_bf16: K = 12 taps x 4 channels (RGB + the zero
   // 4th channel of IN, taps 9..11 zero) in 3 MFMAs; lane kq of MFMA m holds tap
   // 4m + kq, i.e. ONE 8-byte LDS read of the pixel's 4 channels (no per-element

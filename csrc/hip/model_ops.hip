@@ -276,26 +276,9 @@ __global__ __launch_bounds__(256) void stem_mfma_kernel(SMArgs a) {
   const int iy0 = oy0 * a.stride - a.K / 2, ix0 = ox0 * a.stride - a.K / 2;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int r16 = lane & 15, kq = lane >> 4;
-  const float inv_iwt = 1.f / IWT, inv_tx = 1.f / a.TX;
+  const float inv_tx = 1.f / a.TX;
   const uint8_t* fb = a.frames + (size_t)b * a.Hc * a.Wc * 3;
-  for (int i = tid; i < IHT * IWT; i += 256) {
-    const int ry = (int)(((float)i + 0.5f) * inv_iwt);
-    const int y = iy0 + ry, x = ix0 + (i - ry * IWT);
-    float rgb[3] = {0.f, 0.f, 0.f};  // conv zero padding outside the model input
-    if (y >= 0 && y < a.H && x >= 0 && x < a.W) {
-      const int sy = a.lut_y[y], sx = a.lut_x[x];
-      if (sy >= 0 && sx >= 0) {
-        const uint8_t* px = fb + ((size_t)sy * a.Wc + sx) * 3;
-        rgb[0] = px[2] * (1.f / 127.5f) - 1.f;  // BGR -> RGB
-        rgb[1] = px[1] * (1.f / 127.5f) - 1.f;
-        rgb[2] = px[0] * (1.f / 127.5f) - 1.f;
-      } else {
-        rgb[0] = rgb[1] = rgb[2] = -1.f;  // letterbox padding: uint8 0 -> -1
-      }
-    }
-    const bf16x4 v = {(bf16)rgb[0], (bf16)rgb[1], (bf16)rgb[2], (bf16)0.f};
-    *reinterpret_cast<bf16x4*>(IN + (size_t)i * 4) = v;
-  }
+  gather_letterbox_rgb0<6, 256>(IN, fb, a.lut_x, a.lut_y, a.Wc, a.H, a.W, iy0, ix0, IHT, IWT, tid);
   s16x4m wf[NSUB][KG];
   f32x4 bs[NSUB];
 #pragma unroll
