@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import argparse
 import dataclasses
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -68,6 +69,7 @@ class Config:
     degrade: bool = True                   # rank 0 keeps serving alone when a peer rank is lost
     debug_dump: Optional[str] = None       # directory for annotated PNG frames (reference :196-205)
     debug_every: int = 0                   # dump every N-th frame (0 = off)
+    debug_sync: bool = False               # HIP_LAUNCH_BLOCKING=1, eager launches
 
     @property
     def min_area(self) -> float:
@@ -135,7 +137,20 @@ def add_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--debug_dump", default=d.debug_dump,
                    help="write annotated PNG frames here (contours, centroids, labels)")
     p.add_argument("--debug_every", type=int, default=d.debug_every)
+    p.add_argument("--debug_sync", action="store_true",
+                   help="synchronous kernel launches (HIP_LAUNCH_BLOCKING=1, no hipGraph) so a "
+                        "faulting kernel is reported at its own launch")
     return p
+
+
+def apply_debug_env(cfg: Config) -> Config:
+    """--debug_sync: must run before anything initialises the HIP runtime (the
+    variable is read once, at runtime init). hipGraph capture is turned off too:
+    a graph replays its kernels as one submission, which would hide the culprit."""
+    if cfg.debug_sync:
+        os.environ["HIP_LAUNCH_BLOCKING"] = "1"
+        cfg = dataclasses.replace(cfg, graph=False)
+    return cfg
 
 
 def from_args(args: argparse.Namespace) -> Config:

@@ -89,7 +89,7 @@ class Server:
 
 
 def main(argv=None) -> int:
-    cfg = C.parse(argv)
+    cfg = C.apply_debug_env(C.parse(argv))
     logging.basicConfig(level=getattr(logging, cfg.log_level.upper(), logging.INFO),
                         format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     if cfg.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:

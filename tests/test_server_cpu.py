@@ -1,4 +1,5 @@
 """T5: config-1 plumbing — CPU engine + producer + gRPC loopback (no GPU)."""
+import os
 import time
 
 import grpc
@@ -93,3 +94,14 @@ def test_debug_dump_writes_annotated_png(tmp_path):
     files = sorted(p.name for p in tmp_path.iterdir())
     assert files == ["s003_f00000007.png"]
     assert Image.open(tmp_path / files[0]).size[0] > 0
+
+
+def test_debug_sync_sets_launch_blocking_and_disables_graphs(monkeypatch):
+    """--debug_sync: HIP_LAUNCH_BLOCKING=1 before runtime init, eager launches."""
+    from semantic_segmentation_server_amd import config as C
+    monkeypatch.delenv("HIP_LAUNCH_BLOCKING", raising=False)
+    cfg = C.apply_debug_env(C.parse([]))
+    assert cfg.graph and "HIP_LAUNCH_BLOCKING" not in os.environ
+    cfg = C.apply_debug_env(C.parse(["--debug_sync"]))
+    assert cfg.debug_sync and not cfg.graph
+    assert os.environ["HIP_LAUNCH_BLOCKING"] == "1"
