@@ -39,6 +39,6 @@ for i in range(n):
     d = {}
     for s in steps:
         d.update({k: v for k, v in s[i].items()})
-    nm = d["name"].split("(")[0].replace("void ", "").replace("ssa::", "").replace("(anonymous namespace)::", "")[:32]
+    nm = d["name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("ssa::", "")[:32]
     print(f"{i:3d} {nm:32s} {d['grid']:7d} {d['lds']:6d} {d['vgpr']:3d}/{d['agpr']:<3d} " +
           " ".join(f"{d.get(k, float('nan')):14.4g}" for k in keys))
