@@ -120,6 +120,23 @@ void fused_inverted_residual(const FusedIRParams& p, hipStream_t s);
 void fused_ir_persist(const FusedIRParams& p, hipStream_t s);
 // LDS bytes it needs (0: tile too large for the input-tile prefetch registers).
 size_t fused_ir_persist_lds(int CinP, int hidP, int Cout, int stride, int dil, int TY, int TX, int nw = 4);
+// Fused inverted residual over raster spans (fused_ir_span.hip): stride 1, dilation
+// 1-7, Cin % 32 == 0, Cout % 16 == 0. w: host-packed chunk images (hip_ops.pack_fused_span),
+// table: span/halo table (hip_ops.span_table) of S spans, hstride ints each.
+struct FusedSpanParams {
+  const bf16* in = nullptr;   // [B, H, W, Cin]
+  const void* w = nullptr;    // [hidP / 32][(2*Cin/32 + Cout/16 + 1) KiB]
+  const float* bp = nullptr;  // [Cout]
+  const int* table = nullptr;
+  bf16* out = nullptr;        // [B, H, W, Cout]
+  int B = 0, H = 0, W = 0, Cin = 0, hidP = 0, Cout = 0, dil = 1, residual = 0;
+  int S = 8, WR = 0, WCP = 0, hstride = 0;
+  int npi = 4, xg = 2;        // pixel-group wave sets; halo groups per wave (instantiation)
+  int xslots = 0;             // halo groups beyond 16 (their X lives in LDS; xg == 3 only)
+  long long* trace = nullptr; // debug s_memtime timeline [B*S][2][64]
+};
+void fused_ir_span(const FusedSpanParams& p, hipStream_t s);
+size_t fused_ir_span_lds(int Cin, int Cout, int WR, int WCP, int xslots);
 // Fused stem (3x3 s2, 3 -> 32, relu6, letterbox gather) + MobileNetV2 block 0
 // (dw 3x3 on 32 ch + relu6, project 32 -> 16); weights: ws [32][32] bf16 with
 // K = (ky*3+kx)*3 + c (RGB), bs [32] f32, wd [9][32] f16, bd [32] f16, wp [16][32] f16, bp [16].

@@ -1,0 +1,80 @@
+"""Microbenchmark + s_memtime phase timeline of the fused span kernel on the 33x33
+blocks of DeepLabv3-MobileNetV2 (B = 32, random data and weights).
+
+  python scripts/bench_span.py [--B 32] [--trace]
+"""
+import argparse
+import sys
+
+import numpy as np
+import torch
+
+import os  # noqa: E402
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, _ROOT)
+sys.path.insert(0, os.path.join(_ROOT, "tests"))
+from semantic_segmentation_server_amd.ops import fused_span as FS  # noqa: E402
+from test_fused_span_cpu import _block, pack_block  # noqa: E402
+
+BLOCKS = [(7, 64, 64, 1), (10, 64, 96, 1), (11, 96, 96, 1), (13, 96, 160, 1), (14, 160, 160, 2),
+          (16, 160, 320, 2)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=32)
+    ap.add_argument("--H", type=int, default=33)
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--trace", action="store_true")
+    ap.add_argument("--only", type=int, default=0, help="run only this block index")
+    ap.add_argument("--S", type=int, default=0, help="run only this span count")
+    a = ap.parse_args()
+    dev = "cuda"
+    B, H = a.B, a.H
+    for idx, cin, cout, dil in BLOCKS:
+        if a.only and idx != a.only:
+            continue
+        blk, spec = _block(cin, cout, dil, seed=idx)
+        packed = pack_block(blk, spec, device=dev)
+        x = torch.randn(B, H, H, cin, device=dev).to(torch.bfloat16)
+        out = torch.empty(B, H, H, cout, device=dev, dtype=torch.bfloat16)
+        flop = 2 * B * H * H * (cin * spec.hidden + spec.hidden * cout + 9 * spec.hidden)
+        for S in ((a.S,) if a.S else (8, 16)):
+            try:
+                tab = FS.span_table(H, H, S, dil, dev)
+            except ValueError:
+                continue
+            for npi in FS.span_npi_options(cout):
+                run = lambda: FS.fused_ir_span(x, packed, tab, out, B=B, residual=spec.residual, npi=npi)
+                for _ in range(3):
+                    run()
+                st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                st.record()
+                for _ in range(a.reps):
+                    run()
+                en.record()
+                en.synchronize()
+                us = st.elapsed_time(en) / a.reps * 1e3
+                print(f"block{idx:2d} {cin:3d}->{spec.hidden:3d}->{cout:3d} d{dil} S={S:2d} npi={npi}: "
+                      f"{us:7.1f} us  {flop / us / 1e6:7.1f} TFLOP/s  (xg={tab['xg']}, nh_max={tab['nh_max']})",
+                      flush=True)
+                if a.trace:
+                    tr = torch.zeros(B * S * 2 * 64, dtype=torch.int64, device=dev)
+                    FS.fused_ir_span(x, packed, tab, out, B=B, residual=spec.residual, npi=npi, trace=tr)
+                    torch.cuda.synchronize()
+                    t = tr.view(B * S, 2, 64).cpu().numpy().astype(np.int64)
+                    NC = packed["hidP"] // 32
+                    for w in (0, 1):
+                        tt = t[:, w]
+                        pro = np.median(tt[:, 2] - tt[:, 0])
+                        steps = min(NC + 2, 12)
+                        # per step: [C], [A], [B], staging, barrier (stamps 3..7 + 5t; 2 = loop entry)
+                        ph = np.array([[np.median(tt[:, 3 + 5 * k + i] - tt[:, 2 + 5 * k + i]) for i in range(5)]
+                                       for k in range(steps)])
+                        tot = np.median(tt[:, 63] - tt[:, 0])
+                        print(f"   wave{w}: total {tot:.0f} cyc, prologue {pro:.0f}; steady step [C, A, B, stage, barrier] = "
+                              f"{np.median(ph[2:-1], axis=0).round(0).tolist()}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

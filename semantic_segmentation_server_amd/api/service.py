@@ -60,8 +60,14 @@ class SemanticSegmentationServicer:
         return out
 
 
+MAX_V2_OBJECTS = 4096  # per-request cap of GetStreamSegmentedObjects (padding included)
+
+
 class SemanticSegmentationV2Servicer:
-    """v2 extension service."""
+    """v2 extension service. Client input is bounded: ``max_objects`` is clamped to
+    [0, min(buffer capacity, MAX_V2_OBJECTS)] (a huge padded request would otherwise
+    build billions of messages on the node's only RPC host) and an unknown
+    ``stream_id`` is NOT_FOUND instead of creating a buffer."""
 
     def __init__(self, hub: ResultHub, labels: Dict[int, str], num_detections: int = 3,
                  streams: Optional[list] = None, metrics=None,
@@ -74,8 +80,14 @@ class SemanticSegmentationV2Servicer:
         self.health_fn = health_fn
 
     def GetStreamSegmentedObjects(self, request, context):
-        n = request.max_objects or self.num_detections
-        recs = self.hub.buffer(int(request.stream_id)).pop(n)
+        buf = self.hub.get(int(request.stream_id))
+        if buf is None:
+            context.set_code(grpc.StatusCode.NOT_FOUND)
+            context.set_details(f"unknown stream_id {request.stream_id}")
+            return P.StreamSegmentedObjects()
+        cap = min(MAX_V2_OBJECTS, buf.maxlen or MAX_V2_OBJECTS)
+        n = max(0, min(int(request.max_objects or self.num_detections), cap))
+        recs = buf.pop(n)
         data = [P.TaggedObject(object=_obj(r, self.labels), frame_id=int(r["frame"]),
                                timestamp=float(r["ts"]), stream_id=int(r["stream"]))
                 for r in recs]

@@ -27,6 +27,7 @@ from typing import Callable, Dict, List, Optional, Tuple
 import torch
 import torch.nn as nn
 
+from ..ops import fused_span as FS
 from ..ops import hip_ops as K
 from ..ops.hip_ops import conv_out_hw
 from .deeplab import DeepLabV3
@@ -169,7 +170,7 @@ class HipDeepLab:
             for blk in bb.blocks:
                 s = blk.spec
                 d = dict(
-                    spec=s,
+                    spec=s, module=blk,
                     expand=_pack_dense(blk.expand, dev) if blk.expand is not None else None,
                     dw=_pack_dw(blk.dw, dev),
                     project=_pack_dense(blk.project, dev))
@@ -232,6 +233,7 @@ class HipDeepLab:
         self.logit_w = lw[:, :, 0, 0].reshape(lw.shape[0], 1, 1, -1).contiguous().to(dev, torch.bfloat16)
         self.logit_b = lb.to(dev, torch.float32)
         self._plans: Dict[tuple, Tuple[List[Callable], Dict[str, torch.Tensor]]] = {}
+        self._span_tables: Dict[tuple, dict] = {}
         self._labels_out: Optional[torch.Tensor] = None
 
     # ------------------------------------------------------------------ plan
@@ -510,8 +512,44 @@ class HipDeepLab:
             fp = blk["fused"]
             variants.insert(0, ("fused", [lambda *_, x=inp, out=out, h=h, w=w, OH=OH, OW=OW:
                                           K.fused_ir(x, fp, out, B=B, IH=h, IW=w, OH=OH, OW=OW)]))
+        if blk["expand"] is not None and s.stride == 1 and FS.span_npi_options(s.cout):
+            # expanded tensor kept on chip: raster spans of ~h*w/S pixels per workgroup
+            for S in self._span_counts(B, h, w):
+                if not FS.span_supported(s.cin, s.cout, 1, h, w, S, s.dilation):
+                    continue
+                if "span" not in blk:
+                    blk["span"] = self._pack_span(blk, s)
+                tab = self._span_table(h, w, S, s.dilation)
+                for npi in FS.span_npi_options(s.cout):
+                    variants.insert(0, (f"span{S}n{npi}", [
+                        lambda *_, x=inp, out=out, tab=tab, npi=npi, sp=blk["span"]: FS.fused_ir_span(
+                            x, sp, tab, out, B=B, residual=s.residual, npi=npi)]))
         outer_ops.append(Choice(f"block{i}", variants))
         return out, OH, OW, s.cout
+
+    @staticmethod
+    def _span_counts(B: int, h: int, w: int) -> List[int]:
+        """Spans per image for the fused span kernel: the smallest count whose spans fit
+        the kernel's 144 pixels, and 2x / 4x that for small batches (more workgroups)."""
+        s0 = -(-h * w // (FS.MAX_GROUPS * 16))
+        out = [s0, 2 * s0]
+        if B * s0 < 256:
+            out.append(4 * s0)
+        return out
+
+    def _span_table(self, h: int, w: int, S: int, dil: int):
+        key = (h, w, S, dil)
+        if key not in self._span_tables:
+            self._span_tables[key] = FS.span_table(h, w, S, dil, self.device)
+        return self._span_tables[key]
+
+    def _pack_span(self, blk: dict, s) -> dict:
+        m = blk["module"]
+        ew, eb = m.expand.fold()
+        dwf, dbf = m.dw.fold()
+        pwf, pbf = m.project.fold()
+        return FS.pack_fused_span(ew[:, :, 0, 0], eb, dwf[:, 0], dbf, pwf[:, :, 0, 0], pbf, Cin=s.cin,
+                                  hid=s.hidden, Cout=s.cout, device=self.device)
 
     def _resnet_block(self, ops, buf, i, blk, x, B, h, w, c):
         m = blk["blk"]

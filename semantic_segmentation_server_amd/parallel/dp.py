@@ -29,6 +29,7 @@ import torch.distributed as dist
 
 from .dist import DistContext
 from ..runtime.results import RECORD_DTYPE, ResultHub
+from ..utils.tracing import NULL_TRACER
 
 log = logging.getLogger(__name__)
 
@@ -127,6 +128,7 @@ class DataParallelPipeline:
         self.frames_done = 0
         self.records_out = 0
         self._prev_done = None  # compute-done event of the previous step
+        self.tracer = NULL_TRACER  # the serving loop installs its own (--profile)
         if self.cuda and hasattr(engine, "bind_inputs"):
             # one hipGraph per staging slot reads the slot in place (no per-step D2D
             # copy of the B x Hc x Wc x 3 frames into a single static input); with
@@ -164,6 +166,23 @@ class DataParallelPipeline:
             dist.scatter(self.staging[s], chunks, src=0)
         return self.staging[s]
 
+    def _scatter_meta(self, fids, tss, strm):
+        """Scatter ingest: rank 0 holds the ids / capture times / source streams of the
+        whole node batch; every rank receives the slice of the frames it was sent, so
+        records keep their true origin (ranks used to re-tag scattered frames
+        with their own default streams, duplicate frame ids and zero timestamps)."""
+        B, W = self.B, self.ctx.world
+        mine = torch.empty((B, 3), dtype=torch.float64)
+        full = None
+        if self.ctx.is_root:
+            if len(fids) != B * W:
+                raise ValueError(f"scatter ingest: rank 0 needs metadata for {B * W} frames")
+            full = torch.tensor(list(zip(fids, strm, tss)), dtype=torch.float64).reshape(W, B, 3)
+        dist.scatter(mine, list(full.unbind(0)) if full is not None else None, src=0,
+                     group=self.ctx.cpu_group)
+        m = mine.numpy()
+        return m[:, 0].astype(np.int64).tolist(), m[:, 2].tolist(), m[:, 1].astype(np.int64).tolist()
+
     # ---------------------------------------------------------------- step
     def step(self, frame_ids=None, ts=None, streams=None, next_frames=None) -> np.ndarray:
         """Run one step on the prefetched frames; returns rank-0 records (else empty).
@@ -176,11 +195,16 @@ class DataParallelPipeline:
         (double-buffered staging) instead of preceding it.
         """
         B = self.B
-        fids = list(frame_ids) if frame_ids is not None else \
-            list(range(self.frames_done // self.ctx.world, self.frames_done // self.ctx.world + B))
-        tss = list(ts) if ts is not None else [0.0] * B
+        scatter = self.ingest == "scatter" and self.ctx.initialized
+        nb = B * self.ctx.world if (scatter and self.ctx.is_root) else B
+        base = self.frames_done // self.ctx.world * (self.ctx.world if nb > B else 1)
+        fids = list(frame_ids) if frame_ids is not None else list(range(base, base + nb))
+        tss = list(ts) if ts is not None else [0.0] * nb
         strm = list(streams) if streams is not None else \
-            [self.ctx.rank * self.S + i % self.S for i in range(B)]
+            [(self.ctx.rank * self.S + i % self.S) if nb == B else (i // B) * self.S + i % self.S
+             for i in range(nb)]
+        if scatter:
+            fids, tss, strm = self._scatter_meta(fids, tss, strm)
         frames = self._frames_for_step()
         labels, packed = self.engine.run_device(frames)
         if next_frames is not None:
@@ -249,6 +273,10 @@ class DataParallelPipeline:
         return self._collect(prev) if prev is not None else np.zeros(0, RECORD_DTYPE)
 
     def _collect(self, pending) -> np.ndarray:
+        with self.tracer.stage("collect"):
+            return self._collect_inner(pending)
+
+    def _collect_inner(self, pending) -> np.ndarray:
         slot, ev, fids, strm, tss = pending
         if ev is not None:
             ev.synchronize()

@@ -3,22 +3,24 @@
 Launch: ``torchrun --nproc-per-node N --master-addr 127.0.0.1 -m
 semantic_segmentation_server_amd.server --gpus N [flags]``.
 
-Every rank owns ``--streams`` frame sources (global stream id = rank * S + s) and
-one engine on its GPU; each step a rank batches ``--batch`` frames from its
-sources, runs the hipGraph-captured step, and the packed records plus frame
-metadata are RCCL-gathered to rank 0, which pushes them into the per-stream
-result hub behind the v1/v2 services. With ``--ingest scatter`` rank 0 owns the
-sources for the whole node and RCCL-scatters frames instead.
+Every rank owns ``--streams`` frame sources (global stream id = launch rank * S + s) and
+one engine on its GPU. Each rank's loop is the measured pipeline (``runtime/driver.py``):
+a feeder thread fills a ring of pinned batches, ``DataParallelPipeline`` (lag 1, bound
+per-slot hipGraphs, post-processing on its own stream) runs the step and gathers the
+packed records plus frame metadata to rank 0, which pushes them into the per-stream
+result hub behind the v1/v2 services. With ``--ingest scatter`` rank 0 owns the sources
+for the whole node and scatters frames (RCCL) and their metadata (gloo) instead.
 
-Failure handling: every step starts with a tiny all-reduce that
-carries the stop flag; a rank whose source fails keeps stepping on its last good
-batch (logged) so collectives never hang. When a peer rank is lost, the next
-collective fails (peer connection closed, or the ``--rank_timeout`` process-group
-timeout) and rank 0 switches to degraded mode: it drops the process group,
-re-shards onto itself (its own streams, local ingest) and keeps producing and
-serving; Health/grpc.health report ``ranks_alive = 1`` and the cause
-(``--no_degrade`` exits instead). A non-root rank that loses rank 0 exits.
-``--inject_fault rank:step`` raises on that rank/step (used by tests).
+Failure handling: every step starts with a tiny all-reduce carrying the
+stop flag; a source error is retried by the feeder (the rank keeps stepping). When a
+peer is lost, the next collective fails (peer connection closed, or the
+``--rank_timeout`` process-group timeout) on every survivor, and the survivors RE-FORM
+the group (``dist.reform``: membership agreed through a store hosted by launch rank 0,
+renumbered by launch rank, a fresh process group of the next generation). Each survivor
+keeps its own streams (their global ids do not change), so a lost rank costs exactly its
+own cameras; Health / grpc.health report ``ranks_alive`` of the new group. If launch rank
+0 is lost the others exit (it hosts the RPC). ``--no_degrade`` exits instead of
+re-forming. ``--inject_fault rank:step`` raises on that (launch) rank / step (tests).
 """
 from __future__ import annotations
 
@@ -36,10 +38,13 @@ from .dp import DataParallelPipeline
 from ..api import service as S
 from ..config import Config
 from ..labels import load_labels
+from ..runtime.driver import PipelineDriver
 from ..runtime.engine import Engine
+from ..runtime.feeder import BatchFeeder
 from ..runtime.results import ResultHub
 from ..runtime.sources import make_source
 from ..utils.metrics import Metrics
+from ..utils.tracing import Tracer
 
 log = logging.getLogger(__name__)
 
@@ -49,40 +54,56 @@ class DistributedServer:
                  max_steps: Optional[int] = None):
         self.cfg = cfg
         # RCCL only for the rank-0 frame scatter; otherwise a gloo group (records are
-        # gathered from pinned host memory, and an initialised RCCL communicator alone
-        # cost 23% of single-GPU throughput on MI355X -- see bench.py --pg)
+        # gathered from pinned host memory; see DataParallelPipeline)
         pg = "nccl" if cfg.ingest == "scatter" else "gloo"
-        import torch
         self.ctx = ctx or D.init(pg, timeout_s=cfg.rank_timeout,
                                  device="cuda" if torch.cuda.is_available() and cfg.device != "cpu"
                                  else "auto")
-        self.run_ctx = self.ctx  # == ctx until degraded to rank 0 alone
+        self.run_ctx = self.ctx  # the current group (re-formed after a rank loss)
+        self.launch_world = self.ctx.world
         self.degraded = False
         self.max_steps = max_steps
         self.metrics = Metrics()
+        self.tracer = Tracer(self.metrics, enabled=cfg.profile)
         S_ = max(1, cfg.streams)
         self.S = S_
+        me = self.ctx.orig_rank
         own = cfg.ingest == "local" or self.ctx.is_root
-        self.sources = [make_source(cfg.source, self.ctx.rank * S_ + s, cfg.camera_idx,
+        self.sources = [make_source(cfg.source, me * S_ + s, cfg.camera_idx,
                                     cfg.camera_width, cfg.camera_height, cfg.source_path,
                                     fps=cfg.fps_limit, seed=cfg.seed) for s in range(S_)] if own else []
         res = (cfg.camera_width, cfg.camera_height) if not self.sources else self.sources[0].resolution
         self.camera_res = res
         self.engine = Engine(cfg, self.ctx.device)
+        self.engine.tracer = self.tracer
         self.hub = ResultHub(self.ctx.world * S_, cfg.buffer_max) if self.ctx.is_root else None
-        self.pipe = DataParallelPipeline(self.ctx, self.engine, res[0], res[1], cfg.batch,
-                                         cfg.ingest, self.hub, S_)
+        self._ingest = cfg.ingest
+        self.feeder: Optional[BatchFeeder] = None
+        self.driver: Optional[PipelineDriver] = None
+        self._build_pipeline()
         self.steps = 0
         self.alive = True
         self.error: Optional[str] = None
         self.grpc_server = None
         self.port = None
-        self._last = None
-        self._ingest = cfg.ingest
         self.fault = None
         if cfg.inject_fault:
             r, st = cfg.inject_fault.split(":")
             self.fault = (int(r), int(st))
+
+    def _build_pipeline(self) -> None:
+        ctx = self.run_ctx
+        if self.feeder is not None:
+            self.feeder.stop()
+        nb = self.cfg.batch * (ctx.world if self._ingest == "scatter" else 1)
+        self.feeder = BatchFeeder(self.sources, nb, metrics=self.metrics) if self.sources else None
+        if self.feeder is not None:
+            self.feeder.start()
+        pipe = DataParallelPipeline(ctx, self.engine, self.camera_res[0], self.camera_res[1],
+                                    self.cfg.batch, self._ingest, self.hub, self.S, lag=1)
+        pipe.tracer = self.tracer
+        self.driver = PipelineDriver(pipe, self.feeder, self.tracer, self.metrics)
+        self._started = False
 
     # ------------------------------------------------------------------ rpc
     def start_rpc(self) -> None:
@@ -105,80 +126,42 @@ class DistributedServer:
 
     def _health(self):
         alive = self.run_ctx.world if self.alive else 0
-        return self.alive, alive, self.ctx.world, self.error or "ok"
+        return self.alive, alive, self.launch_world, self.error or "ok"
 
-    # ------------------------------------------------------------- degrade
-    def _degrade(self, err: BaseException) -> None:
-        """Peer lost: continue on rank 0 alone (local ingest, no collectives)."""
-        log.error("rank 0 lost a peer (%r): degrading to single-rank serving", err)
-        self.degraded = True
-        self.error = f"degraded to rank 0 alone after: {err!r}"
+    # ------------------------------------------------------------- failure
+    def _reform(self, err: BaseException) -> None:
+        """Peer lost: re-form the group from the survivors and keep serving."""
+        log.error("launch rank %d: collective failed (%r); re-forming the group",
+                  self.ctx.orig_rank, err)
         self.metrics.inc("degrade_events")
-        try:
-            D.destroy(self.ctx)
-        except Exception:  # the group may already be broken
-            pass
-        self.run_ctx = D.DistContext(0, 1, self.ctx.local_rank, self.ctx.device, None)
-        res = self.camera_res
-        self.pipe = DataParallelPipeline(self.run_ctx, self.engine, res[0], res[1], self.cfg.batch,
-                                         "local", self.hub, self.S)
-        self._ingest = "local"
+        t0 = time.perf_counter()
+        new = D.reform(self.run_ctx, timeout_s=self.cfg.rank_timeout)
+        log.info("re-formed the group in %.2f s", time.perf_counter() - t0)
+        self.degraded = True
+        self.error = (f"degraded to {new.world}/{self.launch_world} ranks "
+                      f"(launch ranks {new.members}) after: {err!r}")
+        log.error("group re-formed: %s", self.error)
+        self.run_ctx = new
+        self._build_pipeline()
 
     # ----------------------------------------------------------------- step
-    def _gather_local(self):
-        if not self.sources:
-            return None, None, None, None
-        per = [self.cfg.batch // self.S + (1 if s < self.cfg.batch % self.S else 0)
-               for s in range(self.S)]
-        if self._ingest == "scatter":
-            per = [p * self.run_ctx.world for p in per]
-        imgs, ids, ts, strm = [], [], [], []
-        for src, n in zip(self.sources, per):
-            if n == 0:
-                continue
-            try:
-                f, fid, t = src.read_batch(n)
-            except StopIteration:
-                raise
-            except Exception as e:  # keep the collectives in lock-step: reuse the last batch
-                log.warning("rank %d source %d failed: %s", self.ctx.rank, src.stream, e)
-                self.metrics.inc("source_errors")
-                if self._last is None:
-                    raise
-                return self._last
-            imgs.append(f)
-            ids += list(fid)
-            ts += list(t)
-            strm += [src.stream] * len(fid)
-        out = (np.concatenate(imgs), ids, ts, strm)
-        self._last = out
-        return out
-
     def step(self) -> bool:
         """One lock-step iteration on every rank. Returns False when stopping."""
-        if self.fault and self.fault == (self.ctx.rank, self.steps):
-            raise RuntimeError(f"injected fault on rank {self.ctx.rank} at step {self.steps}")
-        t0 = time.perf_counter()
-        stop = 0.0
-        try:
-            frames, ids, ts, strm = self._gather_local()
-        except StopIteration:
-            stop, frames = 1.0, None
+        if self.fault and self.fault == (self.ctx.orig_rank, self.steps):
+            raise RuntimeError(f"injected fault on rank {self.ctx.orig_rank} at step {self.steps}")
+        if not self._started:
+            first = self.driver.next_batch()
+            eos = 1.0 if (self.feeder is not None and first is None) else 0.0
+            if D.allreduce_max(self.run_ctx, eos) > 0:
+                return False
+            self.driver.start(first)
+            self._started = True
+        nxt = self.driver.next_batch()
+        stop = 1.0 if (self.feeder is not None and nxt is None) else 0.0
         if D.allreduce_max(self.run_ctx, stop) > 0:
+            self.driver.step(None)     # the in-flight batch still runs (collected by finish)
             return False
-        if frames is not None:
-            host = torch.from_numpy(np.ascontiguousarray(frames))
-            if self.engine.is_cuda:
-                host = host.pin_memory()
-            self.pipe.prefetch(host)
-        local_ids = ids if self._ingest == "local" else None
-        recs = self.pipe.step(local_ids, ts if local_ids else None, strm if local_ids else None)
-        dt = (time.perf_counter() - t0) * 1e3
-        n = self.cfg.batch * self.run_ctx.world
-        self.metrics.inc("frames", n)
-        self.metrics.inc("objects", len(recs))
-        self.metrics.observe("step_ms", dt)
-        self.metrics.observe("frame_ms", dt / n)
+        self.driver.step(nxt)
         self.steps += 1
         return self.max_steps is None or self.steps < self.max_steps
 
@@ -189,23 +172,31 @@ class DistributedServer:
                 while True:
                     if stop_event is not None and stop_event.is_set():
                         if D.allreduce_max(self.run_ctx, 1.0) > 0:
+                            self.driver.finish()
                             return
                     if not self.step():
+                        self.driver.finish()
                         return
             except Exception as e:
-                injected_here = self.fault is not None and self.fault[0] == self.ctx.rank
-                if (self.ctx.is_root and self.run_ctx.world > 1 and self.cfg.degrade
-                        and not injected_here):
-                    self._degrade(e)
-                    continue  # keep stepping on rank 0 alone
+                injected_here = self.fault is not None and self.fault[0] == self.ctx.orig_rank
+                if (self.run_ctx.world > 1 and self.cfg.degrade and not injected_here
+                        and self.run_ctx.store is not None):
+                    try:
+                        self._reform(e)
+                        continue  # keep stepping in the re-formed group
+                    except Exception as e2:
+                        log.error("re-forming failed: %r", e2)
+                        e = e2
                 self.alive = False
                 self.error = repr(e)
-                log.exception("rank %d stopped", self.ctx.rank)
+                log.exception("rank %d stopped", self.ctx.orig_rank)
                 raise
 
     def stop(self) -> None:
         if self.grpc_server is not None:
             self.grpc_server.stop(0)
+        if self.feeder is not None:
+            self.feeder.stop()
         for s in self.sources:
             s.close()
         if self.cfg.metrics_dump and self.ctx.is_root:
@@ -213,6 +204,8 @@ class DistributedServer:
 
 
 def serve_distributed(cfg: Config) -> int:
+    from .affinity import pin_to_gpu_numa
+    pin_to_gpu_numa()  # before the first GPU call of this process
     srv = DistributedServer(cfg)
     stop = threading.Event()
     signal.signal(signal.SIGTERM, lambda *a: stop.set())
@@ -222,5 +215,5 @@ def serve_distributed(cfg: Config) -> int:
         pass
     finally:
         srv.stop()
-        D.destroy(srv.ctx)
+        D.destroy(srv.run_ctx)
     return 0

@@ -11,6 +11,11 @@ Here a ``Producer`` thread batches frames from one or more streams per step
 per-stream buffers of a ``ResultHub``. Source errors are logged and retried with
 exponential backoff instead of killing the server; end of stream stops the
 producer (and the server if ``exit_on_eos``).
+
+On a GPU the producer runs the measured pipeline (``runtime/driver.py``: feeder
+thread with a pinned ring -> ``DataParallelPipeline`` with lag 1, bound per-slot
+hipGraphs and split post-processing), the same loop ``bench.py`` times. The
+synchronous ``Engine.step`` loop remains for CPU serving and ``--debug_dump``.
 """
 from __future__ import annotations
 
@@ -46,6 +51,9 @@ class Producer(threading.Thread):
 
     def stop(self) -> None:
         self._stop_evt.set()
+        f = getattr(self, "feeder", None)
+        if f is not None:
+            f.stop()
 
     def _gather(self):
         """Round-robin ``batch`` frames over the live sources."""
@@ -63,9 +71,56 @@ class Producer(threading.Thread):
             streams += [src.stream] * len(fid)
         return np.concatenate(imgs), ids, ts, streams
 
+    def _use_driver(self) -> bool:
+        e = self.engine
+        return bool(getattr(e, "is_cuda", False) and getattr(e, "debug", None) is None
+                    and e.cfg.graph and e.cfg.contour_mode == "fast")
+
+    def _run_driver(self) -> None:
+        from ..parallel.dist import DistContext
+        from ..parallel.dp import DataParallelPipeline
+        from .driver import PipelineDriver
+        from .feeder import BatchFeeder
+        tr = getattr(self.engine, "tracer", None)
+        ctx = DistContext(0, 1, 0, self.engine.device, None)
+        w, h = self.sources[0].resolution
+        feeder = BatchFeeder(self.sources, self.batch, metrics=self.metrics)
+        feeder.start()
+        self.feeder = feeder
+        try:
+            pipe = DataParallelPipeline(ctx, self.engine, w, h, self.batch, "local", self.hub,
+                                        len(self.sources), lag=1)
+            if tr is not None:
+                pipe.tracer = tr
+            drv = PipelineDriver(pipe, feeder, tr, self.metrics)
+            first = drv.next_batch()
+            if first is None:
+                return
+            drv.start(first)
+            while not self._stop_evt.is_set():
+                if self.max_steps is not None and self.steps >= self.max_steps:
+                    break
+                nxt = drv.next_batch()
+                drv.step(nxt)
+                self.steps += 1
+                self.alive_ts = time.time()
+                if nxt is None:
+                    log.info("end of stream after %d steps", self.steps)
+                    break
+            drv.finish()
+        except Exception as e:
+            self.error = e
+            self.metrics.inc("producer_errors")
+            log.exception("device pipeline failed")
+        finally:
+            feeder.stop()
+
     def run(self) -> None:
         failures = 0
         self.hub_clear()
+        if self._use_driver():
+            self._run_driver()
+            return
         while not self._stop_evt.is_set():
             if self.max_steps is not None and self.steps >= self.max_steps:
                 break

@@ -96,7 +96,14 @@ class ResultHub:
         self.maxlen = maxlen
         self._lock = threading.Lock()
 
+    def get(self, stream: int) -> Optional[ResultBuffer]:
+        """The stream's buffer, or None for a stream id the hub does not serve (RPC
+        lookups must not create buffers for arbitrary client-supplied ids)."""
+        with self._lock:
+            return self.buffers.get(stream)
+
     def buffer(self, stream: int) -> ResultBuffer:
+        """The stream's buffer, created on first use (producer side only)."""
         with self._lock:
             buf = self.buffers.get(stream)
             if buf is None:

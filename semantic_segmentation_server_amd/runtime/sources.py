@@ -51,6 +51,22 @@ class FrameSource:
         imgs = np.stack([f.image for f in frames])
         return imgs, [f.frame_id for f in frames], [f.ts for f in frames]
 
+    def read_batch_into(self, out: np.ndarray) -> Tuple[int, List[int], List[float]]:
+        """Fill ``out`` (n, H, W, 3) in place (the feeder's pinned ring slot); returns
+        (frames read, ids, ts). Raises StopIteration when no frame is left."""
+        ids, ts = [], []
+        for i in range(out.shape[0]):
+            try:
+                f = next(self)
+            except StopIteration:
+                if i == 0:
+                    raise
+                break
+            out[i] = f.image
+            ids.append(f.frame_id)
+            ts.append(f.ts)
+        return len(ids), ids, ts
+
     def close(self) -> None:
         pass
 
@@ -109,6 +125,33 @@ class SyntheticSource(FrameSource):
         self._i += n
         now = time.time()
         return self.pool[idx], ids, [now] * n
+
+    def advance(self, n: int):
+        """Consume ``n`` frames without copying pixels (the feeder's replay of a ring
+        slot that already holds pool frames)."""
+        if self.limit is not None:
+            n = min(n, self.limit - self._i)
+            if n <= 0:
+                raise StopIteration
+        ids = list(range(self._i, self._i + n))
+        self._i += n
+        return n, ids, [time.time()] * n
+
+    def read_batch_into(self, out: np.ndarray):
+        n = out.shape[0]
+        if self.limit is not None:
+            n = min(n, self.limit - self._i)
+            if n <= 0:
+                raise StopIteration
+        if self.fps:  # paced like __next__: the batch is ready when its last frame is
+            dt = self._t0 + (self._i + n - 1) / self.fps - time.time()
+            if dt > 0:
+                time.sleep(dt)
+        idx = np.arange(self._i, self._i + n) % len(self.pool)
+        np.take(self.pool, idx, axis=0, out=out[:n])
+        ids = list(range(self._i, self._i + n))
+        self._i += n
+        return n, ids, [time.time()] * n
 
 
 class FileSource(FrameSource):

@@ -147,6 +147,32 @@ def test_grpc_loopback_v1_and_v2():
         server.stop(0)
 
 
+def test_v2_bounds_client_input():
+    """max_objects is clamped, unknown stream ids are NOT_FOUND and never
+    allocate a buffer."""
+    hub = ResultHub(1, maxlen=8)
+    sv = S.SemanticSegmentationV2Servicer(hub, load_labels(), 3)
+    hub.push_records(_recs([15, 7]))
+
+    class Ctx:
+        code = None
+
+        def set_code(self, c):
+            self.code = c
+
+        def set_details(self, d):
+            self.details = d
+    ctx = Ctx()
+    r = sv.GetStreamSegmentedObjects(P.StreamRequest(stream_id=0, max_objects=2 ** 31 - 1, pad=True), ctx)
+    assert len(r.data) == 8 and ctx.code is None          # clamped to the buffer capacity
+    assert [d.object.label for d in r.data[:2]] == ["car", "person"]
+    r = sv.GetStreamSegmentedObjects(P.StreamRequest(stream_id=0, max_objects=-5, pad=True), ctx)
+    assert len(r.data) == 0
+    r = sv.GetStreamSegmentedObjects(P.StreamRequest(stream_id=12345, max_objects=3, pad=True), ctx)
+    assert ctx.code == grpc.StatusCode.NOT_FOUND and len(r.data) == 0
+    assert set(hub.buffers) == {0}
+
+
 def test_grpc_health_v1():
     state = {"ok": True}
     server, port = S.make_server(4, 0, "127.0.0.1")

@@ -67,13 +67,16 @@ def _worker(rank, world, port, ingest, q, lag=0, gather="host"):
             frames[i, 0, 0, 0] = 10 + rank * B + i
     pipe.prefetch(frames)
     recs = pipe.step()
+    # default frame ids advance per step by the frames of one rank (local ingest) or of
+    # the whole node (scatter: ids are rank 0's node-level capture ids)
+    adv = B * world if ingest == "scatter" else B
     if lag:  # records arrive one step late; the second step's come with flush()
         assert len(recs) == 0
         pipe.prefetch(frames)
         recs = pipe.step()
         last = pipe.flush()
         if ctx.is_root:
-            assert np.array_equal(last["cx"], recs["cx"]) and np.all(last["frame"] == recs["frame"] + B)
+            assert np.array_equal(last["cx"], recs["cx"]) and np.all(last["frame"] == recs["frame"] + adv)
     t = D.allreduce_max(ctx, float(rank))
     if ctx.is_root:
         q.put((recs["cx"].tolist(), recs["stream"].tolist(), t, hub.depth))
@@ -103,6 +106,55 @@ def test_dp_gather_and_scatter(world, ingest, lag, gather):
     assert streams == [i // B for i in range(world * B)]
     assert tmax == world - 1
     assert depth == world * B * (2 if lag else 1)
+
+
+def _scatter_meta_worker(rank, world, port, q):
+    """Scatter ingest with real capture metadata on rank 0: every record must carry the
+    id / timestamp / source stream of the frame it came from."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from semantic_segmentation_server_amd.parallel import dist as D
+    from semantic_segmentation_server_amd.parallel.dp import DataParallelPipeline
+    from semantic_segmentation_server_amd.runtime.results import ResultHub
+    ctx = D.init("gloo")
+    B = 2
+    hub = ResultHub(8) if ctx.is_root else None
+    pipe = DataParallelPipeline(ctx, FakeEngine(), 8, 6, B, "scatter", hub, lag=1)
+    nb = B * world if ctx.is_root else B
+    frames = torch.zeros(nb, 6, 8, 3, dtype=torch.uint8)
+    ids = ts = st = None
+    if ctx.is_root:
+        for i in range(nb):
+            frames[i, 0, 0, 0] = 10 + i
+        ids = [1000 + 7 * i for i in range(nb)]
+        ts = [50.0 + i for i in range(nb)]
+        st = [5 if i % 2 else 3 for i in range(nb)]   # two cameras on rank 0
+    pipe.prefetch(frames)
+    pipe.step(ids, ts, st)
+    recs = pipe.flush()
+    if ctx.is_root:
+        q.put((recs["cx"].tolist(), recs["frame"].tolist(), recs["ts"].tolist(), recs["stream"].tolist()))
+    D.barrier(ctx)
+    D.destroy(ctx)
+
+
+def test_scatter_keeps_capture_metadata():
+    world, B = 3, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scatter_meta_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    cx, frame, ts, stream = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n = world * B
+    assert np.allclose(cx, [(10 + i) / 255.0 for i in range(n)], atol=1e-6)
+    assert frame == [1000 + 7 * i for i in range(n)]
+    assert ts == [50.0 + i for i in range(n)]
+    assert stream == [5 if i % 2 else 3 for i in range(n)]
 
 
 def test_unpack_records_order():
@@ -200,3 +252,57 @@ def test_rank_loss_degrades_to_rank0():
     assert status == 1  # SERVING
     # 2 lock-step steps on 2 ranks (4 frames each), then 4 steps on rank 0 alone (2 frames each)
     assert frames == 2 * 4 + 4 * 2
+
+
+def _reform_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import grpc
+    from semantic_segmentation_server_amd import config as C
+    from semantic_segmentation_server_amd.api import proto as P
+    from semantic_segmentation_server_amd.api.service import SemanticSegmentationV2Stub
+    from semantic_segmentation_server_amd.parallel import dist as D
+    from semantic_segmentation_server_amd.parallel.serving import DistributedServer
+    ctx = D.init("gloo", timeout_s=60)
+    cfg = C.parse(["--port", "0", "--host", "127.0.0.1", "--device", "cpu", "--input_size", "65",
+                   "--batch", "2", "--streams", "1", "--gpus", str(world), "--min_area_ratio", "0",
+                   "--inject_fault", "2:2", "--rank_timeout", "60"])
+    srv = DistributedServer(cfg, ctx, max_steps=6)
+    try:
+        srv.run()
+    except RuntimeError:
+        if ctx.orig_rank == 2:
+            os._exit(0)  # the lost rank: drop its connections abruptly
+        raise
+    out = (srv.ctx.orig_rank, srv.steps, srv.run_ctx.world, srv.run_ctx.members)
+    if srv.ctx.is_root:
+        with grpc.insecure_channel(f"127.0.0.1:{srv.port}") as ch:
+            h = SemanticSegmentationV2Stub(ch).Health(P.Empty())
+        per_stream = {s: b.pushed for s, b in srv.hub.buffers.items()}
+        out = out + (h.ranks_alive, h.world_size, h.detail, srv.metrics.snapshot()["frames"], per_stream)
+    q.put(out)
+    srv.stop()
+    D.destroy(srv.run_ctx)
+
+
+def test_rank_loss_reshards_to_survivors():
+    """World 3, launch rank 2 dies at step 2: ranks 0 and 1 re-form a 2-rank group and
+    both keep serving their own streams (SURVEY.md §5.3 P-1 re-shard)."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_reform_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted((q.get(timeout=300) for _ in range(2)), key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    r0, r1 = got
+    assert r0[:4] == (0, 6, 2, [0, 1]) and r1[:4] == (1, 6, 2, [0, 1])
+    alive, wsize, detail, frames, per_stream = r0[4:]
+    assert alive == 2 and wsize == 3 and "degraded to 2/3" in detail
+    # 2 steps x 3 ranks x 2 frames, then 4 steps x 2 ranks x 2 frames
+    assert frames == 2 * 6 + 4 * 4
+    assert per_stream[1] > 0 and per_stream[0] > 0   # rank 1's camera still served after the loss

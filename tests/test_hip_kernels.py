@@ -889,3 +889,38 @@ def test_stream_group_matches_single_engine(monkeypatch):
                 p3 = p3.clone()
             torch.cuda.synchronize()
             assert _records_equal(p1, p3), it
+
+
+@pytest.mark.parametrize("cin,cout,dil,H,S", [
+    (64, 64, 1, 33, 8),     # blocks 7-9 (residual)
+    (64, 96, 1, 33, 8),     # block 10
+    (96, 96, 1, 33, 8),     # blocks 11-12 (residual)
+    (96, 160, 1, 33, 8),    # block 13
+    (160, 160, 2, 33, 8),   # blocks 14-15 (dilation 2, residual)
+    (160, 320, 2, 33, 8),   # block 16
+    (160, 160, 2, 33, 16),  # 16 spans per image
+    (96, 96, 1, 29, 7),     # odd map / span sizes
+    (160, 320, 2, 23, 4),
+])
+def test_fused_ir_span(cin, cout, dil, H, S):
+    """Fused span kernel (expanded tensor on chip) vs the fp32 torch block, and vs the
+    numpy re-execution of its own data flow from the packed operands."""
+    from semantic_segmentation_server_amd.ops import fused_span as FS
+    from test_fused_span_cpu import _block, pack_block  # tests/ is on sys.path (prepend mode)
+    blk, spec = _block(cin, cout, dil, seed=cin * 7 + cout + dil)
+    g = torch.Generator().manual_seed(21)
+    B, W = 3, H
+    x = torch.randn(B, cin, H, W, generator=g).to(torch.bfloat16)
+    with torch.no_grad():
+        ref = blk(x.float())
+    packed = pack_block(blk, spec, device=DEV)
+    table = FS.span_table(H, W, S, dil, DEV)
+    xd = _nhwc(x).to(DEV)
+    emu = FS.emulate_fused_span(_nhwc(x).float().numpy(), packed, table, residual=spec.residual)
+    for npi in FS.span_npi_options(cout):
+        out = torch.full((B, H, W, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
+        FS.fused_ir_span(xd, packed, table, out, B=B, residual=spec.residual, npi=npi)
+        torch.cuda.synchronize()
+        assert torch.isfinite(out).all(), npi
+        assert _rel(_nchw(out).cpu(), ref) < 2e-2, npi
+        assert _rel(out.cpu().float(), torch.from_numpy(emu)) < 5e-3, npi
