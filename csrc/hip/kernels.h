@@ -151,6 +151,24 @@ void stem_block0(const StemBlock0Params& p, hipStream_t s);
 // LDS bytes the tile kernel needs for a (TY, TX) tile (0 if the shape is unsupported).
 size_t fused_ir_tile_lds(int CinP, int stride, int dil, int TY, int TX, int expand);
 
+// DeepLabv3 head (aspp_head.hip): ASPP projection [M, K] x [K, 256] + bias + per-image
+// bias + ReLU, then the logits 1x1 conv (256 -> ncls <= 32) from the on-chip projection
+// tile. wp: [16 subtiles][K/32][64 lanes][8] bf16 (MFMA fragment order), wl: [2][8][64][8]
+// bf16 (classes zero-padded to 32), bl: [32] fp32 (zero-padded).
+struct AsppHeadParams {
+  const bf16* cat = nullptr;        // [M, K] concatenated ASPP branches
+  const bf16* wp = nullptr;
+  const float* bp = nullptr;        // [256]
+  const float* img_bias = nullptr;  // optional [M / HW, 256]
+  const bf16* wl = nullptr;
+  const float* bl = nullptr;
+  bf16* out = nullptr;              // [M, ldo] logits (channels >= ncls written as 0 up to ldo)
+  int M = 0, K = 0, N = 256, HW = 0, ncls = 0, ldo = 0;
+  int G = 9;                        // 16-pixel groups per workgroup (1, 2, 3, 5, 9)
+};
+void aspp_head(const AsppHeadParams& p, hipStream_t s);
+size_t aspp_head_lds(int G, int K);
+
 // Depthwise 3x3 (+bias, ReLU6) fused with the 1x1 projection (+bias [+ residual]):
 // the depthwise output stays in registers as the projection's MFMA operand.
 // Weights: wd [9, hid] fp32, wp [CoutP, hid] bf16 (CoutP = 16 * ceil(Cout / 16)).

@@ -232,6 +232,7 @@ class HipDeepLab:
         lw, lb = model.logits.fold()
         self.logit_w = lw[:, :, 0, 0].reshape(lw.shape[0], 1, 1, -1).contiguous().to(dev, torch.bfloat16)
         self.logit_b = lb.to(dev, torch.float32)
+        self.head = None  # aspp_head packed operands (built with the first plan)
         self._plans: Dict[tuple, Tuple[List[Callable], Dict[str, torch.Tensor]]] = {}
         self._span_tables: Dict[tuple, dict] = {}
         self._labels_out: Optional[torch.Tensor] = None
@@ -360,13 +361,26 @@ class HipDeepLab:
                 lambda *_, wt=wt: torch.mm(cat.view(Mp, self.cat_c), wt, out=raw),
                 lambda *_, h=h, w=w: K.bias_act(raw, self.proj_b, proj, M=Mp, N=A, HW=h * w,
                                                 img_bias=img_bias, act="relu")]))
-        ops.append(Choice("aspp.proj", proj_variants))
         logits = buf("logits", B, h, w, self.ldk)
-        ops.append(pw_choice("logits", lambda *_, h=h, w=w: K.conv_gemm(
+        split = [Choice("aspp.proj", proj_variants), pw_choice("logits", lambda *_, h=h, w=w: K.conv_gemm(
             proj, self.logit_w, self.logit_b, logits, B=B, IH=h, IW=w, Cin=A, OH=h, OW=w,
             Cout=self.num_classes, k=1, ldo=self.ldk, act=None), proj, self.logit_w,
             self.logit_b, logits, M=B * h * w, Cin=A, Cout=self.num_classes, ldo=self.ldk, act=None,
-            N_out=self.ldk))
+            N_out=self.ldk)]
+        if A == 256 and self.cat_c == 1024 and self.num_classes <= 32 and self.ldk <= 32:
+            # projection + bias + pooling bias + ReLU + logits in one kernel: the projection
+            # stays on chip (aspp_head.hip), no vendor GEMM on the hot path
+            if self.head is None:
+                self.head = K.pack_aspp_head(self.proj_w, self.proj_b, self.logit_w, self.logit_b, dev)
+            Mh = B * h * w
+            g0 = K.aspp_head_groups(Mh)
+            head = [(f"head_g{g}", [lambda *_, g=g, h=h, w=w: K.aspp_head(
+                cat.view(Mh, self.cat_c), self.head, logits.view(Mh, self.ldk), M=Mh, HW=h * w,
+                ldo=self.ldk, img_bias=img_bias, G=g)]) for g in K.ASPP_HEAD_G
+                if g == g0 or (g < g0 and -(-Mh // (16 * g)) <= 1024)]
+            ops.append(Choice("aspp.head", head + [("split", split)]))
+        else:
+            ops.extend(split)
         labels = buf("labels", B, H, W, dtype=torch.uint8)
         # labels_out (segment's out=): write the label maps straight into a caller
         # buffer (the engine's per-slot maps) instead of the plan's static one

@@ -717,6 +717,73 @@ def matvec(x, w, bias, out, *, B, N, K, act=None):
     return out
 
 
+ASPP_HEAD_G = (1, 2, 3, 5, 9)  # 16-pixel groups per workgroup (aspp_head.hip instantiations)
+
+
+def _frag_pack(w: torch.Tensor, rows: int) -> torch.Tensor:
+    """[N, K] -> MFMA A-fragment order [ceil(rows/16)][K/32][64 lanes][8] bf16, element
+    (n, k, lane, e) = W[n*16 + lane%16][k*32 + (lane//16)*8 + e] (rows zero-padded)."""
+    N, Kd = w.shape
+    NS = -(-rows // 16)
+    full = torch.zeros(NS * 16, Kd, dtype=torch.float32, device=w.device)
+    full[:N] = w.float()
+    return (full.reshape(NS, 16, Kd // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
+            .to(torch.bfloat16).reshape(-1))
+
+
+def pack_aspp_head(proj_w: torch.Tensor, proj_b: torch.Tensor, logit_w: torch.Tensor,
+                   logit_b: torch.Tensor, device=None) -> dict:
+    """ASPP projection [256, K] + logits [ncls, 256] (folded, fp32 or bf16) -> the
+    operands of ``aspp_head``: fragment-packed weights, fp32 biases (logits padded to 32)."""
+    proj_w = proj_w.reshape(proj_w.shape[0], -1)
+    logit_w = logit_w.reshape(logit_w.shape[0], -1)
+    N, Kd = proj_w.shape
+    ncls = logit_w.shape[0]
+    if N != 256 or Kd % 64 or logit_w.shape[1] != 256 or ncls > 32:
+        raise ValueError("pack_aspp_head: needs proj [256, K % 64 == 0], logits [<= 32, 256]")
+    dev = device or proj_w.device
+    bl = torch.zeros(32, dtype=torch.float32)
+    bl[:ncls] = logit_b.detach().float().cpu()
+    return dict(wp=_frag_pack(proj_w.detach().cpu(), 256).to(dev),
+                bp=proj_b.detach().float().contiguous().to(dev),
+                wl=_frag_pack(logit_w.detach().cpu(), 32).to(dev), bl=bl.to(dev), K=Kd, ncls=ncls)
+
+
+def aspp_head_groups(M: int) -> int:
+    """Pixel groups per workgroup: the smallest instantiation that keeps the grid within
+    one workgroup per CU (256), else the largest."""
+    groups = -(-M // 16)
+    for g in ASPP_HEAD_G:
+        if -(-groups // g) <= 256:
+            return g
+    return ASPP_HEAD_G[-1]
+
+
+def aspp_head(cat, packed: dict, out, *, M: int, HW: int, ldo: int, img_bias=None,
+              G: Optional[int] = None) -> torch.Tensor:
+    """Fused ASPP projection (+bias, +per-image bias, ReLU) and logits conv (aspp_head.hip).
+    cat: [M, K] bf16; out: [M, ldo] bf16 logits (channels ncls..ldo-1 written as zeros)."""
+    K, ncls = packed["K"], packed["ncls"]
+    G = aspp_head_groups(M) if G is None else G
+    if G not in ASPP_HEAD_G or K != 1024 or ldo % 4 or not ncls <= ldo <= 32:
+        raise ValueError(f"aspp_head: unsupported G={G} K={K} ldo={ldo}")
+    _chk(cat, torch.bfloat16, "cat", M * K)
+    _chk(out, torch.bfloat16, "out", M * ldo)
+    _chk(packed["wp"], torch.bfloat16, "wp", 256 * K)
+    _chk(packed["wl"], torch.bfloat16, "wl", 32 * 256)
+    _chk(packed["bp"], torch.float32, "bp", 256)
+    _chk(packed["bl"], torch.float32, "bl", 32)
+    if img_bias is not None:
+        if M % HW:
+            raise ValueError("aspp_head: M must be a multiple of HW with img_bias")
+        _chk(img_bias, torch.float32, "img_bias", (M // HW) * 256)
+    _hip_mod().aspp_head(_ptr(cat), _ptr(packed["wp"]), _ptr(packed["bp"]), _ptr(img_bias),
+                         _ptr(packed["wl"]), _ptr(packed["bl"]), _ptr(out), M, K, HW, ncls, ldo, G,
+                         _stream())
+    _dbg('aspp_head')
+    return out
+
+
 UPSAMPLE_VARIANTS = {"rows": 3, "rows_tag": 4, "lane": 1, "lane_tag": 2, "direct": 5}
 
 

@@ -924,3 +924,38 @@ def test_fused_ir_span(cin, cout, dil, H, S):
         assert torch.isfinite(out).all(), npi
         assert _rel(_nchw(out).cpu(), ref) < 2e-2, npi
         assert _rel(out.cpu().float(), torch.from_numpy(emu)) < 5e-3, npi
+
+
+@pytest.mark.parametrize("M,HW,ncls,ldo,img", [
+    (32 * 33 * 33, 33 * 33, 21, 24, True),   # the B = 32 headline head (G = 9)
+    (33 * 33, 33 * 33, 21, 24, True),        # batch 1 (G = 1)
+    (4 * 33 * 33, 33 * 33, 19, 20, False),   # Cityscapes classes, no pooling branch
+    (3 * 121 + 0, 121, 32, 32, True),        # M tail inside a 16-pixel group, full 32 classes
+])
+@pytest.mark.parametrize("G", [None, 1, 2, 3, 5, 9])
+def test_aspp_head(M, HW, ncls, ldo, img, G):
+    """Fused ASPP projection + logits vs fp32 torch: relu(cat Wp^T + bp + ib) rounded to
+    bf16 (the kernel's on-chip projection tile), then Wl . proj + bl."""
+    K = _hip()
+    g = torch.Generator().manual_seed(11)
+    Kd = 1024
+    cat = torch.relu(torch.randn(M, Kd, generator=g)).to(torch.bfloat16)
+    wp = (torch.randn(256, Kd, generator=g) / Kd ** 0.5).to(torch.bfloat16)
+    bp = torch.randn(256, generator=g) * 0.1
+    wl = (torch.randn(ncls, 256, generator=g) / 16).to(torch.bfloat16)
+    bl = torch.randn(ncls, generator=g)
+    ib = torch.randn(M // HW, 256, generator=g) * 0.5 if img else None
+    proj = cat.float() @ wp.float().t() + bp
+    if img:
+        proj = proj + ib.repeat_interleave(HW, 0)
+    proj = torch.relu(proj).to(torch.bfloat16).float()
+    ref = proj @ wl.float().t() + bl
+    packed = K.pack_aspp_head(wp, bp, wl, bl, device=DEV)
+    out = torch.full((M, ldo), float("nan"), dtype=torch.bfloat16, device=DEV)
+    K.aspp_head(cat.to(DEV), packed, out, M=M, HW=HW, ldo=ldo,
+                img_bias=None if ib is None else ib.to(DEV), G=G)
+    torch.cuda.synchronize()
+    got = out.float().cpu()
+    assert torch.isfinite(got).all()
+    assert _rel(got[:, :ncls], ref) < 1e-2
+    assert torch.all(got[:, ncls:] == 0)
