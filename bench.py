@@ -65,7 +65,12 @@ def main() -> int:
     p.add_argument("--dtype", default="bf16")
     p.add_argument("--streams", type=int, default=1,
                    help="concurrent camera streams per GPU, each with its own HIP stream + hipGraph")
+    p.add_argument("--serve", action="store_true",
+                   help="time the real serving loop (Server / DistributedServer: feeder thread, "
+                        "pinned ring, lag-1 pipeline, gRPC services up) instead of the bench loop")
     a = p.parse_args()
+    if a.serve:
+        return _serve_bench(a)
 
     import numpy as np
     import torch
@@ -150,7 +155,7 @@ def main() -> int:
 
     if ctx.is_root:
         out = {
-            "metric": BASELINE_METRIC,
+            "metric": _metric(a),
             "value": round(fps, 2),
             "unit": "frames/s",
             "n_gpus": ctx.world,
@@ -163,7 +168,7 @@ def main() -> int:
             "dtype": a.dtype,
             "data": f"synthetic {a.camera} BGR frames, random-init weights",
             "config": {
-                "model": "DeepLabv3-MobileNetV2" if a.arch == "mnv2" else "DeepLabv3-ResNet50",
+                "model": _model_name(a),
                 "aspp": a.aspp,
                 "global_batch": a.batch * ctx.world,
                 "per_gpu_batch": a.batch,
@@ -188,6 +193,94 @@ def main() -> int:
         print(json.dumps(out), flush=True)
     D.destroy(ctx)
     return 0
+
+
+def _serve_bench(a) -> int:
+    """Served fps: the production loop with a synthetic camera (no fps cap) and the
+    gRPC services up; W steps of warmup, then the frames of the next K steps over their
+    wall time, while a client subprocess times GetSegmentedObjects (rank 0)."""
+    import threading
+    import torch
+    from semantic_segmentation_server_amd import config as C
+    from semantic_segmentation_server_amd.parallel.affinity import pin_to_gpu_numa
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    pin_to_gpu_numa()
+    cam_w, cam_h = (int(v) for v in a.camera.split("x"))
+    cfg = C.Config(arch=a.arch, aspp=a.aspp, input_size=a.input_size, backend=a.backend,
+                   dtype=a.dtype, batch=a.batch, graph=a.graph, contour_mode=a.contour_mode,
+                   ingest=a.ingest, camera_width=cam_w, camera_height=cam_h, streams=a.streams,
+                   num_classes=21 if a.arch == "mnv2" else 19, port=0, host="127.0.0.1",
+                   dataset="pascal" if a.arch == "mnv2" else "cityscapes", gpus=world)
+    total = a.warmup + a.steps
+    if world > 1:
+        from semantic_segmentation_server_amd.parallel import dist as D
+        from semantic_segmentation_server_amd.parallel.serving import DistributedServer
+        srv = DistributedServer(cfg, max_steps=None)
+        ctx = srv.ctx
+        steps = lambda: srv.steps  # noqa: E731
+        stop_evt = threading.Event()
+        th = threading.Thread(target=srv.run, args=(stop_evt,), daemon=True)
+        root, port = ctx.is_root, None
+        th.start()
+    else:
+        from semantic_segmentation_server_amd.server import Server
+        srv = Server(cfg).start()
+        steps = lambda: srv.producer.steps  # noqa: E731
+        root, port = True, srv.port
+    t_lim = time.time() + 600
+    while steps() < a.warmup and time.time() < t_lim:
+        time.sleep(0.0005)
+    if world > 1:
+        port = srv.port
+    s0, t0 = steps(), time.perf_counter()
+    while steps() < s0 + a.steps and time.time() < t_lim:
+        time.sleep(0.0002)
+    s1, t1 = steps(), time.perf_counter()
+    fps = (s1 - s0) * a.batch * world / (t1 - t0)
+    rpc = None
+    if root and a.rpc > 0 and port:
+        mpctx = mp.get_context("spawn")
+        parent, child = mpctx.Pipe()
+        proc = mpctx.Process(target=_client_proc, args=(port, a.rpc, child), daemon=True)
+        proc.start()
+        rpc = parent.recv() if parent.poll(120) else {"error": "client timeout"}
+        proc.join(10)
+    if world > 1:
+        stop_evt.set()
+        th.join(60)
+        srv.stop()
+        D.destroy(srv.run_ctx)
+    else:
+        srv.stop(0)
+    if root:
+        out = {
+            "metric": _metric(a), "value": round(fps, 2), "unit": "frames/s", "n_gpus": world,
+            "steps": s1 - s0, "warmup": a.warmup, "ms_per_step": round((t1 - t0) / max(1, s1 - s0) * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
+            "data": f"synthetic {a.camera} BGR frames, random-init weights",
+            "config": {"model": _model_name(a), "global_batch": a.batch * world, "seq_len": a.input_size,
+                       "parallelism": f"dp{world}", "mode": "served (feeder + lag-1 pipeline + gRPC)",
+                       "streams_per_gpu": a.streams},
+            "p50_get_segmented_objects_ms": rpc.get("p50_ms") if rpc else None,
+            "p99_get_segmented_objects_ms": rpc.get("p99_ms") if rpc else None,
+        }
+        print(json.dumps(out), flush=True)
+    return 0
+
+
+def _model_name(a) -> str:
+    return "DeepLabv3-MobileNetV2" if a.arch == "mnv2" else "DeepLabv3-ResNet50"
+
+
+def _metric(a) -> str:
+    """The headline metric string, with the config's own input size and dataset (the
+    BASELINE.json string for the headline config)."""
+    if a.arch == "mnv2" and a.input_size == 513:
+        return BASELINE_METRIC
+    ds = "PASCAL VOC" if a.arch == "mnv2" else "Cityscapes"
+    return (f"frames/sec (whole node) + p50 GetSegmentedObjects latency, "
+            f"{a.input_size}x{a.input_size} {ds}")
 
 
 def _rpc_under_load(ctx, pipe, hub, run_steps, n_calls, D):

@@ -46,7 +46,7 @@ struct FrameWS {
   long long* t10;      // [N]
   long long* t01;      // [N]
   int32_t* hist;       // [K][bins]
-  int32_t* nslot;      // [0] selected, [1] overflow flag, [2] cross-tile edges, [3] selected holes
+  int32_t* nslot;      // [0] selected, [1] contours dropped (> K passed), [2] cross-tile edges, [3] selected holes
   int32_t* slot_node;  // [K]
   int32_t* cidx;       // [N] per tile-local root pixel: its index among the tile's roots
   int32_t* rootpix;    // [ntiles][kTileRoots] raster index of each tile-local root
@@ -55,6 +55,7 @@ struct FrameWS {
   int32_t* clabel;     // [kMergeCap] final label of each compact node
   int32_t* flag;       // [4]: [0] = 1 -> frame took the global union-find fallback
   int32_t* edges;      // [kEdgeCap][2] cross-tile unions (tile-local root pairs, -1 = outside)
+  int32_t* bcnt;       // [ceil(N / 256)] passing contours per k_select block (raster order)
 };
 
 constexpr int TW = 32, TH = 32;     // local CCL tile
@@ -81,7 +82,7 @@ Layout layout(int H, int W, int K, int bins) {
   l.small_bytes = al(16 + (size_t)K * bins * 4 + (size_t)K * 4);
   l.big_bytes = al((l.N + 1) * 4) + al(l.N) + 4 * al(l.N * 4) + 4 * al(l.N * 8) + al(l.N * 4) +
                 al(l.ntiles * kTileRoots * 4) + 2 * al(l.ntiles * 4) + al(kMergeCap * 4) + al(16) +
-                al((size_t)kEdgeCap * 8);
+                al((size_t)kEdgeCap * 8) + al((l.N + 255) / 256 * 4);
   return l;
 }
 
@@ -109,6 +110,7 @@ __host__ __device__ inline FrameWS frame_ws(char* ws, const Layout& l, int B, in
   f.clabel = reinterpret_cast<int32_t*>(p); p += al(kMergeCap * 4);
   f.flag = reinterpret_cast<int32_t*>(p); p += al(16);
   f.edges = reinterpret_cast<int32_t*>(p); p += al((size_t)kEdgeCap * 8);
+  f.bcnt = reinterpret_cast<int32_t*>(p); p += al((l.N + 255) / 256 * 4);
   return f;
 }
 
@@ -789,22 +791,92 @@ __global__ __launch_bounds__(256) void k_tree(KArgs a) {
 }
 
 // ---------------------------------------------------------------- select
+// k_select counts, per 256-pixel block, the roots whose contour passes min_area;
+// k_assign (one workgroup per frame) scans those counts and hands the record slots
+// to the first K passing contours in raster order of their discovery pixel. The
+// choice is deterministic (round 1 took them in atomicAdd order, so with more than K
+// passing contours the kept subset changed from run to run) and keeps the
+// smallest discovery keys: among siblings those come LAST in findContours order, so
+// they are the records the reference's LIFO buffer serves first
+// (/root/reference/sem_seg_server.py:186-192, 52-60). Contours past K are counted in
+// nslot[1]; k_finalize flags the frame by a negative record count.
+__device__ __forceinline__ bool passes(const FrameWS& f, const KArgs& a, int p) {
+  if (f.L[p + 1] != p + 1) return false;
+  const int t = f.t00[p];
+  return t != 0 && (double)t * 0.5 >= a.min_area;
+}
+
 __global__ __launch_bounds__(256) void k_select(KArgs a) {
   const int b = blockIdx.y;
   const int N = a.ch * a.cw;
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= N) return;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
-  if (f.L[p + 1] != p + 1) return;
-  const double area = (double)f.t00[p] * 0.5;
-  if (!(area >= a.min_area) || f.t00[p] == 0) return;
-  const int s = atomicAdd(f.nslot, 1);
-  if (s < a.K) {
-    f.slot[p] = s;
-    f.slot_node[s] = p + 1;
-    if (!f.mask[p]) atomicAdd(f.nslot + 3, 1);  // a selected hole: k_hist needs its ring
-  } else {
-    f.nslot[1] = 1;  // overflow: contour dropped
+  const int n = __syncthreads_count(p < N && passes(f, a, p));
+  if (threadIdx.x == 0) f.bcnt[blockIdx.x] = n;
+}
+
+__global__ __launch_bounds__(1024) void k_assign(KArgs a) {
+  __shared__ int s_pre[1024];
+  __shared__ int s_tot;
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int N = a.ch * a.cw;
+  const int nb = (N + 255) / 256;
+  FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
+  // per-thread chunk of consecutive blocks, then an exclusive scan over the threads
+  const int per = (nb + 1023) / 1024;
+  const int b0 = min(nb, t * per), b1 = min(nb, b0 + per);
+  int own = 0;
+  for (int i = b0; i < b1; ++i) own += f.bcnt[i];
+  s_pre[t] = own;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
+    const int v = t >= o ? s_pre[t - o] : 0;
+    __syncthreads();
+    s_pre[t] += v;
+    __syncthreads();
+  }
+  if (t == 1023) s_tot = s_pre[1023];
+  int base = s_pre[t] - own;  // passing contours before this thread's blocks
+  __syncthreads();
+  const int total = s_tot;
+  const int kept = min(total, a.K);
+  // walk this thread's blocks with a non-zero count below the cut; each such block's
+  // 256 pixels are ranked by one 64-lane sweep per 64 pixels (ballot prefix counts).
+  // Blocks are handed to waves: gather (block, base) pairs in LDS first.
+  __shared__ int s_blk[256], s_base[256], s_n;
+  if (t == 0) s_n = 0;
+  __syncthreads();
+  for (int i = b0; i < b1 && base < kept; ++i) {
+    const int c = f.bcnt[i];
+    if (c) {
+      const int k = atomicAdd(&s_n, 1);  // at most K (<= 256) blocks hold kept contours
+      if (k < 256) { s_blk[k] = i; s_base[k] = base; }
+      base += c;
+    }
+  }
+  __syncthreads();
+  const int nblk = min(s_n, 256);
+  const int wid = t >> 6, lane = t & 63;
+  int holes = 0;
+  for (int k = wid; k < nblk; k += 16) {
+    int r = s_base[k];
+    for (int q = 0; q < 4; ++q) {
+      const int p = s_blk[k] * 256 + q * 64 + lane;
+      const bool ok = p < N && passes(f, a, p);
+      const unsigned long long m = __ballot(ok);
+      const int rank = r + __popcll(m & ((1ull << lane) - 1));
+      if (ok && rank < kept) {
+        f.slot[p] = rank;
+        f.slot_node[rank] = p + 1;
+        holes += f.mask[p] == 0;
+      }
+      r += __popcll(m);
+    }
+  }
+  if (holes) atomicAdd(f.nslot + 3, holes);
+  if (t == 0) {
+    f.nslot[0] = kept;
+    f.nslot[1] = total - kept;
   }
 }
 
@@ -895,6 +967,32 @@ __global__ __launch_bounds__(256) void k_hist(KArgs a) {
 // ---------------------------------------------------------------- finalize
 constexpr int kMaxDepth = 32;
 
+__device__ __forceinline__ int disc_key(const FrameWS& f, int n) {
+  const int r = n - 1;
+  return f.mask[r] ? r : r - 1;
+}
+
+__device__ __forceinline__ int node_depth(const FrameWS& f, int n) {
+  int d = 0;
+  for (; n != 0; n = f.parent[n - 1]) ++d;
+  return d;
+}
+
+// Does node a (depth da) come before node b (depth db) in findContours pre-order?
+// (a is an ancestor of b, or at the first divergence a's branch has the larger key.)
+__device__ bool precedes(const FrameWS& f, int a, int da, int b, int db) {
+  int u = a, v = b;
+  for (; db > da; --db) v = f.parent[v - 1];
+  if (u == v) return true;   // a is an ancestor of b
+  for (; da > db; --da) u = f.parent[u - 1];
+  if (u == v) return false;  // b is an ancestor of a
+  while (f.parent[u - 1] != f.parent[v - 1]) {
+    u = f.parent[u - 1];
+    v = f.parent[v - 1];
+  }
+  return disc_key(f, u) > disc_key(f, v);
+}
+
 __global__ __launch_bounds__(64) void k_finalize(KArgs a) {
   const int b = blockIdx.x;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
@@ -905,8 +1003,11 @@ __global__ __launch_bounds__(64) void k_finalize(KArgs a) {
   __shared__ int s_order[256];
   __shared__ int s_emit[256];
   __shared__ float s_val[256][5];
+  __shared__ int s_deep;
   const int ns = min(*f.nslot, min(a.K, 256));
   const int t = threadIdx.x;
+  if (t == 0) s_deep = 0;
+  __syncthreads();
   for (int i = t; i < ns; i += 64) {
     const int node = f.slot_node[i];
     s_node[i] = node;
@@ -920,6 +1021,12 @@ __global__ __launch_bounds__(64) void k_finalize(KArgs a) {
     }
     for (int k = 0; k < len; ++k) s_path[i][k] = chain[len - 1 - k];
     s_len[i] = len;
+    if (len == kMaxDepth) {
+      // chain truncated (nesting deeper than kMaxDepth): order by parent walks instead
+      int n = node, d = 0;
+      for (; n != 0 && d <= kMaxDepth; n = f.parent[n - 1]) ++d;
+      if (n != 0) s_deep = 1;
+    }
     // statistics
     const int r = node - 1;
     const int* h = f.hist + (size_t)i * a.bins;
@@ -947,7 +1054,17 @@ __global__ __launch_bounds__(64) void k_finalize(KArgs a) {
   }
   __syncthreads();
   // rank in pre-order: ancestor first; siblings by descending discovery key
-  for (int i = t; i < ns; i += 64) {
+  if (s_deep) {  // exact order at any depth: lift to equal depth, then walk to the LCA
+    for (int i = t; i < ns; i += 64) {
+      int rank = 0;
+      const int di = node_depth(f, s_node[i]);
+      for (int j = 0; j < ns; ++j)
+        if (j != i) rank += precedes(f, s_node[j], node_depth(f, s_node[j]), s_node[i], di);
+      s_order[rank] = i;
+    }
+    __syncthreads();
+  }
+  for (int i = t; i < ns && !s_deep; i += 64) {
     int rank = 0;
     for (int j = 0; j < ns; ++j) {
       if (j == i) continue;
@@ -972,7 +1089,7 @@ __global__ __launch_bounds__(64) void k_finalize(KArgs a) {
       for (int c = 0; c < 5; ++c) rec[1 + 5 * n + c] = s_val[i][c];
       ++n;
     }
-    rec[0] = (float)n;
+    rec[0] = f.nslot[1] > 0 ? -(float)n : (float)n;  // negative: contours dropped past K
   }
 }
 
@@ -1056,6 +1173,7 @@ void postprocess(const PostParams& p, hipStream_t s) {
   if (st++ < stages) hipLaunchKernelGGL(k_quads, gs, blk, 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_tree, gp, blk, 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_select, gp, blk, 0, s, a);
+  if (st++ < stages) hipLaunchKernelGGL(k_assign, dim3(p.B), dim3(1024), 0, s, a);
   if (st++ < stages)
     hipLaunchKernelGGL(k_hist, gh, blk, (size_t)std::min(p.K, 256) * p.num_bins * 4, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_finalize, dim3(p.B), dim3(64), 0, s, a);

@@ -241,6 +241,16 @@ def allreduce_max(ctx: DistContext, v: float, poll_s: float = 0.05) -> float:
     return float(t.item())
 
 
+def broadcast_obj(ctx: DistContext, obj):
+    """Rank 0's picklable ``obj`` on every rank (host group: gloo when RCCL is the
+    default backend). Used once per plan build to share rank 0's autotune picks."""
+    if ctx.world == 1 or not ctx.initialized:
+        return obj
+    buf = [obj if ctx.is_root else None]
+    dist.broadcast_object_list(buf, src=0, group=ctx.cpu_group)
+    return buf[0]
+
+
 def allreduce_sum(ctx: DistContext, v: float) -> float:
     if not ctx.initialized:
         return v

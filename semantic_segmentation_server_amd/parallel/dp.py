@@ -34,9 +34,28 @@ from ..utils.tracing import NULL_TRACER
 log = logging.getLogger(__name__)
 
 
+_overflow_frames = 0
+
+
+def overflow_frames() -> int:
+    """Frames (process lifetime) whose contours passing min_area exceeded the K record
+    slots: the device kept the first K by discovery key and flagged the frame with a
+    negative record count (postprocess.hip k_assign / k_finalize)."""
+    return _overflow_frames
+
+
 def unpack_records(packed: np.ndarray, K: int, frame_ids, ts, streams) -> np.ndarray:
-    """packed: (F, 1 + 5K) float32 -> RECORD_DTYPE rows in push order."""
-    counts = packed[:, 0].astype(np.int64)
+    """packed: (F, 1 + 5K) float32 -> RECORD_DTYPE rows in push order. A negative count
+    marks a frame with more than K passing contours (|count| == K were kept)."""
+    global _overflow_frames
+    raw = packed[:, 0]
+    over = int((raw < 0).sum())
+    if over:
+        if _overflow_frames == 0:
+            log.warning("a frame had more than K=%d contours above min_area; the first K by "
+                        "discovery order were kept (raise --max_segments)", K)
+        _overflow_frames += over
+    counts = np.abs(raw).astype(np.int64)
     total = int(counts.sum())
     out = np.zeros(total, RECORD_DTYPE)
     j = 0
@@ -129,6 +148,12 @@ class DataParallelPipeline:
         self.records_out = 0
         self._prev_done = None  # compute-done event of the previous step
         self.tracer = NULL_TRACER  # the serving loop installs its own (--profile)
+        hm = getattr(engine, "_hip_model", None)
+        if hm is not None and hasattr(hm, "pick_sync") and ctx.world > 1 and ctx.initialized:
+            # the plan is built (and autotuned) in lock-step on every rank: rank 0 times the
+            # variants, the others take its picks, so all ranks run identical kernels
+            from . import dist as _D
+            hm.pick_sync = lambda picks, _ctx=ctx: _D.broadcast_obj(_ctx, picks)
         if self.cuda and hasattr(engine, "bind_inputs"):
             # one hipGraph per staging slot reads the slot in place (no per-step D2D
             # copy of the B x Hc x Wc x 3 frames into a single static input); with

@@ -125,9 +125,14 @@ def quad_stats(node: np.ndarray, fg: np.ndarray):
 
 
 def component_segments(labels_cropped: np.ndarray, min_area: float,
-                       palette: Optional[np.ndarray] = None) -> List[tuple]:
+                       palette: Optional[np.ndarray] = None,
+                       max_records: Optional[int] = None) -> List[tuple]:
     """Same output as ``reference.segments_exact``:
-    [(label, score, area_px, cx, cy, order_key, is_hole)] in contour order."""
+    [(label, score, area_px, cx, cy, order_key, is_hole)] in contour order.
+
+    ``max_records`` (the device's K record slots): when more contours pass min_area,
+    keep the ``max_records`` with the smallest node id (raster index of the discovery
+    pixel), the device's deterministic rule (postprocess.hip k_assign)."""
     if _ndi is None:
         raise RuntimeError("scipy is required for the CPU component path")
     lab = np.asarray(labels_cropped, np.uint8)
@@ -163,7 +168,9 @@ def component_segments(labels_cropped: np.ndarray, min_area: float,
         if p != 0:
             t = total[p]
             t[0] += total[n][0]; t[1] += total[n][1]; t[2] += total[n][2]
-    cand = [n for n in nodes.tolist() if total[n][0] * 0.5 >= min_area]
+    cand = [n for n in nodes.tolist() if total[n][0] != 0 and total[n][0] * 0.5 >= min_area]
+    if max_records is not None and len(cand) > max_records:
+        cand = sorted(cand)[:max_records]
     if not cand:
         return []
     # subtree membership per candidate via ancestor walks of every node

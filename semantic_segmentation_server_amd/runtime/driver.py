@@ -42,6 +42,7 @@ class PipelineDriver:
         self.steps = 0
         self.frames = 0
         self._t_last = None
+        self._overflow_seen = 0
 
     # ------------------------------------------------------------------ helpers
     def _h2d_event(self) -> Optional["torch.cuda.Event"]:
@@ -96,7 +97,12 @@ class PipelineDriver:
         self.frames += n
         now = time.perf_counter()
         if self.metrics is not None:
+            from ..parallel.dp import overflow_frames
             dt = (now - self._t_last) * 1e3
+            ov = overflow_frames()
+            if ov != self._overflow_seen:  # frames with more than K contours above min_area
+                self.metrics.inc("record_overflow_frames", ov - self._overflow_seen)
+                self._overflow_seen = ov
             self.metrics.inc("frames", n)
             self.metrics.inc("objects", len(recs))
             self.metrics.observe("step_ms", dt)

@@ -361,10 +361,10 @@ def test_device_postprocess_matches_spec(seed, h, w, min_area):
     torch.cuda.synchronize()
     rec = rec.cpu().numpy()
     for i in range(B):
-        exp = component_segments(maps[i, :h, :w], min_area)
-        n = int(rec[i, 0])
+        exp = component_segments(maps[i, :h, :w], min_area, max_records=64)
+        n = abs(int(rec[i, 0]))
         got = rec[i, 1:1 + 5 * n].reshape(n, 5)
-        assert n == min(len(exp), 64), (i, n, len(exp))
+        assert n == len(exp), (i, n, len(exp))
         for j in range(n):
             lab, score, area, cx, cy = exp[j][:5]
             assert int(got[j, 0]) == lab
@@ -396,9 +396,9 @@ def test_device_postprocess_many_components(block, period, min_area):
     post = DevicePostprocess(torch.device(DEV), h, w, pascal_colormap(), K=64)
     rec = post.run(torch.from_numpy(maps).to(DEV), w, h, min_area).cpu().numpy()
     for i in range(2):
-        exp = component_segments(maps[i], min_area)
-        n = int(rec[i, 0])
-        assert n == min(len(exp), 64), (n, len(exp))
+        exp = component_segments(maps[i], min_area, max_records=64)
+        n = abs(int(rec[i, 0]))
+        assert n == len(exp), (n, len(exp))
         got = rec[i, 1:1 + 5 * n].reshape(n, 5)
         for j in range(n):
             lab_, score, area, cx, cy = exp[j][:5]
@@ -406,6 +406,68 @@ def test_device_postprocess_many_components(block, period, min_area):
             assert got[j, 2] == np.float32(min(1.0, area / (w * h)))
             assert got[j, 3] == np.float32(min(1.0, cx / w))
             assert got[j, 4] == np.float32(min(1.0, cy / h))
+
+
+@pytest.mark.parametrize("K", [8, 64])
+def test_device_postprocess_overflow_deterministic(K):
+    """More contours pass min_area than there are record slots: the device keeps the
+    first K by discovery key (same rule as the spec's ``max_records``), flags the frame
+    with a negative count, and gives identical records on every run."""
+    from semantic_segmentation_server_amd.labels import pascal_colormap
+    from semantic_segmentation_server_amd.postprocess.components import component_segments
+    from semantic_segmentation_server_amd.postprocess.device import DevicePostprocess
+    h = w = 257
+    lab = np.zeros((h, w), np.uint8)
+    rng = np.random.default_rng(5)
+    for y in range(2, h - 12, 14):       # ~300 blobs of 6-10 px, classes 7 / 15
+        for x in range(2, w - 12, 14):
+            s_ = int(rng.integers(6, 11))
+            lab[y:y + s_, x:x + s_] = 15 if rng.random() < 0.5 else 7
+    lab[100:140, 100:160] = 0            # a hole inside nothing (background) - no-op
+    maps = np.stack([lab, lab[::-1].copy(), np.zeros_like(lab)])
+    post = DevicePostprocess(torch.device(DEV), h, w, pascal_colormap(), K=K)
+    outs = []
+    for _ in range(3):
+        outs.append(post.run(torch.from_numpy(maps).to(DEV), w, h, 10.0).cpu().numpy().copy())
+    for o in outs[1:]:
+        assert np.array_equal(o, outs[0])
+    rec = outs[0]
+    for i in range(2):
+        full = component_segments(maps[i], 10.0)
+        assert len(full) > K
+        exp = component_segments(maps[i], 10.0, max_records=K)
+        assert int(rec[i, 0]) == -len(exp)   # overflow flag: negative count
+        got = rec[i, 1:1 + 5 * K].reshape(K, 5)
+        for j in range(K):
+            lab_, score, area, cx, cy = exp[j][:5]
+            assert int(got[j, 0]) == lab_ and abs(got[j, 1] - score) < 1e-6
+            assert got[j, 3] == np.float32(min(1.0, cx / w)) and got[j, 4] == np.float32(min(1.0, cy / h))
+    assert rec[2, 0] == 0
+
+
+def test_device_postprocess_deep_nesting():
+    """Concentric 3-px rings nest ~80 contours deep (> the 32-entry ancestor chains of
+    k_finalize): the record order must still be findContours pre-order."""
+    from semantic_segmentation_server_amd.labels import pascal_colormap
+    from semantic_segmentation_server_amd.postprocess.components import component_segments
+    from semantic_segmentation_server_amd.postprocess.device import DevicePostprocess
+    h = w = 257
+    yy, xx = np.mgrid[0:h, 0:w]
+    ring = np.maximum(np.abs(yy - 128), np.abs(xx - 128)) // 3
+    lab = np.where(ring % 2 == 0, 15, 0).astype(np.uint8)
+    lab[:, :] = np.where(ring >= 42, 0, lab)
+    maps = lab[None].copy()
+    post = DevicePostprocess(torch.device(DEV), h, w, pascal_colormap(), K=128)
+    rec = post.run(torch.from_numpy(maps).to(DEV), w, h, 0.0).cpu().numpy()
+    exp = component_segments(lab, 0.0, max_records=128)
+    assert len(exp) > 40, len(exp)
+    n = abs(int(rec[0, 0]))
+    assert n == len(exp)
+    got = rec[0, 1:1 + 5 * n].reshape(n, 5)
+    for j in range(n):
+        lab_, score, area, cx, cy = exp[j][:5]
+        assert int(got[j, 0]) == lab_ and abs(got[j, 1] - score) < 1e-6, j
+        assert got[j, 2] == np.float32(min(1.0, area / (w * h))), j
 
 
 def _small_cfg(**kw):
