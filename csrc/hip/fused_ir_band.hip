@@ -1,0 +1,365 @@
+// Row-streaming fused MobileNetV2 inverted residual for the high-resolution blocks
+// (blocks 1-6 of DeepLabv3-MobileNetV2 at 513^2: 257^2 -> 129^2 -> 65^2 -> 33^2 maps,
+// Cin 16..32, hidden 96..192, Cout 24..64, stride 1 or 2, dilation 1), gfx950.
+//
+//   out = project( relu6( dw3x3_s( relu6( expand(x) ) ) ) ) [+ x]
+//
+// Round 1 ran these blocks as 2-D tile kernels (fused_ir / fused_ir_persist): every
+// tile re-expanded its input halo (1.3-4.6x the outputs at these tile sizes), and each
+// 32-channel hidden chunk cost two workgroup barriers around a few MFMAs, so blocks 1-6
+// took 365 us per 32-frame step against a ~40 us HBM/MFMA roofline
+// (profiles/r2_v1_layer_times.txt). The reference runs the whole network as one Edge
+// TPU call (/root/reference/sem_seg_server.py:162).
+//
+// Here a workgroup owns a BAND: R output rows x TW = 16 * NW output columns of one
+// image, and streams the band's input rows top to bottom:
+//   * every input row is expanded exactly once (no vertical halo recompute inside the
+//     band; the horizontal halo is 2 columns): MFMA 16x16x32 bf16, A = the block's
+//     expansion weights (fragment-packed, LDS), B = 16 input pixels straight from HBM
+//     (one 16-byte load per lane, prefetched one row ahead) -> relu6 -> fp16 row E in
+//     LDS holding ALL hidden channels of the row;
+//   * the depthwise is accumulated per input row into register-resident fp16 partial
+//     sums of the 2 (stride 2) or 3 (stride 1) output rows that row feeds: each E read
+//     (one 16-byte ds_read per tap column) serves every open output row, so an input
+//     pixel is read 3x (not 9x) from LDS;
+//   * when an output row's last input row has been added, its depthwise result feeds
+//     the projection MFMA (fp16, K = 32 per hidden chunk) as the B fragment directly
+//     (lane = 8 channels of one pixel), and the row is stored (+ bias, + residual);
+//   * one barrier per input row (two with a single E slot, chosen when two slots
+//     would keep the CU below two workgroups).
+// Lane -> pixel mapping: wave w owns output columns 16w..16w+15 of the band (MFMA B
+// columns), so the depthwise of a lane is the one pixel whose projection it feeds.
+// E layout: pixel-major rows of hidP fp16 + 16 B pad (pitch/16 odd: the 16 lanes of a
+// ds_read_b128 quarter on consecutive pixels hit distinct 16-byte bank groups); stride-2
+// rows are stored even columns first, then odd columns (the even half padded to 8 mod 16
+// entries), so the three taps of 16 consecutive outputs read 16 consecutive entries.
+#include "common.h"
+#include "kernels.h"
+
+namespace ssa {
+
+namespace {
+
+typedef _Float16 f16;
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kBW = 4;           // waves per workgroup
+constexpr int kBT = 64 * kBW;    // threads
+// output columns per band: the band's input columns ((TW - 1) * S + 3) fill exactly
+// 64 (stride 1) / 128 (stride 2) pixels = 1 / 2 whole MFMA pixel groups per wave, so no
+// wave carries an idle expansion group (the lanes of the 16th output column of wave 3,
+// stride 1, and of its 16th, stride 2... are masked instead)
+__host__ __device__ constexpr int band_cols(int S) { return S == 1 ? 62 : 63; }
+
+struct BandArgs {
+  const bf16* in; const char* blob; bf16* out;
+  int B, IH, IW, Cin, OH, OW, Cout, residual;
+  int R, nbx, nby;          // rows per band, bands across / down
+  int HE, P, EROW;          // stride-2 even-half entries, E pixel pitch (B), E row bytes
+  int blob_bytes;           // host-packed weights, copied to LDS once
+  int o_be, o_wd, o_bd, o_wp, o_bp;  // section offsets inside the blob (bytes)
+};
+
+// Workgroup barrier for LDS hand-offs only. __syncthreads() is a workgroup release
+// fence: with the previous row's output stores pending it makes the compiler drain
+// vmcnt to 0 -- which, on the in-order vector memory counter, also waits for the input
+// rows prefetched behind those stores and exposed a full HBM round trip per input row.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Host-packed blob: [We frags NSH KiB][be hidP f32][wd 9 x hidP f16][bd hidP f16]
+// [Wp frags NS*NCH KiB][bp NS*16 f32]; sections 16-byte aligned. The host folds the
+// relu6 scale: expansion weights and bias and the depthwise bias come divided by 6, the
+// projection weights multiplied by 6, so both relu6 become [0, 1] clamps that fold into
+// the clamp bit of the instruction producing the value (E' = E / 6, D' = D / 6).
+template <int S, int NSH, int NS, int NSLOT>
+__global__ __launch_bounds__(kBT) void fused_ir_band_kernel(BandArgs a) {
+  constexpr int NCH = NSH / 2;            // 32-channel hidden chunks
+  constexpr int HID = NSH * 16;
+  constexpr int NDS = S == 1 ? 3 : 2;     // open output rows (D accumulator slots)
+  constexpr int U = S == 1 ? 3 : 4;       // step unroll: static slot roles
+  constexpr int GI = S;                   // input pixel groups per wave per row (IWT <= 64 / 128)
+  constexpr int kTW = band_cols(S);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r16 = lane & 15, kq = lane >> 4;
+
+  int blk = blockIdx.x;
+  const int bx = blk % a.nbx;
+  blk /= a.nbx;
+  const int by = blk % a.nby;
+  const int b = blk / a.nby;
+  const int x0 = bx * kTW, y0 = by * a.R, y1 = min(y0 + a.R, a.OH);
+  const int twv = min(kTW, a.OW - x0);            // valid output columns of this band
+  const int iwv = (twv - 1) * S + 3;              // local input columns it reads
+  const int ixb = x0 * S - 1;                     // global column of local input column 0
+
+  // ---- weights -> LDS (16-byte copies)
+  for (int i = tid; i < a.blob_bytes / 16; i += kBT)
+    *reinterpret_cast<i32x4*>(smem + i * 16) = *reinterpret_cast<const i32x4*>(a.blob + i * 16);
+  const char* sWe = smem;
+  const float* sBe = reinterpret_cast<const float*>(smem + a.o_be);
+  const char* sWd = smem + a.o_wd;
+  const char* sBd = smem + a.o_bd;
+  const char* sWp = smem + a.o_wp;
+  const float* sBp = reinterpret_cast<const float*>(smem + a.o_bp);
+  char* sE = smem + ((a.blob_bytes + 15) & ~15);
+  __syncthreads();  // (the only full barrier: no global store is pending yet)
+
+  // ---- this lane's output pixel and its three tap columns in E
+  const int xl = wid * 16 + r16;
+  const bool xv = xl < twv;
+  const int xc = xv ? xl : 0;
+  int ecol[3];
+  if (S == 1) {
+    ecol[0] = xc * a.P; ecol[1] = (xc + 1) * a.P; ecol[2] = (xc + 2) * a.P;
+  } else {
+    ecol[0] = xc * a.P; ecol[1] = (a.HE + xc) * a.P; ecol[2] = (xc + 1) * a.P;
+  }
+  // ---- this wave's input pixel groups: local column i = (wid + k*NW)*16 + r16
+  int epix[GI], gcol[GI];
+  bool pin[GI];
+#pragma unroll
+  for (int k = 0; k < GI; ++k) {
+    const int g = wid + k * kBW;
+    const int i = g * 16 + r16;
+    const int ic = i < iwv ? i : 0;
+    // columns past the band's input (and out-of-image ones) write into the sink entry
+    // at the row's end (an aliased real entry would race with the lane that owns it)
+    gcol[k] = ixb + ic;
+    pin[k] = i < iwv && gcol[k] >= 0 && gcol[k] < a.IW;
+    // out-of-image columns keep the zeros written below (the expansion of a padding
+    // pixel goes to the sink instead of being masked per MFMA)
+    epix[k] = pin[k] ? (S == 1 ? ic : ((ic & 1) ? a.HE + (ic >> 1) : (ic >> 1))) * a.P : a.EROW - a.P;
+  }
+  // zero the E entries of this band's out-of-image columns (at most the first and the
+  // last local column) in every slot, once: they are never written again
+  for (int z = tid; z < NSLOT * 2 * (HID / 8); z += kBT) {
+    const int slot = z / (2 * (HID / 8)), rem = z % (2 * (HID / 8));
+    const int side = rem / (HID / 8), c8 = rem % (HID / 8);
+    const int i = side == 0 ? 0 : iwv - 1;
+    const int gc = ixb + i;
+    if (gc < 0 || gc >= a.IW) {
+      const int e = S == 1 ? i : ((i & 1) ? a.HE + (i >> 1) : (i >> 1));
+      *reinterpret_cast<i32x4*>(sE + slot * a.EROW + e * a.P + c8 * 16) = i32x4{0, 0, 0, 0};
+    }
+  }
+  __syncthreads();
+  // X fragment loads (B operand): lane = pixel r16, channels kq*8..+7 (zero past Cin)
+  const bool kin = kq * 8 < a.Cin;
+  // input rows prefetched U steps ahead (slot = step % U, static after the unroll): one
+  // step of compute is ~1k cycles against ~2-4k of HBM latency
+  bf16x8 xq[U][GI];
+  // Branch- and select-free: every lane issues all GI loads, clamped to a valid pixel
+  // (a conditional load, or a zero-select right after the load, made the compiler wait
+  // for the row just prefetched). No masking is needed: channel-padding lanes read real
+  // (finite) channels that meet zero expansion weights, and out-of-image columns are
+  // zeroed when E is written; out-of-image rows are never expanded.
+  auto load_x = [&](int iy, bf16x8* dst) {
+    const int iyc = min(max(iy, 0), a.IH - 1);
+#pragma unroll
+    for (int k = 0; k < GI; ++k) {
+      const int col = min(max(gcol[k], 0), a.IW - 1);
+      const int ch = kin ? kq * 8 : 0;
+      dst[k] = ld8(a.in + (((size_t)b * a.IH + iyc) * a.IW + col) * a.Cin + ch);
+    }
+  };
+
+  f16x8 D[NDS][NCH];
+#pragma unroll
+  for (int s = 0; s < NDS; ++s)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) D[s][c] = f16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  const f16x8 h0 = {0, 0, 0, 0, 0, 0, 0, 0}, h1 = {1, 1, 1, 1, 1, 1, 1, 1};
+
+  const int iy0 = y0 * S - 1;
+  const int n_in = (y1 - y0 - 1) * S + 3;
+#pragma unroll
+  for (int q = 0; q < U; ++q) load_x(iy0 + q, xq[q]);
+
+  // whole unrolled rounds: steps past n_in expand rows nobody reads and feed output
+  // rows past the band (skipped), which keeps the round straight-line code (an early
+  // exit inside it made the compiler's wait counts at the loop header fall back to 0)
+  for (int t0 = 0; t0 < n_in; t0 += U) {
+#pragma unroll
+    for (int ph = 0; ph < U; ++ph) {
+      const int t = t0 + ph;
+      const int iy = iy0 + t;
+      const bool rowin = iy >= 0 && iy < a.IH;  // uniform
+      char* E = sE + (NSLOT == 2 ? (t & 1) : 0) * a.EROW;
+      if (NSLOT == 1) lds_barrier();  // every read of the previous row is done
+      // ---- [expand] input row iy -> E (fp16, relu6; zero at image columns outside)
+      if (rowin) {
+#pragma unroll
+        for (int hs = 0; hs < NSH; ++hs) {
+          const bf16x8 wf = *reinterpret_cast<const bf16x8*>(sWe + hs * 1024 + lane * 16);
+          const f32x4 be4 = *reinterpret_cast<const f32x4*>(sBe + hs * 16 + kq * 4);
+#pragma unroll
+          for (int k = 0; k < GI; ++k) {
+            const f32x4 e = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xq[ph][k], be4, 0, 0, 0);
+            // relu6 is a [0, 1] clamp on the 1/6-scaled values: the clamp bit of the
+            // conversion, no separate max / min
+            f16x4 o = {(f16)e[0], (f16)e[1], (f16)e[2], (f16)e[3]};
+            o = __builtin_elementwise_min(__builtin_elementwise_max(o, h0.lo), h1.lo);
+            *reinterpret_cast<f16x4*>(E + epix[k] + (hs * 16 + kq * 4) * 2) = o;
+          }
+        }
+      }
+      // the input pixels of row t + U: in flight under the next U steps
+      load_x(iy + U, xq[ph]);  // (past the band's last row: a harmless clamped reload)
+      lds_barrier();
+      // ---- [depthwise] row iy into the open output rows it feeds
+      // stride 1: output y0+t (ky 0, slot t%3), y0+t-1 (ky 1), y0+t-2 (ky 2, completes)
+      // stride 2: t even -> y0+t/2 (ky 0), y0+t/2-1 (ky 2, completes); t odd -> ky 1
+      const int nct = S == 1 ? 3 : ((ph & 1) ? 1 : 2);
+      int ky[3], sl[3], orow[3];
+      if (S == 1) {
+        ky[0] = 0; sl[0] = ph % 3;       orow[0] = y0 + t;
+        ky[1] = 1; sl[1] = (ph + 2) % 3; orow[1] = y0 + t - 1;
+        ky[2] = 2; sl[2] = (ph + 1) % 3; orow[2] = y0 + t - 2;
+      } else if ((ph & 1) == 0) {
+        ky[0] = 0; sl[0] = (ph / 2) % 2;     orow[0] = y0 + t / 2;
+        ky[1] = 2; sl[1] = (ph / 2 + 1) % 2; orow[1] = y0 + t / 2 - 1;
+        ky[2] = 0; sl[2] = 0;                orow[2] = -1;
+      } else {
+        ky[0] = 1; sl[0] = ((ph - 1) / 2) % 2; orow[0] = y0 + (t - 1) / 2;
+        ky[1] = 0; sl[1] = 0;                  orow[1] = -1;
+        ky[2] = 0; sl[2] = 0;                  orow[2] = -1;
+      }
+      if (rowin && xv) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          const int co = (c * 32 + kq * 8) * 2;
+          f16x8 v[3];
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) v[kx] = *reinterpret_cast<const f16x8*>(E + ecol[kx] + co);
+#pragma unroll
+          for (int j = 0; j < nct; ++j) {
+            if (orow[j] < y0 || orow[j] >= y1) continue;  // uniform
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+              const f16x8 w = *reinterpret_cast<const f16x8*>(sWd + ((ky[j] * 3 + kx) * HID) * 2 + co);
+              D[sl[j]][c] = v[kx] * w + D[sl[j]][c];
+            }
+          }
+        }
+      }
+      // ---- [complete] the output row whose last input row this was
+      const int jc = S == 1 ? 2 : ((ph & 1) ? -1 : 1);
+      if (jc >= 0) {
+        const int o = orow[jc < 0 ? 0 : jc];
+        const int sc = sl[jc < 0 ? 0 : jc];
+        if (o >= y0 && o < y1) {
+          f32x4 acc[NS];
+#pragma unroll
+          for (int n = 0; n < NS; ++n) acc[n] = *reinterpret_cast<const f32x4*>(sBp + n * 16 + kq * 4);
+#pragma unroll
+          for (int c = 0; c < NCH; ++c) {
+            const f16x8 bd = *reinterpret_cast<const f16x8*>(sBd + (c * 32 + kq * 8) * 2);
+            f16x8 d = D[sc][c] + bd;
+            d = __builtin_elementwise_min(__builtin_elementwise_max(d, h0), h1);
+            D[sc][c] = h0;
+#pragma unroll
+            for (int n = 0; n < NS; ++n) {
+              const f16x8 wp = *reinterpret_cast<const f16x8*>(sWp + (n * NCH + c) * 1024 + lane * 16);
+              acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wp, d, acc[n], 0, 0, 0);
+            }
+          }
+          if (xv) {
+            const size_t opix = ((size_t)b * a.OH + o) * a.OW + x0 + xl;
+#pragma unroll
+            for (int n = 0; n < NS; ++n) {
+              const int ch = n * 16 + kq * 4;
+              if (ch >= a.Cout) continue;
+              f32x4 v = acc[n];
+              if (a.residual) {  // stride 1, Cin == Cout: same pixel of the input
+                const bf16x4 r = *reinterpret_cast<const bf16x4*>(a.in + opix * a.Cin + ch);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] += (float)r[q];
+              }
+              const bf16x4 ob = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+              *reinterpret_cast<bf16x4*>(a.out + opix * a.Cout + ch) = ob;
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int S, int NSH, int NS, int NSLOT>
+void launch_band(const BandArgs& a, size_t lds, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_ir_band_kernel<S, NSH, NS, NSLOT>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
+          "fused_ir_band attr");
+    attr = true;
+  }
+  hipLaunchKernelGGL((fused_ir_band_kernel<S, NSH, NS, NSLOT>), dim3(a.B * a.nby * a.nbx), dim3(kBT), lds,
+                     st, a);
+  check_launch("fused_ir_band");
+}
+
+struct BandGeom {
+  int IWT, HE, NE, P, EROW;
+};
+
+BandGeom band_geom(int stride, int hidP, int OW) {
+  BandGeom g;
+  const int tw = OW < band_cols(stride) ? OW : band_cols(stride);
+  g.IWT = (tw - 1) * stride + 3;
+  g.P = hidP * 2 + 16;
+  if (stride == 1) {
+    g.HE = 0;
+    g.NE = g.IWT;
+  } else {
+    const int even = (g.IWT + 1) / 2;
+    g.HE = even + ((8 - even % 16) + 16) % 16;  // == 8 (mod 16)
+    g.NE = g.HE + g.IWT / 2;
+  }
+  g.EROW = (g.NE + 1) * g.P;  // + a sink entry for the padding lanes of the last group
+  return g;
+}
+
+}  // namespace
+
+size_t fused_ir_band_lds(int stride, int hidP, int OW, int blob_bytes, int nslot) {
+  const BandGeom g = band_geom(stride, hidP, OW);
+  return (size_t)((blob_bytes + 15) & ~15) + (size_t)nslot * g.EROW;
+}
+
+int fused_ir_band_cols(int stride) { return band_cols(stride); }
+
+void fused_ir_band(const FusedBandParams& p, hipStream_t st) {
+  if (p.stride != 1 && p.stride != 2) throw std::invalid_argument("fused_ir_band: stride 1 or 2");
+  if (p.Cin > 32 || p.Cin % 8 || p.hidP % 32 || p.R < 1) throw std::invalid_argument("fused_ir_band: Cin <= 32, hidP % 32");
+  if (p.residual && (p.stride != 1 || p.Cin != p.Cout)) throw std::invalid_argument("fused_ir_band: bad residual");
+  if (p.OH != (p.IH - 1) / p.stride + 1 || p.OW != (p.IW - 1) / p.stride + 1)
+    throw std::invalid_argument("fused_ir_band: output size must be the pad-1 3x3 conv's");
+  const BandGeom g = band_geom(p.stride, p.hidP, p.OW);
+  const size_t lds = fused_ir_band_lds(p.stride, p.hidP, p.OW, p.blob_bytes, p.nslot);
+  if (lds > 160 * 1024) throw std::invalid_argument("fused_ir_band: LDS over 160 KiB");
+  BandArgs a{p.in, reinterpret_cast<const char*>(p.blob), p.out, p.B, p.IH, p.IW, p.Cin, p.OH, p.OW, p.Cout,
+             p.residual, p.R, cdiv(p.OW, band_cols(p.stride)), cdiv(p.OH, p.R), g.HE, g.P, g.EROW, p.blob_bytes,
+             p.o_be, p.o_wd, p.o_bd, p.o_wp, p.o_bp};
+  const int NSH = p.hidP / 16, NS = (p.Cout + 15) / 16;
+#define BAND(S_, NSH_, NS_)                                                     \
+  if (p.stride == S_ && NSH == NSH_ && NS == NS_) {                             \
+    if (p.nslot == 2) launch_band<S_, NSH_, NS_, 2>(a, lds, st);                \
+    else launch_band<S_, NSH_, NS_, 1>(a, lds, st);                             \
+    return;                                                                     \
+  }
+  // block 1 (16 -> 96 -> 24, s2), 2 (24 -> 144 -> 24), 3 (24 -> 144 -> 32, s2),
+  // 4-5 (32 -> 192 -> 32), 6 (32 -> 192 -> 64, s2); hidden 144 runs padded to 160
+  BAND(2, 6, 2) BAND(1, 10, 2) BAND(2, 10, 2) BAND(1, 12, 2) BAND(2, 12, 4)
+#undef BAND
+  throw std::invalid_argument("fused_ir_band: no instantiation for this (stride, hidden, Cout)");
+}
+
+}  // namespace ssa

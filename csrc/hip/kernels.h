@@ -137,6 +137,19 @@ struct FusedSpanParams {
 };
 void fused_ir_span(const FusedSpanParams& p, hipStream_t s);
 size_t fused_ir_span_lds(int Cin, int Cout, int WR, int WCP, int xslots);
+// Row-streaming fused inverted residual (fused_ir_band.hip): blocks with Cin <= 32,
+// stride 1/2, dilation 1. blob: host-packed weights (hip_ops.pack_fused_band) with the
+// section offsets below; R output rows per band, nslot E row buffers (1 or 2).
+struct FusedBandParams {
+  const bf16* in = nullptr;   // [B, IH, IW, Cin]
+  const void* blob = nullptr;
+  bf16* out = nullptr;        // [B, OH, OW, Cout]
+  int B = 0, IH = 0, IW = 0, Cin = 0, OH = 0, OW = 0, Cout = 0, hidP = 0, stride = 1, residual = 0;
+  int R = 8, nslot = 2, blob_bytes = 0, o_be = 0, o_wd = 0, o_bd = 0, o_wp = 0, o_bp = 0;
+};
+void fused_ir_band(const FusedBandParams& p, hipStream_t s);
+size_t fused_ir_band_lds(int stride, int hidP, int OW, int blob_bytes, int nslot);
+int fused_ir_band_cols(int stride);
 // Fused stem (3x3 s2, 3 -> 32, relu6, letterbox gather) + MobileNetV2 block 0
 // (dw 3x3 on 32 ch + relu6, project 32 -> 16); weights: ws [32][32] bf16 with
 // K = (ky*3+kx)*3 + c (RGB), bs [32] f32, wd [9][32] f16, bd [32] f16, wp [16][32] f16, bp [16].

@@ -27,6 +27,7 @@ from typing import Callable, Dict, List, Optional, Tuple
 import torch
 import torch.nn as nn
 
+from ..ops import fused_band as FB
 from ..ops import fused_span as FS
 from ..ops import hip_ops as K
 from ..ops.hip_ops import conv_out_hw
@@ -578,8 +579,42 @@ class HipDeepLab:
                     variants.insert(0, (f"span{S}n{npi}", [
                         lambda *_, x=inp, out=out, tab=tab, npi=npi, sp=blk["span"]: FS.fused_ir_span(
                             x, sp, tab, out, B=B, residual=s.residual, npi=npi)]))
+        if blk["expand"] is not None and FB.band_supported(s.cin, hid, s.cout, s.stride, s.dilation):
+            # row-streaming bands: every input row expanded once into an on-chip fp16 row
+            if "band" not in blk:
+                blk["band"] = self._pack_band(blk, s)
+            bp_ = blk["band"]
+            for nslot in (2, 1):
+                if FB.band_lds(bp_, s.stride, OW, nslot) > 160 * 1024:
+                    continue
+                for R in self._band_rows(B, OH, OW, s.stride):
+                    variants.insert(0, (f"band{R}s{nslot}", [
+                        lambda *_, x=inp, out=out, h=h, w=w, R=R, nslot=nslot, bp_=bp_: FB.fused_ir_band(
+                            x, bp_, out, B=B, IH=h, IW=w, stride=s.stride, residual=s.residual, R=R,
+                            nslot=nslot)]))
         outer_ops.append(Choice(f"block{i}", variants))
         return out, OH, OW, s.cout
+
+    def _pack_band(self, blk: dict, s) -> dict:
+        m = blk["module"]
+        ew, eb = m.expand.fold()
+        dwf, dbf = m.dw.fold()
+        pwf, pbf = m.project.fold()
+        return FB.pack_fused_band(ew[:, :, 0, 0], eb, dwf[:, 0], dbf, pwf[:, :, 0, 0], pbf, Cin=s.cin,
+                                  hid=s.hidden, Cout=s.cout, device=self.device)
+
+    @staticmethod
+    def _band_rows(B: int, OH: int, OW: int, stride: int) -> List[int]:
+        """Rows per band for fused_ir_band: grids of ~1-4 workgroups per CU slot (2 per
+        CU x 256 CUs); fewer rows re-expand more halo rows, more rows fill fewer CUs."""
+        nbx = -(-OW // FB.band_cols(stride))
+        out = []
+        for target in (512, 1024, 2048):
+            R = max(2, -(-B * nbx * OH // target))
+            R = min(R, OH)
+            if R not in out:
+                out.append(R)
+        return out
 
     @staticmethod
     def _span_counts(B: int, h: int, w: int) -> List[int]:

@@ -27,6 +27,12 @@ CSRC = os.path.join(ROOT, "csrc")
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 ARCH = os.environ.get("SSA_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# per-source extra flags: MFMA results in VGPRs instead of AGPRs (the kernels whose
+# MFMA epilogues run per fragment on the VALU paid one v_accvgpr_read per result dword)
+EXTRA_FLAGS = {
+    "fused_ir_band.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"],
+    "aspp_head.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"],
+}
 
 
 def _pybind_includes():
@@ -83,7 +89,7 @@ def build_hip(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
     out = os.path.join(HERE, "_hip" + EXT_SUFFIX)
     cflags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fno-gpu-rdc",
               "-Wno-unused-result", "-munsafe-fp-atomics"]
-    stamp = _stamp(hip_srcs + hdrs + [binding], cflags)
+    stamp = _stamp(hip_srcs + hdrs + [binding], cflags + [repr(sorted(EXTRA_FLAGS.items()))])
     if not force and _up_to_date(out, stamp):
         return out
     bdir = os.path.join(ROOT, "build", "hip")
@@ -94,11 +100,12 @@ def build_hip(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
         # per-object cache: a source is recompiled only when it, a header or the flags
         # changed (the full gfx950 build takes ~2 minutes)
         obj = os.path.join(bdir, os.path.basename(src) + ".o")
-        ostamp = _stamp([src] + hdrs, cflags)
+        flags = cflags + EXTRA_FLAGS.get(os.path.basename(src), [])
+        ostamp = _stamp([src] + hdrs, flags)
         if not force and _up_to_date(obj, ostamp):
             return obj
         lang = ["-x", "hip"] if src.endswith(".hip") else []
-        cmd = [HIPCC] + cflags + inc + lang + ["-c", src, "-o", obj + ".tmp"]
+        cmd = [HIPCC] + flags + inc + lang + ["-c", src, "-o", obj + ".tmp"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         _run(cmd)

@@ -1,0 +1,56 @@
+"""CPU tier for the row-streaming fused inverted-residual kernel's host side
+(ops/fused_band.py): the weight blob is unpacked by a numpy re-execution of the
+kernel's data flow and checked against the fp32 torch block."""
+import numpy as np
+import pytest
+import torch
+
+from semantic_segmentation_server_amd.models.layers import init_random
+from semantic_segmentation_server_amd.models.mobilenetv2 import InvertedResidual, IRSpec
+from semantic_segmentation_server_amd.ops import fused_band as FB
+
+
+def band_block(cin, cout, stride, seed):
+    spec = IRSpec(cin, cout, 6, stride, 1)
+    blk = InvertedResidual(spec)
+    init_random(blk, seed=seed)
+    for m in blk.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.uniform_(-0.2, 0.2)
+            m.running_var.uniform_(0.5, 2.0)
+    return blk.eval(), spec
+
+
+def pack_band(blk, spec, device=None):
+    ew, eb = blk.expand.fold()
+    dwf, dbf = blk.dw.fold()
+    pwf, pbf = blk.project.fold()
+    return FB.pack_fused_band(ew[:, :, 0, 0], eb, dwf[:, 0], dbf, pwf[:, :, 0, 0], pbf, Cin=spec.cin,
+                              hid=spec.hidden, Cout=spec.cout, device=device)
+
+
+# the MobileNetV2 blocks 1-6 shapes (Cin, Cout, stride)
+SHAPES = [(16, 24, 2), (24, 24, 1), (24, 32, 2), (32, 32, 1), (32, 64, 2)]
+
+
+@pytest.mark.parametrize("cin,cout,stride", SHAPES)
+def test_band_emulation_matches_block(cin, cout, stride):
+    blk, spec = band_block(cin, cout, stride, seed=cin * 3 + cout)
+    assert FB.band_supported(cin, spec.hidden, cout, stride, 1)
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(2, cin, 13, 11, generator=g).to(torch.bfloat16).float()
+    with torch.no_grad():
+        ref = blk(x).permute(0, 2, 3, 1).numpy()
+    got = FB.emulate_fused_band(x.permute(0, 2, 3, 1).numpy(), pack_band(blk, spec), stride=stride,
+                                residual=spec.residual)
+    rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
+    assert rel < 1e-2, rel
+
+
+def test_band_blob_layout():
+    blk, spec = band_block(24, 24, 1, seed=3)
+    p = pack_band(blk, spec)
+    assert p["hidP"] == 160 and p["blob_bytes"] % 16 == 0
+    offs = [p["o_be"], p["o_wd"], p["o_bd"], p["o_wp"], p["o_bp"]]
+    assert offs == sorted(offs) and all(o % 16 == 0 for o in offs)
+    assert p["o_be"] == 10 * 1024 and p["o_bp"] - p["o_wp"] == 2 * 5 * 1024

@@ -1021,3 +1021,39 @@ def test_aspp_head(M, HW, ncls, ldo, img, G):
     assert torch.isfinite(got).all()
     assert _rel(got[:, :ncls], ref) < 1e-2
     assert torch.all(got[:, ncls:] == 0)
+
+
+@pytest.mark.parametrize("cin,cout,stride,H,W", [
+    (16, 24, 2, 257, 257),   # block 1 (3 column bands, the last 1 column wide)
+    (24, 24, 1, 129, 129),   # block 2 (residual)
+    (24, 32, 2, 129, 129),   # block 3
+    (32, 32, 1, 65, 65),     # blocks 4-5 (residual)
+    (32, 64, 2, 65, 65),     # block 6
+    (24, 24, 1, 23, 37),     # odd map, rows not a multiple of R
+])
+@pytest.mark.parametrize("R,nslot", [(8, 2), (5, 1), (3, 2)])
+def test_fused_ir_band(cin, cout, stride, H, W, R, nslot):
+    """Row-streaming fused block vs the fp32 torch block, and vs the numpy re-execution
+    of its own data flow from the packed blob."""
+    from semantic_segmentation_server_amd.ops import fused_band as FB
+    from test_fused_band_cpu import band_block, pack_band  # tests/ is on sys.path
+    blk, spec = band_block(cin, cout, stride, seed=cin * 5 + cout + stride)
+    g = torch.Generator().manual_seed(31)
+    B = 2
+    x = torch.randn(B, cin, H, W, generator=g).to(torch.bfloat16)
+    with torch.no_grad():
+        ref = blk(x.float())
+    packed = pack_band(blk, spec, device=DEV)
+    if FB.band_lds(packed, stride, (W - 1) // stride + 1, nslot) > 160 * 1024:
+        pytest.skip("LDS")
+    OH, OW = (H - 1) // stride + 1, (W - 1) // stride + 1
+    out = torch.full((B, OH, OW, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
+    FB.fused_ir_band(_nhwc(x).to(DEV), packed, out, B=B, IH=H, IW=W, stride=stride,
+                     residual=spec.residual, R=R, nslot=nslot)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    assert _rel(_nchw(out).cpu(), ref) < 2e-2
+    if H * W <= 129 * 129:
+        emu = FB.emulate_fused_band(_nhwc(x).float().numpy(), packed, stride=stride,
+                                    residual=spec.residual)
+        assert _rel(out.cpu().float(), torch.from_numpy(emu)) < 5e-3
