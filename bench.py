@@ -55,16 +55,22 @@ def main() -> int:
     p.add_argument("--gather", choices=["host", "rccl"], default="host",
                    help="record gather to rank 0: pinned-host + gloo (default) or RCCL")
     p.add_argument("--pg", choices=["auto", "nccl", "gloo"], default="auto",
-                   help="process-group backend; auto: RCCL only when an RCCL data path is "
-                        "requested (--ingest scatter / --gather rccl), else gloo -- an "
-                        "initialised RCCL communicator cost 23%% of single-GPU throughput "
-                        "on MI355X (17.5k vs 22.7k frames/s) with no collective in the loop")
+                   help="process-group backend; auto: RCCL when an RCCL data path is requested "
+                        "(--ingest scatter / --gather rccl), else gloo. Measured on one MI355X "
+                        "(world-size-1 groups, profiles/r2_pg_ab.txt): no group 24.33k, gloo + "
+                        "host gather 24.42k, RCCL + host gather 23.60k, RCCL + RCCL gather "
+                        "24.07k frames/s -- equal within noise; the host gather stays the "
+                        "default (no collective kernel in the GPU stream, rehearsed at dp8)")
     p.add_argument("--contour_mode", choices=["fast", "exact", "none"], default="fast")
     p.add_argument("--no-graph", dest="graph", action="store_false")
     p.add_argument("--rpc", type=int, default=2000, help="GetSegmentedObjects calls to time (0: skip)")
     p.add_argument("--dtype", default="bf16")
     p.add_argument("--streams", type=int, default=1,
-                   help="concurrent camera streams per GPU, each with its own HIP stream + hipGraph")
+                   help="concurrent camera streams per GPU: their frames fill one batched step "
+                        "(one hipGraph; records tagged with their stream id)")
+    p.add_argument("--per_stream_graphs", action="store_true",
+                   help="config-5 alternative: one engine + HIP stream + hipGraph per camera "
+                        "stream (measured slower than the batched step, kept for comparison)")
     p.add_argument("--serve", action="store_true",
                    help="time the real serving loop (Server / DistributedServer: feeder thread, "
                         "pinned ring, lag-1 pipeline, gRPC services up) instead of the bench loop")
@@ -90,7 +96,7 @@ def main() -> int:
                    ingest=a.ingest, camera_width=cam_w, camera_height=cam_h,
                    num_classes=21 if a.arch == "mnv2" else 19,
                    dataset="pascal" if a.arch == "mnv2" else "cityscapes")
-    if a.streams > 1:
+    if a.streams > 1 and a.per_stream_graphs:
         from semantic_segmentation_server_amd.runtime.multistream import StreamGroup
         engine = StreamGroup(cfg, ctx.device, a.streams)
     else:
@@ -184,6 +190,8 @@ def main() -> int:
                 "hipgraph": bool(a.graph and ctx.device.type == "cuda"),
                 "contour_mode": a.contour_mode,
                 "streams_per_gpu": a.streams,
+                "stream_mode": "per-stream graphs" if (a.streams > 1 and a.per_stream_graphs)
+                else "batched",
             },
             "p50_get_segmented_objects_ms": rpc.get("p50_ms") if rpc else None,
             "p99_get_segmented_objects_ms": rpc.get("p99_ms") if rpc else None,
