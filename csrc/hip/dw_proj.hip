@@ -199,7 +199,14 @@ __device__ __attribute__((aligned(16))) int4 g_dwp_zero[8];
 // rows overlap, so the re-reads hit that XCD's L2).
 template <int NS, int ST>
 __global__ __launch_bounds__(1024) void dw_proj_rows_kernel(DPPArgs a, int TY, int HPP, int xcd) {
-  // HPP: halo pixels rounded up to 16 (one 1 KiB DMA piece per 16 pixels)
+  // HPP: halo pixels rounded up to 64. The halo chunk is stored as 4 channel-octet
+  // PLANES [octet][HPP pixels][16 B] (plane stride HPP * 16 B, a multiple of 1 KiB):
+  // a depthwise ds_read_b128 lane group reads 16 distinct consecutive pixels of ONE
+  // 16-byte bank slot column each, so it is conflict-free. Round 1 stored pixels as
+  // 64-byte rows of all 4 octets: the 16 pixels of a lane group hit only 4 bank slots
+  // (2-way conflicts on every depthwise read, ~1 conflict cycle per LDS instruction in
+  // profiles/r1_hip_v10_pmc_summary.txt). One 1 KiB LDS-DMA piece = 64 pixels of one
+  // octet plane (piece j: octet j % 4, pixels (j / 4) * 64 ..).
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int WB = (NS + 1) * 1024;            // weight image per chunk
   const int BUF = HPP * 64 + WB;             // halo [HPP][32 ch fp16] + weights
@@ -215,7 +222,8 @@ __global__ __launch_bounds__(1024) void dw_proj_rows_kernel(DPPArgs a, int TY, i
   const int p = wid * 16 + r16;
   const int py = p / a.OW, px = p - py * a.OW;
   const bool pv = p < TY * a.OW && oy0 + py < a.OH;
-  const int dwbase = (pv ? (py * HWW + px) * 64 : 0) + kq * 16;  // halo byte offset of tap (0,0)
+  const int PLANE = HPP * 16;
+  const int dwbase = (pv ? (py * HWW + px) * 16 : 0) + kq * PLANE;  // halo byte offset of tap (0,0)
   const int m = (b * a.OH + oy0 + py) * a.OW + px;
   // DMA sources of this wave's halo pieces (element offsets for channel 0, -1: zero page)
   const int npieces = HPP / 16;
@@ -224,11 +232,11 @@ __global__ __launch_bounds__(1024) void dw_proj_rows_kernel(DPPArgs a, int TY, i
 #pragma unroll
   for (int k = 0; k < MAXP; ++k) {
     const int piece = wid + k * NW;
-    const int hp = piece * 16 + (lane >> 2);
+    const int hp = (piece >> 2) * 64 + lane, oct = piece & 3;
     const int hy = hp / HWW, hx = hp - hy * HWW;
     const int iy = oy0 - dl + hy, ix = hx - dl;
     const bool ok = piece < npieces && hy < TY + 2 * dl && iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW;
-    hsrc[k] = ok ? ((b * a.IH + iy) * a.IW + ix) * a.hid + (lane & 3) * 8 : -1;
+    hsrc[k] = ok ? ((b * a.IH + iy) * a.IW + ix) * a.hid + oct * 8 : -1;
   }
   const int nchunks = a.hid / 32;
   auto issue = [&](int c, int buf) {
@@ -238,7 +246,7 @@ __global__ __launch_bounds__(1024) void dw_proj_rows_kernel(DPPArgs a, int TY, i
       const int piece = wid + k * NW;
       if (piece < npieces) {
         const void* src = hsrc[k] >= 0 ? (const void*)(a.h + hsrc[k] + c * 32) : (const void*)g_dwp_zero;
-        __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(dst + piece * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(dst + (piece & 3) * PLANE + (piece >> 2) * 1024), 16, 0, 0);
       }
     }
     const char* wsrc = reinterpret_cast<const char*>(a.w) + (size_t)c * WB + lane * 16;
@@ -250,7 +258,7 @@ __global__ __launch_bounds__(1024) void dw_proj_rows_kernel(DPPArgs a, int TY, i
   f32x4 acc[NS];
 #pragma unroll
   for (int n = 0; n < NS; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int trow = dl * HWW * 64, tcol = dl * 64;  // tap strides (bytes)
+  const int trow = dl * HWW * 16, tcol = dl * 16;  // tap strides (bytes, within an octet plane)
 
   // DMA instructions this wave issues per chunk (wave-uniform, fixed over chunks)
   int kw = 0;
@@ -337,7 +345,7 @@ __global__ __launch_bounds__(1024) void dw_proj_rows_kernel(DPPArgs a, int TY, i
 template <int NS, int ST>
 void launch_dwp_rows_st(const DPPArgs& a, int TY, int xcd, hipStream_t s) {
   const int HP = (TY + 2 * a.dil) * (a.OW + 2 * a.dil);
-  const int HPP = (HP + 15) / 16 * 16;
+  const int HPP = (HP + 63) / 64 * 64;
   const int nw = (TY * a.OW + 15) / 16;
   const size_t lds = ST * ((size_t)HPP * 64 + (NS + 1) * 1024);
   if (nw > 16 || lds > 160 * 1024 || HPP / 16 > 4 * nw)

@@ -151,10 +151,12 @@ def pw_choice(name: str, gemm_op: Callable, x: torch.Tensor, w: torch.Tensor, b:
 
 def _dwp_rows_fit(ty: int, stages: int, dil: int, OW: int, cout: int) -> bool:
     """dw_proj_rows tile (ty rows x OW, <= 16 waves) and its LDS ring fit the CU."""
-    if -(-ty * OW // 16) > 16:
+    nw = -(-ty * OW // 16)
+    if nw > 16:
         return False
-    halo = (ty + 2 * dil) * (OW + 2 * dil)
-    return stages * ((-(-halo // 16) * 16) * 64 + (cout // 16 + 1) * 1024) <= 160 * 1024
+    halo = -(-(ty + 2 * dil) * (OW + 2 * dil) // 64) * 64  # octet planes of 64-pixel DMA pieces
+    return (halo // 16 <= 4 * nw and
+            stages * (halo * 64 + (cout // 16 + 1) * 1024) <= 160 * 1024)
 
 
 class HipDeepLab:
