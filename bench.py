@@ -43,8 +43,8 @@ def _client_proc(port: int, n: int, conn) -> None:
 def main() -> int:
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
     p.add_argument("--backend", choices=["hip", "torch"], default="hip")
     p.add_argument("--arch", default="mnv2")

@@ -16,7 +16,7 @@
 //                "outside" node 0
 //   k_compress   label = root with path halving (root = raster index of the
 //                component's first pixel + 1, 0 = outside)
-//   k_roots      per component: zero accumulators, parent in the border tree
+//                (component roots: zero accumulators)
 //   k_quads      per 2x2 quad: polygon pieces (full square / triangle) as exact
 //                integer moments a00 = 2A, a10 = 6*int x, a01 = 6*int y
 //   k_tree       subtree sums: every component adds its own pieces to all its
@@ -525,19 +525,27 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(KArgs a) {
 
 // Cross-tile merges (and image-border background -> outside node 0). Only
 // pixels on a tile's left column / top row or on the image border do work.
+// Launched with a small grid per frame (grid-stride over the pixels): frames the LDS
+// merge handled (nearly all) leave after ONE flag load per workgroup instead of a
+// full-frame grid of early-exiting threads (18 us per 32 frames in round 1).
+__device__ __forceinline__ void ccl_boundary_pixel(KArgs& a, FrameWS& f, int p);
+
 __global__ __launch_bounds__(256) void k_ccl_boundary(KArgs a) {
   const int b = blockIdx.y;
   const int N = a.ch * a.cw;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= N) return;
-  if (frame_ws(a.ws, a.lay, a.B, b).flag[0] == 0) return;  // merged in LDS
+  FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
+  if (f.flag[0] == 0) return;  // merged in LDS
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < N; p += gridDim.x * blockDim.x)
+    ccl_boundary_pixel(a, f, p);
+}
+
+__device__ __forceinline__ void ccl_boundary_pixel(KArgs& a, FrameWS& f, int p) {
   const int y = p / a.cw, x = p - y * a.cw;
   const bool left = x > 0 && (x % TW) == 0;
   const bool top = y > 0 && (y % TH) == 0;
   const bool edge = x == 0 || y == 0 || x == a.cw - 1 || y == a.ch - 1;
   const bool rtile = (x % TW) == TW - 1 && x + 1 < a.cw && y > 0;  // up-right neighbour in next tile
   if (!left && !top && !edge && !rtile) return;
-  FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
   const uint8_t m = f.mask[p];
   const int me = p + 1;
   // Skip unions already implied by the previous pixel along the same tile edge:
@@ -588,40 +596,34 @@ __global__ __launch_bounds__(256) void k_compress(KArgs a) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= N) return;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
+  int r;
   if (f.flag[0] == 0) {  // compact merge: pixel -> its tile-local root -> final label
     const int lr = f.L[p + 1] - 1;
     const int ly = lr / a.cw, lx = lr - ly * a.cw;
     const int tx_n = (a.cw + TW - 1) / TW;
     const int t = (ly / TH) * tx_n + lx / TW;
-    f.L[p + 1] = f.clabel[f.toff[t] + f.cidx[lr]];
-    return;
+    r = f.clabel[f.toff[t] + f.cidx[lr]];
+    f.L[p + 1] = r;
+  } else {
+    // Read-only traversal: a path-halving store here could overwrite another
+    // thread's final root store with a stale grandparent (observed: 1 pixel in ~1M
+    // left pointing at a non-root). Every concurrent store below writes a root, so
+    // plain traversal always terminates at the true root.
+    r = find_root(f.L, p + 1);
+    __hip_atomic_store(f.L + p + 1, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // Read-only traversal: a path-halving store here could overwrite another
-  // thread's final root store with a stale grandparent (observed: 1 pixel in ~1M
-  // left pointing at a non-root). Every concurrent store below writes a root, so
-  // plain traversal always terminates at the true root.
-  const int r = find_root(f.L, p + 1);
-  __hip_atomic_store(f.L + p + 1, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// ---------------------------------------------------------------- roots
-__global__ __launch_bounds__(256) void k_roots(KArgs a) {
-  const int b = blockIdx.y;
-  const int N = a.ch * a.cw;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= N) return;
-  FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
-  if (f.L[p + 1] != p + 1) return;  // not a root (or outside)
-  const int x = p % a.cw;
-  // parent = component of the left neighbour of the first pixel (0 at the border)
-  f.parent[p] = x > 0 ? f.L[p] : 0;
-  f.slot[p] = -1;
-  f.a00[p] = 0;
-  f.t00[p] = 0;
-  f.a10[p] = 0;
-  f.a01[p] = 0;
-  f.t10[p] = 0;
-  f.t01[p] = 0;
+  // the component's first pixel (its label is its own raster index + 1): zero its
+  // accumulators here (round 1 spent a separate full-frame pass, k_roots, on this;
+  // the parent link needs every final label and is set by k_tree)
+  if (r == p + 1) {
+    f.slot[p] = -1;
+    f.a00[p] = 0;
+    f.t00[p] = 0;
+    f.a10[p] = 0;
+    f.a01[p] = 0;
+    f.t10[p] = 0;
+    f.t01[p] = 0;
+  }
 }
 
 // Per-block privatisation of the component sums. A real scene's mask has a few
@@ -778,6 +780,11 @@ __global__ __launch_bounds__(256) void k_tree(KArgs a) {
   if (p >= N) return;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
   if (f.L[p + 1] != p + 1) return;
+  // parent in the border tree = component of the left neighbour of the first pixel
+  // (0 at the image border); a pure function of the final labels, so the ancestor walk
+  // below evaluates it directly instead of reading links other threads are writing
+  auto parent_of = [&](int n) { return (n - 1) % a.cw > 0 ? f.L[n - 1] : 0; };
+  f.parent[p] = parent_of(p + 1);
   const int o00 = f.a00[p];
   const long long o10 = f.a10[p], o01 = f.a01[p];
   if (o00 == 0 && o10 == 0 && o01 == 0) return;
@@ -786,7 +793,7 @@ __global__ __launch_bounds__(256) void k_tree(KArgs a) {
     atomicAdd(f.t00 + n - 1, o00);
     atomicAdd(reinterpret_cast<unsigned long long*>(f.t10 + n - 1), (unsigned long long)o10);
     atomicAdd(reinterpret_cast<unsigned long long*>(f.t01 + n - 1), (unsigned long long)o01);
-    n = f.parent[n - 1];
+    n = parent_of(n);
   }
 }
 
@@ -1157,9 +1164,8 @@ void postprocess(const PostParams& p, hipStream_t s) {
     }
     if (st++ < stages) hipLaunchKernelGGL(k_ccl_merge, dim3(p.B), dim3(1024), lds, s, a);
   }
-  if (st++ < stages) hipLaunchKernelGGL(k_ccl_boundary, gp, blk, 0, s, a);
+  if (st++ < stages) hipLaunchKernelGGL(k_ccl_boundary, dim3(std::min(cdiv(N, 256), 64), p.B), blk, 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_compress, gp, blk, 0, s, a);
-  if (st++ < stages) hipLaunchKernelGGL(k_roots, gp, blk, 0, s, a);
   // strip-privatised passes: kQuadBlocks strips per frame (SSA_QUAD_BLOCKS overrides, tuning)
   const char* qb_env = getenv("SSA_QUAD_BLOCKS");
   const int qblocks = qb_env ? std::max(1, atoi(qb_env)) : kQuadBlocks;
