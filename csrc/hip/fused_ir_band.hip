@@ -44,13 +44,12 @@ typedef _Float16 f16;
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int kBW = 4;           // waves per workgroup
-constexpr int kBT = 64 * kBW;    // threads
-// output columns per band: the band's input columns ((TW - 1) * S + 3) fill exactly
-// 64 (stride 1) / 128 (stride 2) pixels = 1 / 2 whole MFMA pixel groups per wave, so no
-// wave carries an idle expansion group (the lanes of the 16th output column of wave 3,
-// stride 1, and of its 16th, stride 2... are masked instead)
-__host__ __device__ constexpr int band_cols(int S) { return S == 1 ? 62 : 63; }
+// A band spans the FULL map width: NW = ceil(OW / 16) waves, wave w owning output
+// columns 16w..16w+15 (9 waves at 129 columns, 5 at 65, 3 at 33). Round-2's first
+// version cut 62/63-column bands, and the odd map widths (2^k + 1) left a last band of
+// 1-5 columns running a whole workgroup. The band's input row ((OW - 1) * S + 3 pixels)
+// then fills ceil(IWT / 16) MFMA pixel groups, S per wave at most.
+__host__ __device__ constexpr int band_waves(int OW) { return (OW + 15) / 16; }
 
 struct BandArgs {
   const bf16* in; const char* blob; bf16* out;
@@ -76,14 +75,15 @@ __device__ __forceinline__ void lds_barrier() {
 // relu6 scale: expansion weights and bias and the depthwise bias come divided by 6, the
 // projection weights multiplied by 6, so both relu6 become [0, 1] clamps that fold into
 // the clamp bit of the instruction producing the value (E' = E / 6, D' = D / 6).
-template <int S, int NSH, int NS, int NSLOT>
-__global__ __launch_bounds__(kBT) void fused_ir_band_kernel(BandArgs a) {
+template <int S, int NSH, int NS, int NSLOT, int NW>
+__global__ __launch_bounds__(64 * NW) void fused_ir_band_kernel(BandArgs a) {
+  constexpr int kBW = NW, kBT = 64 * NW;
   constexpr int NCH = NSH / 2;            // 32-channel hidden chunks
   constexpr int HID = NSH * 16;
   constexpr int NDS = S == 1 ? 3 : 2;     // open output rows (D accumulator slots)
   constexpr int U = S == 1 ? 3 : 4;       // step unroll: static slot roles
-  constexpr int GI = S;                   // input pixel groups per wave per row (IWT <= 64 / 128)
-  constexpr int kTW = band_cols(S);
+  constexpr int GI = S;                   // input pixel groups per wave per row
+  constexpr int kTW = 16 * NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -292,16 +292,16 @@ __global__ __launch_bounds__(kBT) void fused_ir_band_kernel(BandArgs a) {
   }
 }
 
-template <int S, int NSH, int NS, int NSLOT>
+template <int S, int NSH, int NS, int NSLOT, int NW>
 void launch_band(const BandArgs& a, size_t lds, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_ir_band_kernel<S, NSH, NS, NSLOT>),
+    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_ir_band_kernel<S, NSH, NS, NSLOT, NW>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
           "fused_ir_band attr");
     attr = true;
   }
-  hipLaunchKernelGGL((fused_ir_band_kernel<S, NSH, NS, NSLOT>), dim3(a.B * a.nby * a.nbx), dim3(kBT), lds,
+  hipLaunchKernelGGL((fused_ir_band_kernel<S, NSH, NS, NSLOT, NW>), dim3(a.B * a.nby * a.nbx), dim3(64 * NW), lds,
                      st, a);
   check_launch("fused_ir_band");
 }
@@ -312,7 +312,7 @@ struct BandGeom {
 
 BandGeom band_geom(int stride, int hidP, int OW) {
   BandGeom g;
-  const int tw = OW < band_cols(stride) ? OW : band_cols(stride);
+  const int tw = OW;
   g.IWT = (tw - 1) * stride + 3;
   g.P = hidP * 2 + 16;
   if (stride == 1) {
@@ -334,7 +334,7 @@ size_t fused_ir_band_lds(int stride, int hidP, int OW, int blob_bytes, int nslot
   return (size_t)((blob_bytes + 15) & ~15) + (size_t)nslot * g.EROW;
 }
 
-int fused_ir_band_cols(int stride) { return band_cols(stride); }
+int fused_ir_band_cols(int stride) { (void)stride; return 0; }  // full map width
 
 void fused_ir_band(const FusedBandParams& p, hipStream_t st) {
   if (p.stride != 1 && p.stride != 2) throw std::invalid_argument("fused_ir_band: stride 1 or 2");
@@ -346,18 +346,20 @@ void fused_ir_band(const FusedBandParams& p, hipStream_t st) {
   const size_t lds = fused_ir_band_lds(p.stride, p.hidP, p.OW, p.blob_bytes, p.nslot);
   if (lds > 160 * 1024) throw std::invalid_argument("fused_ir_band: LDS over 160 KiB");
   BandArgs a{p.in, reinterpret_cast<const char*>(p.blob), p.out, p.B, p.IH, p.IW, p.Cin, p.OH, p.OW, p.Cout,
-             p.residual, p.R, cdiv(p.OW, band_cols(p.stride)), cdiv(p.OH, p.R), g.HE, g.P, g.EROW, p.blob_bytes,
+             p.residual, p.R, 1, cdiv(p.OH, p.R), g.HE, g.P, g.EROW, p.blob_bytes,
              p.o_be, p.o_wd, p.o_bd, p.o_wp, p.o_bp};
   const int NSH = p.hidP / 16, NS = (p.Cout + 15) / 16;
-#define BAND(S_, NSH_, NS_)                                                     \
-  if (p.stride == S_ && NSH == NSH_ && NS == NS_) {                             \
-    if (p.nslot == 2) launch_band<S_, NSH_, NS_, 2>(a, lds, st);                \
-    else launch_band<S_, NSH_, NS_, 1>(a, lds, st);                             \
-    return;                                                                     \
+  const int NW = band_waves(p.OW);
+#define BAND(S_, NSH_, NS_, NW_)                                                 \
+  if (p.stride == S_ && NSH == NSH_ && NS == NS_ && NW == NW_) {                 \
+    if (p.nslot == 2) launch_band<S_, NSH_, NS_, 2, NW_>(a, lds, st);            \
+    else launch_band<S_, NSH_, NS_, 1, NW_>(a, lds, st);                         \
+    return;                                                                      \
   }
   // block 1 (16 -> 96 -> 24, s2), 2 (24 -> 144 -> 24), 3 (24 -> 144 -> 32, s2),
   // 4-5 (32 -> 192 -> 32), 6 (32 -> 192 -> 64, s2); hidden 144 runs padded to 160
-  BAND(2, 6, 2) BAND(1, 10, 2) BAND(2, 10, 2) BAND(1, 12, 2) BAND(2, 12, 4)
+  // (map widths at 513^2: 129, 129, 65, 65, 33)
+  BAND(2, 6, 2, 9) BAND(1, 10, 2, 9) BAND(2, 10, 2, 5) BAND(1, 12, 2, 5) BAND(2, 12, 4, 3)
 #undef BAND
   throw std::invalid_argument("fused_ir_band: no instantiation for this (stride, hidden, Cout)");
 }

@@ -581,7 +581,7 @@ class HipDeepLab:
                     variants.insert(0, (f"span{S}n{npi}", [
                         lambda *_, x=inp, out=out, tab=tab, npi=npi, sp=blk["span"]: FS.fused_ir_span(
                             x, sp, tab, out, B=B, residual=s.residual, npi=npi)]))
-        if blk["expand"] is not None and FB.band_supported(s.cin, hid, s.cout, s.stride, s.dilation):
+        if blk["expand"] is not None and FB.band_supported(s.cin, hid, s.cout, s.stride, s.dilation, OW):
             # row-streaming bands: every input row expanded once into an on-chip fp16 row
             if "band" not in blk:
                 blk["band"] = self._pack_band(blk, s)
@@ -607,13 +607,12 @@ class HipDeepLab:
 
     @staticmethod
     def _band_rows(B: int, OH: int, OW: int, stride: int) -> List[int]:
-        """Rows per band for fused_ir_band: grids of ~1-4 workgroups per CU slot (2 per
-        CU x 256 CUs); fewer rows re-expand more halo rows, more rows fill fewer CUs."""
-        nbx = -(-OW // FB.band_cols(stride))
+        """Rows per band for fused_ir_band (full-width bands): grids of ~1-4 workgroups
+        per CU slot (2 per CU x 256 CUs); fewer rows re-expand more halo rows, more rows
+        fill fewer CUs."""
         out = []
-        for target in (512, 1024, 2048):
-            R = max(2, -(-B * nbx * OH // target))
-            R = min(R, OH)
+        for target in (256, 512, 1024):
+            R = min(max(2, -(-B * OH // target)), OH)
             if R not in out:
                 out.append(R)
         return out

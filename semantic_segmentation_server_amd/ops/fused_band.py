@@ -1,8 +1,8 @@
 """Host side of the row-streaming fused inverted-residual kernel (csrc/hip/fused_ir_band.hip).
 
 The kernel runs one MobileNetV2 inverted residual with Cin <= 32, stride 1 or 2 and
-dilation 1 (blocks 1-6 of DeepLabv3-MobileNetV2) over bands of R output rows x 62
-(stride 1) / 63 (stride 2) columns, expanding each input row once into an on-chip fp16
+dilation 1 (blocks 1-6 of DeepLabv3-MobileNetV2) over bands of R full-width output rows
+(ceil(OW / 16) waves), expanding each input row once into an on-chip fp16
 row and accumulating the depthwise per row in registers. This module builds the one
 weight blob the kernel copies into LDS, launches it, and re-executes its data flow in
 numpy from the packed bytes (CPU tests of the packing without a GPU).
@@ -29,20 +29,16 @@ from typing import Dict
 import numpy as np
 import torch
 
-# (stride, hidP / 16, ceil(Cout / 16)) instantiated in fused_ir_band.hip
-BAND_SHAPES = {(2, 6, 2), (1, 10, 2), (2, 10, 2), (1, 12, 2), (2, 12, 4)}
+# (stride, hidP / 16, ceil(Cout / 16), waves = ceil(OW / 16)) instantiated in
+# fused_ir_band.hip: blocks 1-6 at 513^2 (output widths 129, 129, 65, 65, 65, 33)
+BAND_SHAPES = {(2, 6, 2, 9), (1, 10, 2, 9), (2, 10, 2, 5), (1, 12, 2, 5), (2, 12, 4, 3)}
 
 
-def band_cols(stride: int) -> int:
-    """Output columns per band (fused_ir_band.hip band_cols): the band's input columns
-    fill whole 16-pixel MFMA groups, 1 (stride 1) or 2 (stride 2) per wave."""
-    return 62 if stride == 1 else 63
-
-
-def band_supported(cin: int, hid: int, cout: int, stride: int, dil: int) -> bool:
+def band_supported(cin: int, hid: int, cout: int, stride: int, dil: int, OW: int) -> bool:
+    """A band spans the full output width OW (ceil(OW / 16) waves of 16 columns)."""
     hidP = -(-hid // 32) * 32
     return (dil == 1 and cin <= 32 and cin % 8 == 0 and stride in (1, 2)
-            and (stride, hidP // 16, -(-cout // 16)) in BAND_SHAPES)
+            and (stride, hidP // 16, -(-cout // 16), -(-OW // 16)) in BAND_SHAPES)
 
 
 def _al(n: int) -> int:
@@ -105,7 +101,7 @@ def fused_ir_band(x: torch.Tensor, packed: Dict, out: torch.Tensor, *, B: int, I
         raise ValueError("fused_ir_band: residual needs stride 1 and Cin == Cout")
     if nslot not in (1, 2) or R < 1:
         raise ValueError("fused_ir_band: nslot 1 or 2, R >= 1")
-    if not band_supported(Cin, packed["hid"], Cout, stride, 1):
+    if not band_supported(Cin, packed["hid"], Cout, stride, 1, OW):
         raise ValueError("fused_ir_band: no instantiation for this block")
     _chk(x, torch.bfloat16, "x", B * IH * IW * Cin)
     _chk(out, torch.bfloat16, "out", B * OH * OW * Cout)

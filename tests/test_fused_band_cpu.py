@@ -30,13 +30,13 @@ def pack_band(blk, spec, device=None):
 
 
 # the MobileNetV2 blocks 1-6 shapes (Cin, Cout, stride)
-SHAPES = [(16, 24, 2), (24, 24, 1), (24, 32, 2), (32, 32, 1), (32, 64, 2)]
+SHAPES = [(16, 24, 2, 129), (24, 24, 1, 129), (24, 32, 2, 65), (32, 32, 1, 65), (32, 64, 2, 33)]
 
 
-@pytest.mark.parametrize("cin,cout,stride", SHAPES)
-def test_band_emulation_matches_block(cin, cout, stride):
+@pytest.mark.parametrize("cin,cout,stride,OW", SHAPES)
+def test_band_emulation_matches_block(cin, cout, stride, OW):
     blk, spec = band_block(cin, cout, stride, seed=cin * 3 + cout)
-    assert FB.band_supported(cin, spec.hidden, cout, stride, 1)
+    assert FB.band_supported(cin, spec.hidden, cout, stride, 1, OW)
     g = torch.Generator().manual_seed(2)
     x = torch.randn(2, cin, 13, 11, generator=g).to(torch.bfloat16).float()
     with torch.no_grad():

@@ -1029,7 +1029,8 @@ def test_aspp_head(M, HW, ncls, ldo, img, G):
     (24, 32, 2, 129, 129),   # block 3
     (32, 32, 1, 65, 65),     # blocks 4-5 (residual)
     (32, 64, 2, 65, 65),     # block 6
-    (24, 24, 1, 23, 37),     # odd map, rows not a multiple of R
+    (24, 24, 1, 100, 129),   # rows not a multiple of R
+    (32, 32, 1, 7, 65),      # fewer rows than R
 ])
 @pytest.mark.parametrize("R,nslot", [(8, 2), (5, 1), (3, 2)])
 def test_fused_ir_band(cin, cout, stride, H, W, R, nslot):
@@ -1046,6 +1047,7 @@ def test_fused_ir_band(cin, cout, stride, H, W, R, nslot):
     packed = pack_band(blk, spec, device=DEV)
     if FB.band_lds(packed, stride, (W - 1) // stride + 1, nslot) > 160 * 1024:
         pytest.skip("LDS")
+    assert FB.band_supported(cin, spec.hidden, cout, stride, 1, (W - 1) // stride + 1)
     OH, OW = (H - 1) // stride + 1, (W - 1) // stride + 1
     out = torch.full((B, OH, OW, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
     FB.fused_ir_band(_nhwc(x).to(DEV), packed, out, B=B, IH=H, IW=W, stride=stride,
