@@ -290,6 +290,12 @@ PYBIND11_MODULE(_hip, m) {
            S(stream));
   });
 
+  m.def("aspp_pool", [](uintptr_t in, uintptr_t ws, uintptr_t w1t, uintptr_t b1, uintptr_t w2t,
+                        uintptr_t img_bias, int B, int HW, int C, int N, uintptr_t stream) {
+    aspp_pool(P<const bf16>(in), P<float>(ws), P<const float>(w1t), P<const float>(b1), P<const float>(w2t),
+              P<float>(img_bias), B, HW, C, N, S(stream));
+  });
+
   m.def("upsample_argmax", [](uintptr_t logits, uintptr_t labels, int B, int h, int w, int K,
                               int ldk, int H, int W, uintptr_t stream, int variant) {
     upsample_argmax(P<const bf16>(logits), P<uint8_t>(labels), B, h, w, K, ldk, H, W, S(stream),

@@ -244,6 +244,8 @@ void global_avgpool(const bf16* in, float* out, float* ws, int B, int HW, int C,
 // out = act(in + bias[n] + img_bias[m / HW][n]) over an [M, N] bf16 matrix (GEMM epilogue)
 void bias_act(const bf16* in, const float* bias, const float* img_bias, bf16* out, long long M, int N,
               int HW, int act, hipStream_t s);
+void aspp_pool(const bf16* in, float* ws, const float* w1t, const float* b1, const float* w2t,
+               float* img_bias, int B, int HW, int C, int N, hipStream_t s);
 void matvec(const float* x, const float* w, const float* bias, float* out, int B, int N, int K,
             int act, hipStream_t s);
 

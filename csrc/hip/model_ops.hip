@@ -518,6 +518,70 @@ void matvec(const float* x, const float* w, const float* bias, float* out, int B
   check_launch("matvec");
 }
 
+// ---------------------------------------------------------------- ASPP image-pooling branch
+// The whole branch after the pixel sums in ONE workgroup per image (was gap_reduce +
+// two matvec launches, ~3 x 10 us of launch-bound kernels per step for ~0.3 MFLOP):
+//   gap[k]      = sum_s part[b][s][k] / HW                    (LDS)
+//   pooled[n]   = relu(sum_k w1t[k][n] gap[k] + b1[n])         (LDS)
+//   img_bias[n] = sum_k w2t[k][n] pooled[k]                   (-> projection epilogue)
+// Weights are host-transposed [K][N] so a lane per output channel reads a coalesced
+// 1 KiB row per k; four independent partial sums per lane keep loads in flight.
+constexpr int kPoolMaxC = 2048, kPoolMaxN = 512;
+
+__global__ __launch_bounds__(256) void aspp_pool_kernel(const float* __restrict__ part,
+                                                        const float* __restrict__ w1t,
+                                                        const float* __restrict__ b1,
+                                                        const float* __restrict__ w2t,
+                                                        float* __restrict__ img_bias, int HW, int C,
+                                                        int N) {
+  __shared__ float s_gap[kPoolMaxC];
+  __shared__ float s_pool[kPoolMaxN];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float inv = 1.f / (float)HW;
+  const float* pb = part + (size_t)b * kGapSlices * C;
+  for (int k = tid; k < C; k += 256) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < kGapSlices; ++q) s += pb[(size_t)q * C + k];
+    s_gap[k] = s * inv;
+  }
+  __syncthreads();
+  for (int n = tid; n < N; n += 256) {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int k = 0;
+    for (; k + 4 <= C; k += 4) {
+      s0 += w1t[(size_t)k * N + n] * s_gap[k];
+      s1 += w1t[(size_t)(k + 1) * N + n] * s_gap[k + 1];
+      s2 += w1t[(size_t)(k + 2) * N + n] * s_gap[k + 2];
+      s3 += w1t[(size_t)(k + 3) * N + n] * s_gap[k + 3];
+    }
+    for (; k < C; ++k) s0 += w1t[(size_t)k * N + n] * s_gap[k];
+    s_pool[n] = fmaxf((s0 + s1) + (s2 + s3) + b1[n], 0.f);
+  }
+  __syncthreads();
+  for (int n = tid; n < N; n += 256) {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int k = 0;
+    for (; k + 4 <= N; k += 4) {
+      s0 += w2t[(size_t)k * N + n] * s_pool[k];
+      s1 += w2t[(size_t)(k + 1) * N + n] * s_pool[k + 1];
+      s2 += w2t[(size_t)(k + 2) * N + n] * s_pool[k + 2];
+      s3 += w2t[(size_t)(k + 3) * N + n] * s_pool[k + 3];
+    }
+    for (; k < N; ++k) s0 += w2t[(size_t)k * N + n] * s_pool[k];
+    img_bias[(size_t)b * N + n] = (s0 + s1) + (s2 + s3);
+  }
+}
+
+void aspp_pool(const bf16* in, float* ws, const float* w1t, const float* b1, const float* w2t,
+               float* img_bias, int B, int HW, int C, int N, hipStream_t s) {
+  if (C > kPoolMaxC || N > kPoolMaxN || C % 8) throw std::invalid_argument("aspp_pool: C <= 2048, C % 8, N <= 512");
+  hipLaunchKernelGGL(gap_partial_kernel, dim3(B, kGapSlices, cdiv(C / 8, 64)), dim3(256), 0, s, in,
+                     ws, HW, C);
+  hipLaunchKernelGGL(aspp_pool_kernel, dim3(B), dim3(256), 0, s, ws, w1t, b1, w2t, img_bias, HW, C, N);
+  check_launch("aspp_pool");
+}
+
 // ---------------------------------------------------------------- upsample + argmax
 // Logits of one frame (h x w x K, ~50 KB at 33x33x24 bf16) stay L1/L2 resident;
 // each lane produces 4 consecutive output pixels of a row and one 4-byte store.

@@ -345,16 +345,24 @@ class HipDeepLab:
             ops[aspp_at:] = [Choice("aspp.branches", grouped + [seq])]
         img_bias = None
         if self.has_pool:
-            gap = buf("gap", B, c, dtype=torch.float32)
-            pooled = buf("pooled", B, A, dtype=torch.float32)
             img_bias = buf("img_bias", B, A, dtype=torch.float32)
             gws = K.gap_workspace(B, c, dev)
             bufs["gap_ws"] = gws
-            ops.append(lambda *_, x=x, h=h, w=w, c=c: K.global_avgpool(x, gap, B=B, HW=h * w, C=c,
-                                                                       ws=gws))
-            ops.append(lambda *_, c=c: K.matvec(gap, self.pool_w, self.pool_b, pooled, B=B, N=A,
-                                                K=c, act="relu"))
-            ops.append(lambda *_: K.matvec(pooled, self.proj_pool_w, None, img_bias, B=B, N=A, K=A))
+            if c <= 2048 and A <= 512 and c % 8 == 0:
+                # GAP partials + one per-image kernel for the pooled MLP (aspp_pool)
+                w1t = self.pool_w.t().contiguous()
+                w2t = self.proj_pool_w.t().contiguous()
+                bufs["pool_w1t"], bufs["pool_w2t"] = w1t, w2t
+                ops.append(lambda *_, x=x, h=h, w=w, c=c, w1t=w1t, w2t=w2t: K.aspp_pool(
+                    x, gws, w1t, self.pool_b, w2t, img_bias, B=B, HW=h * w, C=c, N=A))
+            else:
+                gap = buf("gap", B, c, dtype=torch.float32)
+                pooled = buf("pooled", B, A, dtype=torch.float32)
+                ops.append(lambda *_, x=x, h=h, w=w, c=c: K.global_avgpool(x, gap, B=B, HW=h * w, C=c,
+                                                                           ws=gws))
+                ops.append(lambda *_, c=c: K.matvec(gap, self.pool_w, self.pool_b, pooled, B=B, N=A,
+                                                    K=c, act="relu"))
+                ops.append(lambda *_: K.matvec(pooled, self.proj_pool_w, None, img_bias, B=B, N=A, K=A))
         proj = buf("aspp_proj", B, h, w, A)
         proj_variants = [(f"v{v}", [
             lambda *_, h=h, w=w, v=v: K.conv_gemm(

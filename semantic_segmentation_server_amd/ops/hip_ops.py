@@ -717,6 +717,22 @@ def matvec(x, w, bias, out, *, B, N, K, act=None):
     return out
 
 
+def aspp_pool(x, ws, w1t, b1, w2t, img_bias, *, B, HW, C, N):
+    """ASPP image-pooling branch -> per-image projection bias: GAP (two-pass, ws =
+    gap_workspace) then relu(w1t^T gap + b1) and w2t^T pooled in one workgroup per image.
+    w1t [C, N] and w2t [N, N] are the transposed fp32 weights."""
+    _chk(x, torch.bfloat16, "x", B * HW * C)
+    _chk(ws, torch.float32, "ws", int(_hip_mod().gap_workspace_floats(B, C)))
+    _chk(w1t, torch.float32, "w1t", C * N)
+    _chk(b1, torch.float32, "b1", N)
+    _chk(w2t, torch.float32, "w2t", N * N)
+    _chk(img_bias, torch.float32, "img_bias", B * N)
+    _hip_mod().aspp_pool(_ptr(x), _ptr(ws), _ptr(w1t), _ptr(b1), _ptr(w2t), _ptr(img_bias), B, HW, C, N,
+                         _stream())
+    _dbg('aspp_pool')
+    return img_bias
+
+
 ASPP_HEAD_G = (1, 2, 3, 5, 9)  # 16-pixel groups per workgroup (aspp_head.hip instantiations)
 
 

@@ -322,6 +322,26 @@ def test_maxpool_gap_matvec():
     assert torch.allclose(mv.cpu(), F.relu(gref @ wm.t() + bm), atol=1e-3)
 
 
+@pytest.mark.parametrize("B,h,w,C,N", [(3, 33, 33, 320, 256), (2, 17, 13, 2048, 256), (1, 9, 7, 40, 24)])
+def test_aspp_pool(B, h, w, C, N):
+    """GAP + relu(W1 gap + b1) + W2 pooled in two launches vs an fp32 torch reference
+    (the ASPP image-pooling branch folded into the projection's per-image bias)."""
+    K = _hip()
+    g = torch.Generator().manual_seed(11)
+    x = (torch.randn(B, C, h, w, generator=g) + 0.3).to(torch.bfloat16)
+    w1 = torch.randn(N, C, generator=g) / C ** 0.5
+    b1 = torch.randn(N, generator=g)
+    w2 = torch.randn(N, N, generator=g) / N ** 0.5
+    ib = torch.full((B, N), float("nan"), device=DEV)
+    ws = K.gap_workspace(B, C, DEV)
+    K.aspp_pool(_nhwc(x).to(DEV), ws, w1.t().contiguous().to(DEV), b1.to(DEV), w2.t().contiguous().to(DEV),
+                ib, B=B, HW=h * w, C=C, N=N)
+    torch.cuda.synchronize()
+    gref = x.float().mean((2, 3))
+    ref = F.relu(gref @ w1.t() + b1) @ w2.t()
+    assert _rel(ib.cpu(), ref) < 1e-4
+
+
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("h,H,K", [(33, 513, 21), (65, 1025, 19), (9, 65, 21), (33, 257, 30)])
 def test_upsample_argmax(h, H, K, variant):
