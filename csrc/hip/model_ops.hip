@@ -524,61 +524,94 @@ void matvec(const float* x, const float* w, const float* bias, float* out, int B
 //   gap[k]      = sum_s part[b][s][k] / HW                    (LDS)
 //   pooled[n]   = relu(sum_k w1t[k][n] gap[k] + b1[n])         (LDS)
 //   img_bias[n] = sum_k w2t[k][n] pooled[k]                   (-> projection epilogue)
-// Weights are host-transposed [K][N] so a lane per output channel reads a coalesced
-// 1 KiB row per k; four independent partial sums per lane keep loads in flight.
-constexpr int kPoolMaxC = 2048, kPoolMaxN = 512;
+// Weights are host-transposed [K][N]. Each of the 1024 threads owns 4 consecutive
+// outputs (one float4 weight load per k) and a K slice; the slices are summed through
+// LDS. A first version gave each thread whole K=320 dot products: ~80 dependent L2
+// round trips per thread, 30 us for one image (profiles/r2_b1 trace).
+constexpr int kPoolMaxC = 2048, kPoolMaxN = 512, kPoolThreads = 1024;
 
-__global__ __launch_bounds__(256) void aspp_pool_kernel(const float* __restrict__ part,
-                                                        const float* __restrict__ w1t,
-                                                        const float* __restrict__ b1,
-                                                        const float* __restrict__ w2t,
-                                                        float* __restrict__ img_bias, int HW, int C,
-                                                        int N) {
+__device__ __forceinline__ float4 pool_slice(const float* __restrict__ wt, const float* s_x, int k0,
+                                             int k1, int N, int q) {
+  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
+  int k = k0;
+  for (; k + 2 <= k1; k += 2) {
+    const float4 w0 = *reinterpret_cast<const float4*>(wt + (size_t)k * N + 4 * q);
+    const float4 w1 = *reinterpret_cast<const float4*>(wt + (size_t)(k + 1) * N + 4 * q);
+    const float x0 = s_x[k], x1 = s_x[k + 1];
+    a0.x += w0.x * x0; a0.y += w0.y * x0; a0.z += w0.z * x0; a0.w += w0.w * x0;
+    a1.x += w1.x * x1; a1.y += w1.y * x1; a1.z += w1.z * x1; a1.w += w1.w * x1;
+  }
+  if (k < k1) {
+    const float4 w0 = *reinterpret_cast<const float4*>(wt + (size_t)k * N + 4 * q);
+    const float x0 = s_x[k];
+    a0.x += w0.x * x0; a0.y += w0.y * x0; a0.z += w0.z * x0; a0.w += w0.w * x0;
+  }
+  return make_float4(a0.x + a1.x, a0.y + a1.y, a0.z + a1.z, a0.w + a1.w);
+}
+
+__global__ __launch_bounds__(kPoolThreads) void aspp_pool_kernel(const float* __restrict__ part,
+                                                                 const float* __restrict__ w1t,
+                                                                 const float* __restrict__ b1,
+                                                                 const float* __restrict__ w2t,
+                                                                 float* __restrict__ img_bias, int HW,
+                                                                 int C, int N) {
   __shared__ float s_gap[kPoolMaxC];
   __shared__ float s_pool[kPoolMaxN];
+  __shared__ float4 s_red[kPoolThreads];
   const int b = blockIdx.x, tid = threadIdx.x;
   const float inv = 1.f / (float)HW;
   const float* pb = part + (size_t)b * kGapSlices * C;
-  for (int k = tid; k < C; k += 256) {
+  for (int k = tid; k < C; k += kPoolThreads) {
     float s = 0.f;
 #pragma unroll
     for (int q = 0; q < kGapSlices; ++q) s += pb[(size_t)q * C + k];
     s_gap[k] = s * inv;
   }
+  const int nq = N >> 2;                    // float4 output columns
+  const int nks = kPoolThreads / nq;        // K slices
+  const int q = tid % nq, ks = tid / nq;
   __syncthreads();
-  for (int n = tid; n < N; n += 256) {
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int k = 0;
-    for (; k + 4 <= C; k += 4) {
-      s0 += w1t[(size_t)k * N + n] * s_gap[k];
-      s1 += w1t[(size_t)(k + 1) * N + n] * s_gap[k + 1];
-      s2 += w1t[(size_t)(k + 2) * N + n] * s_gap[k + 2];
-      s3 += w1t[(size_t)(k + 3) * N + n] * s_gap[k + 3];
-    }
-    for (; k < C; ++k) s0 += w1t[(size_t)k * N + n] * s_gap[k];
-    s_pool[n] = fmaxf((s0 + s1) + (s2 + s3) + b1[n], 0.f);
+  {
+    const int per = (C + nks - 1) / nks;
+    const int k0 = min(C, ks * per), k1 = min(C, k0 + per);
+    if (ks < nks) s_red[ks * nq + q] = pool_slice(w1t, s_gap, k0, k1, N, q);
   }
   __syncthreads();
-  for (int n = tid; n < N; n += 256) {
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int k = 0;
-    for (; k + 4 <= N; k += 4) {
-      s0 += w2t[(size_t)k * N + n] * s_pool[k];
-      s1 += w2t[(size_t)(k + 1) * N + n] * s_pool[k + 1];
-      s2 += w2t[(size_t)(k + 2) * N + n] * s_pool[k + 2];
-      s3 += w2t[(size_t)(k + 3) * N + n] * s_pool[k + 3];
+  if (tid < nq) {
+    float4 s = s_red[tid];
+    for (int j = 1; j < nks; ++j) {
+      const float4 v = s_red[j * nq + tid];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
-    for (; k < N; ++k) s0 += w2t[(size_t)k * N + n] * s_pool[k];
-    img_bias[(size_t)b * N + n] = (s0 + s1) + (s2 + s3);
+    s_pool[4 * tid + 0] = fmaxf(s.x + b1[4 * tid + 0], 0.f);
+    s_pool[4 * tid + 1] = fmaxf(s.y + b1[4 * tid + 1], 0.f);
+    s_pool[4 * tid + 2] = fmaxf(s.z + b1[4 * tid + 2], 0.f);
+    s_pool[4 * tid + 3] = fmaxf(s.w + b1[4 * tid + 3], 0.f);
+  }
+  __syncthreads();
+  {
+    const int per = (N + nks - 1) / nks;
+    const int k0 = min(N, ks * per), k1 = min(N, k0 + per);
+    if (ks < nks) s_red[ks * nq + q] = pool_slice(w2t, s_pool, k0, k1, N, q);
+  }
+  __syncthreads();
+  if (tid < nq) {
+    float4 s = s_red[tid];
+    for (int j = 1; j < nks; ++j) {
+      const float4 v = s_red[j * nq + tid];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    *reinterpret_cast<float4*>(img_bias + (size_t)b * N + 4 * tid) = s;
   }
 }
 
 void aspp_pool(const bf16* in, float* ws, const float* w1t, const float* b1, const float* w2t,
                float* img_bias, int B, int HW, int C, int N, hipStream_t s) {
-  if (C > kPoolMaxC || N > kPoolMaxN || C % 8) throw std::invalid_argument("aspp_pool: C <= 2048, C % 8, N <= 512");
+  if (C > kPoolMaxC || N > kPoolMaxN || C % 8 || N % 4)
+    throw std::invalid_argument("aspp_pool: C <= 2048, C % 8, N <= 512, N % 4");
   hipLaunchKernelGGL(gap_partial_kernel, dim3(B, kGapSlices, cdiv(C / 8, 64)), dim3(256), 0, s, in,
                      ws, HW, C);
-  hipLaunchKernelGGL(aspp_pool_kernel, dim3(B), dim3(256), 0, s, ws, w1t, b1, w2t, img_bias, HW, C, N);
+  hipLaunchKernelGGL(aspp_pool_kernel, dim3(B), dim3(kPoolThreads), 0, s, ws, w1t, b1, w2t, img_bias, HW, C, N);
   check_launch("aspp_pool");
 }
 

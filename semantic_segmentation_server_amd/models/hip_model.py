@@ -348,7 +348,7 @@ class HipDeepLab:
             img_bias = buf("img_bias", B, A, dtype=torch.float32)
             gws = K.gap_workspace(B, c, dev)
             bufs["gap_ws"] = gws
-            if c <= 2048 and A <= 512 and c % 8 == 0:
+            if c <= 2048 and A <= 512 and c % 8 == 0 and A % 4 == 0:
                 # GAP partials + one per-image kernel for the pooled MLP (aspp_pool)
                 w1t = self.pool_w.t().contiguous()
                 w2t = self.proj_pool_w.t().contiguous()
