@@ -4,6 +4,7 @@
 #include <pybind11/stl.h>
 
 #include "contours.h"
+#include "v4l2.h"
 
 namespace py = pybind11;
 using namespace ssa;
@@ -108,4 +109,34 @@ PYBIND11_MODULE(_host, m) {
   m.def("segments", &segments, py::arg("labels"), py::arg("palette"), py::arg("min_area"),
         "Reference post-processing of one cropped label map -> "
         "[(label, score, area, cx, cy, contour_index, is_hole)] in contour order.");
+
+  m.def("yuv422_to_bgr", [](const U8& src, bool uyvy) {
+    if (src.ndim() != 2 || src.shape(1) % 4) throw std::invalid_argument("yuv422_to_bgr: (H, 2*W) uint8, W even");
+    const int H = (int)src.shape(0), W = (int)src.shape(1) / 2;
+    py::array_t<uint8_t> out({(ssize_t)H, (ssize_t)W, (ssize_t)3});
+    yuv422_to_bgr(src.data(), 2 * W, W, H, uyvy, out.mutable_data());
+    return out;
+  }, py::arg("src"), py::arg("uyvy") = false,
+        "Packed 4:2:2 (YUYV, or UYVY) -> BGR, BT.601 limited range (OpenCV's COLOR_YUV2BGR_YUYV convention).");
+
+  py::class_<V4L2Capture>(m, "V4L2Capture")
+      .def(py::init<const std::string&, int, int, int>(), py::arg("device"), py::arg("width") = 640,
+           py::arg("height") = 480, py::arg("nbuf") = 4)
+      .def_property_readonly("width", &V4L2Capture::width)
+      .def_property_readonly("height", &V4L2Capture::height)
+      .def_property_readonly("fourcc", &V4L2Capture::fourcc)
+      .def("read_into", [](V4L2Capture& c, py::array_t<uint8_t, py::array::c_style> dst, int timeout_ms) {
+             if (dst.ndim() != 3 || dst.shape(0) != c.height() || dst.shape(1) != c.width() || dst.shape(2) != 3)
+               throw std::invalid_argument("read_into: dst must be (height, width, 3) uint8");
+             uint32_t seq = 0;
+             int64_t ts = 0;
+             bool ok;
+             {
+               py::gil_scoped_release nogil;
+               ok = c.read(dst.mutable_data(), timeout_ms, &seq, &ts);
+             }
+             return py::make_tuple(ok, seq, ts);
+           }, py::arg("dst"), py::arg("timeout_ms") = 1000,
+           "Next frame as BGR into dst; returns (ok, driver sequence, timestamp us).")
+      .def("close", &V4L2Capture::close);
 }

@@ -9,7 +9,9 @@ here, so:
   noise) at a given camera resolution; the benchmark source.
 * ``FileSource``     — replays ``.npy`` (N, H, W, 3) uint8 stacks or a directory
   of images readable by Pillow.
-* ``V4L2Source``     — gated: only if ``cv2`` is importable (camera boxes).
+* ``V4L2Source``     — a V4L2 camera through the native capture in ``_host``
+  (``csrc/host/v4l2.cpp``: mmap streaming, YUYV/UYVY -> BGR in C++), no OpenCV;
+  ``SSA_CAPTURE=cv2`` selects ``cv2.VideoCapture`` where OpenCV is installed.
 
 Every source yields ``Frame`` objects and exposes ``resolution`` (w, h). Sources
 are iterators; ``read_batch(n)`` returns a pinned host batch for the engine.
@@ -180,25 +182,64 @@ class FileSource(FrameSource):
         return f
 
 
-class V4L2Source(FrameSource):  # pragma: no cover - needs a camera and cv2
-    def __init__(self, camera_idx: int, stream: int = 0):
-        import cv2  # gated: not installed in the build image
-        self.cap = cv2.VideoCapture(camera_idx)
+class V4L2Source(FrameSource):
+    """A V4L2 camera (reference: ``cv2.VideoCapture(camera_idx)``, sem_seg_server.py:144-148,
+    probed once for its native resolution at :268-270). ``camera_idx`` is the N of
+    ``/dev/videoN``; the driver picks the nearest size to ``width`` x ``height``."""
+
+    def __init__(self, camera_idx: int, stream: int = 0, width: int = 640, height: int = 480,
+                 timeout_ms: int = 2000, device: Optional[str] = None):
         self.stream = stream
-        self.resolution = (int(self.cap.get(cv2.CAP_PROP_FRAME_WIDTH)),
-                           int(self.cap.get(cv2.CAP_PROP_FRAME_HEIGHT)))
+        self.timeout_ms = int(timeout_ms)
         self._i = 0
+        self._cv = None
+        self.cap = None
+        if os.environ.get("SSA_CAPTURE", "native") == "cv2":  # pragma: no cover - needs cv2
+            import cv2
+            self._cv = cv2.VideoCapture(camera_idx)
+            self.resolution = (int(self._cv.get(cv2.CAP_PROP_FRAME_WIDTH)),
+                               int(self._cv.get(cv2.CAP_PROP_FRAME_HEIGHT)))
+            return
+        from ..ops.native import host
+        self.cap = host().V4L2Capture(device or f"/dev/video{int(camera_idx)}", int(width), int(height))
+        self.resolution = (int(self.cap.width), int(self.cap.height))
+
+    def _read(self, out: np.ndarray) -> bool:
+        if self._cv is not None:  # pragma: no cover
+            ok, img = self._cv.read()
+            if ok:
+                out[...] = img
+            return bool(ok)
+        ok, _seq, _ts = self.cap.read_into(out, self.timeout_ms)
+        return bool(ok)
 
     def __next__(self) -> Frame:
-        ok, img = self.cap.read()
-        if not ok:
-            raise StopIteration
+        w, h = self.resolution
+        img = np.empty((h, w, 3), np.uint8)
+        if not self._read(img):
+            raise StopIteration  # end of stream / camera gone: the producer stops (:146-148)
         f = Frame(img, self._i, self.stream, time.time())
         self._i += 1
         return f
 
+    def read_batch_into(self, out: np.ndarray):
+        """Frames straight into the feeder's pinned ring slot (no intermediate copy)."""
+        ids, ts = [], []
+        for i in range(out.shape[0]):
+            if not self._read(out[i]):
+                if i == 0:
+                    raise StopIteration
+                break
+            ids.append(self._i)
+            ts.append(time.time())
+            self._i += 1
+        return len(ids), ids, ts
+
     def close(self):
-        self.cap.release()
+        if self._cv is not None:  # pragma: no cover
+            self._cv.release()
+        if self.cap is not None:
+            self.cap.close()
 
 
 def probe_resolution(kind: str, camera_idx: int = 1, width: int = 640, height: int = 480,
@@ -209,7 +250,7 @@ def probe_resolution(kind: str, camera_idx: int = 1, width: int = 640, height: i
     if kind == "file":
         return FileSource(path).resolution
     if kind == "camera":
-        src = V4L2Source(camera_idx)
+        src = V4L2Source(camera_idx, width=width, height=height)
         res = src.resolution
         src.close()
         return res
@@ -224,5 +265,5 @@ def make_source(kind: str, stream: int = 0, camera_idx: int = 1, width: int = 64
     if kind == "file":
         return FileSource(path, stream, loop=limit is None)
     if kind == "camera":
-        return V4L2Source(camera_idx + stream, stream)
+        return V4L2Source(camera_idx + stream, stream, width=width, height=height)
     raise ValueError(kind)
