@@ -159,6 +159,16 @@ def _dwp_rows_fit(ty: int, stages: int, dil: int, OW: int, cout: int) -> bool:
             stages * (halo * 64 + (cout // 16 + 1) * 1024) <= 160 * 1024)
 
 
+def _copy_picks(src: List[Callable], dst: List[Callable]) -> None:
+    """Give every Choice of ``dst`` (a plan built by the same code) the pick of the
+    Choice at the same position in ``src``, nested choices included."""
+    for a, b in zip(src, dst):
+        if isinstance(a, Choice) and isinstance(b, Choice):
+            b.pick = a.pick
+            for (_, va), (_, vb) in zip(a.variants, b.variants):
+                _copy_picks(va, vb)
+
+
 class HipDeepLab:
     def __init__(self, model: DeepLabV3, device: torch.device, cfg=None):
         if device.type != "cuda":
@@ -248,8 +258,11 @@ class HipDeepLab:
         self._labels_out: Optional[torch.Tensor] = None
 
     # ------------------------------------------------------------------ plan
-    def _plan(self, B: int, Hc: int, Wc: int):
-        key = (B, Hc, Wc)
+    def _plan(self, B: int, Hc: int, Wc: int, part: int = 0):
+        """Kernel list + static buffers for (B, camera). ``part`` > 0: an independent
+        copy (own buffers) of the same plan, for concurrent sub-batches on separate
+        streams; it takes part 0's autotune picks."""
+        key = (B, Hc, Wc) if part == 0 else (B, Hc, Wc, part)
         if key in self._plans:
             return self._plans[key]
         dev = self.device
@@ -408,7 +421,13 @@ class HipDeepLab:
             logits, self._labels_out if self._labels_out is not None else labels, B=B, h=h, w=w,
             K=self.num_classes, ldk=self.ldk, H=H, W=W, variant=v)]) for name in ("rows", "lane")]))
         self._plans[key] = (ops, bufs)
-        self._autotune(ops, B, Hc, Wc)
+        if part == 0:
+            self._autotune(ops, B, Hc, Wc)
+        else:
+            _copy_picks(self._plan(B, Hc, Wc)[0], ops)
+            args = self._tune_inputs(B, Hc, Wc)
+            for op in ops:  # populate every buffer once, outside any capture
+                op(*args)
         return self._plans[key]
 
     def _tune_inputs(self, B: int, Hc: int, Wc: int):
@@ -680,13 +699,14 @@ class HipDeepLab:
 
     # ------------------------------------------------------------------ run
     def segment(self, frames: torch.Tensor, lut_x: torch.Tensor, lut_y: torch.Tensor,
-                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                out: Optional[torch.Tensor] = None, part: int = 0) -> torch.Tensor:
         """frames: (B, Hc, Wc, 3) uint8 BGR on device -> (B, H, W) uint8 labels (static
-        buffer, or ``out``)."""
+        buffer, or ``out``). ``part``: which independent copy of the plan to run (the
+        engine's concurrent half-batches use parts 0 and 1)."""
         B, Hc, Wc, _ = frames.shape
         if lut_x.numel() != self.W or lut_y.numel() != self.H:
             raise ValueError("letterbox LUTs do not match the model input size")
-        ops, bufs = self._plan(B, Hc, Wc)
+        ops, bufs = self._plan(B, Hc, Wc, part)
         if out is not None and (out.shape != bufs["labels"].shape or out.dtype != torch.uint8
                                 or not out.is_contiguous() or out.device != bufs["labels"].device):
             raise ValueError("segment: out must match the (B, H, W) uint8 label buffer")

@@ -32,11 +32,20 @@ class DevicePostprocess:
             self._bufs[B] = (ws, rec)
         return self._bufs[B]
 
-    def run(self, labels: torch.Tensor, crop_w: int, crop_h: int, min_area: float) -> torch.Tensor:
+    def run(self, labels: torch.Tensor, crop_w: int, crop_h: int, min_area: float,
+            out: torch.Tensor = None) -> torch.Tensor:
+        """Packed records of ``labels`` into the static buffer for this B, or into ``out``
+        ([B, 1 + 5K] fp32, e.g. a row slice of a bigger batch's buffer). The workspace is
+        shared per B: runs that share it must be ordered on one stream."""
         B = labels.shape[0]
         if labels.shape[1:] != (self.H, self.W):
             raise ValueError(f"labels {tuple(labels.shape)} != (B, {self.H}, {self.W})")
         ws, rec = self._buffers(B)
+        if out is not None:
+            if (out.shape != rec.shape or out.dtype != rec.dtype or not out.is_contiguous()
+                    or out.device != rec.device):
+                raise ValueError("DevicePostprocess.run: out must be a contiguous [B, 1 + 5K] fp32 buffer")
+            rec = out
         hip_ops.postprocess(labels, self.palette, ws, rec, B=B, H=self.H, W=self.W, crop_h=crop_h,
                             crop_w=crop_w, min_area=min_area, K=self.K, bins=self.bins, thr=self.thr)
         return rec

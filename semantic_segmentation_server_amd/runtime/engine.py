@@ -24,6 +24,7 @@ Post-processing (``contour_mode``):
 from __future__ import annotations
 
 import logging
+import os
 import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -148,12 +149,12 @@ class Engine:
             logits = self.model(x)
         return R.upsample_argmax(logits, self.H, self.W)
 
-    def _device_post(self, labels: torch.Tensor):
+    def _device_post(self, labels: torch.Tensor, out: Optional[torch.Tensor] = None):
         if self._hip_post is None:
             from ..postprocess.device import DevicePostprocess
             self._hip_post = DevicePostprocess(self.device, self.H, self.W, self.palette,
                                                self.cfg.max_segments)
-        return self._hip_post.run(labels, self.crop_w, self.crop_h, self.min_area)
+        return self._hip_post.run(labels, self.crop_w, self.crop_h, self.min_area, out=out)
 
     def _use_device_post(self) -> bool:
         return self.is_cuda and self.cfg.contour_mode == "fast"
@@ -219,6 +220,12 @@ class Engine:
             return
         self._split = bool(split_post) and self._use_device_post()
         self.result_stream = torch.cuda.Stream(self.device) if self._split else None
+        # SSA_MODEL_PARTS=P: the model of each step as P concurrent sub-batch graphs on P
+        # streams, each followed by its own post-processing graph (split_post path; B % P
+        # == 0 and B >= 2P, else one graph). Measured at B = 32: 2 parts 25.1k / 25.7k
+        # frames/s vs 22.4k / 24.0k for one graph (profiles/r2_parts_ab.txt)
+        self.model_parts = int(os.environ.get("SSA_MODEL_PARTS", "2"))
+        self.model_streams: List[torch.cuda.Stream] = []
         self._bound = {b.data_ptr(): b for b in bufs}
         self._bound_graphs = {}
         if self.cam is not None:  # capture now, not inside the first timed steps
@@ -243,15 +250,45 @@ class Engine:
             torch.cuda.current_stream(self.device).wait_stream(s)
             if getattr(self, "_split", False):
                 lab = torch.empty((b.shape[0], self.H, self.W), dtype=torch.uint8, device=self.device)
-                gm = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gm):  # the model writes the slot's own label maps
-                    if hasattr(self._hip_model, "_labels_out"):
-                        self._hip_model.segment(b, self.lut_x, self.lut_y, out=lab)
-                    else:
-                        lab.copy_(self._infer_eager(b))
-                gp = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gp):
-                    post = self._device_post(lab)
+                hm = self._hip_model if hasattr(self._hip_model, "_labels_out") else None
+                B = b.shape[0]
+                P = self.model_parts if hm is not None else 1
+                P = P if P > 1 and B % P == 0 and B >= 2 * P else 1
+                if P > 1:
+                    # P independent sub-batch model graphs, replayed on P streams: the
+                    # latency-bound kernels of one part fill the others' tails; each
+                    # part's post-processing starts as soon as its labels exist
+                    h = B // P
+                    sls = [slice(i * h, (i + 1) * h) for i in range(P)]
+                    for part, sl in enumerate(sls):
+                        hm.segment(b[sl], self.lut_x, self.lut_y, out=lab[sl], part=part)
+                    post = torch.zeros((B, 1 + 5 * self.cfg.max_segments), dtype=torch.float32,
+                                       device=self.device)
+                    for sl in sls:  # warm-up outside capture
+                        self._device_post(lab[sl], out=post[sl])
+                    torch.cuda.synchronize(self.device)
+                    gm, gp = [], []
+                    for part, sl in enumerate(sls):
+                        g_ = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g_):
+                            hm.segment(b[sl], self.lut_x, self.lut_y, out=lab[sl], part=part)
+                        gm.append(g_)
+                        g_ = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g_):
+                            self._device_post(lab[sl], out=post[sl])
+                        gp.append(g_)
+                    while len(self.model_streams) < P - 1:
+                        self.model_streams.append(torch.cuda.Stream(self.device))
+                else:
+                    gm = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(gm):  # the model writes the slot's own label maps
+                        if hm is not None:
+                            hm.segment(b, self.lut_x, self.lut_y, out=lab)
+                        else:
+                            lab.copy_(self._infer_eager(b))
+                    gp = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(gp):
+                        post = self._device_post(lab)
                 ent = (tuple(frames.shape), gm, lab, post, gp, torch.cuda.Event())
             else:
                 g = torch.cuda.CUDAGraph()
@@ -279,6 +316,31 @@ class Engine:
                     return labels, post
                 cur = torch.cuda.current_stream(self.device)
                 cur.wait_event(post_done)  # this slot's previous post-processing read `labels`
+                if isinstance(g, list):
+                    # model parts on cur + model_streams, each part's post-processing on
+                    # the result stream as soon as its labels exist; cur joins every part
+                    # (the staging slot is free only after all of them read it)
+                    rs = self.result_stream
+                    streams = [cur] + self.model_streams[:len(g) - 1]
+                    fork = torch.cuda.Event()
+                    fork.record(cur)
+                    ready = []
+                    for st_, g_ in zip(streams, g):
+                        if st_ is not cur:
+                            st_.wait_event(fork)
+                        with torch.cuda.stream(st_):
+                            g_.replay()
+                        ev = torch.cuda.Event()
+                        ev.record(st_)
+                        ready.append(ev)
+                    for ev in ready[1:]:
+                        cur.wait_event(ev)
+                    with torch.cuda.stream(rs):
+                        for ev, gp_ in zip(ready, gpost):
+                            rs.wait_event(ev)
+                            gp_.replay()
+                    post_done.record(rs)
+                    return labels, post
                 g.replay()
                 ready = torch.cuda.Event()
                 ready.record(cur)

@@ -634,6 +634,49 @@ def test_dp_pipeline_records_match_eager(lag):
     assert sorted(got_all) == sorted(x for w in want for x in w)
 
 
+@pytest.mark.parametrize("parts", [2, 4])
+def test_dp_pipeline_model_parts_match_eager(monkeypatch, parts):
+    """SSA_MODEL_PARTS=P: each step's model runs as P concurrent sub-batch graphs on P
+    streams and each part's post-processing starts as soon as its labels exist; the
+    records must equal those of eager, synchronous per-part steps (the part plans' own
+    kernel picks)."""
+    from semantic_segmentation_server_amd.parallel import dist as D
+    from semantic_segmentation_server_amd.parallel.dp import DataParallelPipeline
+    from semantic_segmentation_server_amd.runtime.engine import Engine
+    from semantic_segmentation_server_amd.runtime.sources import SyntheticSource
+    monkeypatch.setenv("SSA_MODEL_PARTS", str(parts))
+    n = 2 * parts  # two frames per part
+    kw = dict(batch=n, input_size=257, min_area_ratio=0.002)
+    eng = Engine(_small_cfg(graph=True, **kw), torch.device(DEV))
+    src = SyntheticSource(160, 120, seed=7, pool=4)
+    batches = [torch.from_numpy(np.ascontiguousarray(src.read_batch(n)[0])) for _ in range(2)]
+    eng.set_camera(160, 120)
+    want = []
+    for k in range(6):
+        f = batches[k % 2].to(DEV)
+        for h in range(parts):
+            lab = eng._hip_model.segment(f[2 * h:2 * h + 2], eng.lut_x, eng.lut_y, part=0)
+            post = eng._device_post(lab)
+            ids = [k * n + 2 * h, k * n + 2 * h + 1]
+            r = eng._hip_post.fetch(post, ids, [0.0, 0.0], [0, 0], eng.W, eng.H)
+            want.extend(zip(r["frame"].tolist(), r["label"].tolist(), r["area"].round(6).tolist()))
+    torch.cuda.synchronize()
+    ctx = D.init()
+    pipe = DataParallelPipeline(ctx, eng, 160, 120, n, "local", None, lag=1)
+    assert eng.model_parts == parts
+    got = []
+    pipe.prefetch(batches[0].pin_memory())
+    for k in range(6):
+        recs = pipe.step(next_frames=batches[(k + 1) % 2].pin_memory() if k < 5 else None)
+        got.extend(zip(recs["frame"].tolist(), recs["label"].tolist(), recs["area"].round(6).tolist()))
+    last = pipe.flush()
+    got.extend(zip(last["frame"].tolist(), last["label"].tolist(), last["area"].round(6).tolist()))
+    torch.cuda.synchronize()
+    assert len(eng.model_streams) == parts - 1  # the parts path ran
+    assert len(want) > 0
+    assert sorted(got) == sorted(want)
+
+
 def test_engine_step_records_flow():
     from semantic_segmentation_server_amd.runtime.engine import Engine
     from semantic_segmentation_server_amd.runtime.sources import SyntheticSource
