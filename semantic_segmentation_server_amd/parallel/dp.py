@@ -238,8 +238,12 @@ class DataParallelPipeline:
                     if self._prev_done is None else self.copy_stream.wait_event(self._prev_done)
             self.prefetch(next_frames)
         if self.cuda:
-            self._prev_done = torch.cuda.Event()
-            self._prev_done.record(torch.cuda.current_stream(self.dev))
+            consumed = getattr(self.engine, "last_consumed", None)
+            if consumed is not None:  # slot-parallel engine: the model ran on its own stream
+                self._prev_done = consumed
+            else:
+                self._prev_done = torch.cuda.Event()
+                self._prev_done.record(torch.cuda.current_stream(self.dev))
         if packed is None:  # host post-processing path (torch backend / exact mode)
             self.frames_done += B * self.ctx.world
             return self.engine.records_from_labels(labels, fids, tss, strm)

@@ -222,11 +222,21 @@ class Engine:
         self.result_stream = torch.cuda.Stream(self.device) if self._split else None
         # SSA_MODEL_PARTS=P: the model of each step as P concurrent sub-batch graphs on P
         # streams, each followed by its own post-processing graph (split_post path; B % P
-        # == 0 and B >= 2P, else one graph). Measured at B = 32: 2 parts 25.1k / 25.7k
-        # frames/s vs 22.4k / 24.0k for one graph (profiles/r2_parts_ab.txt)
-        self.model_parts = int(os.environ.get("SSA_MODEL_PARTS", "2"))
+        # == 0 and B >= 2P, else one graph). Measured at B = 32: 2 parts 26.0k frames/s vs
+        # 24.0k for one graph (profiles/r2_parts_ab.txt); slot-parallel (default, below)
+        # measured faster still, so parts are off unless asked for.
+        self.model_parts = int(os.environ.get("SSA_MODEL_PARTS", "1"))
         self.model_streams: List[torch.cuda.Stream] = []
         self._bound = {b.data_ptr(): b for b in bufs}
+        self._slot_of = {b.data_ptr(): i for i, b in enumerate(bufs)}
+        # slot-parallel (default; SSA_SLOT_PARALLEL=0 turns it off): every staging slot
+        # owns a plan copy and a model stream, so step k+1's model runs concurrently with
+        # step k's. Latency-bound kernels of one step fill the other's tails: B = 32
+        # 26.9k / 27.3k frames/s vs 25.9k / 25.6k for 2 sub-batch parts, batch 1 0.39 /
+        # 0.38 ms per frame vs 0.52 / 0.48 (profiles/r2_slot_ab.txt)
+        self.slot_parallel = os.environ.get("SSA_SLOT_PARALLEL", "1") == "1" and self._split
+        self.slot_streams: List[torch.cuda.Stream] = []
+        self.last_consumed = None
         self._bound_graphs = {}
         if self.cam is not None:  # capture now, not inside the first timed steps
             for b in bufs:
@@ -252,7 +262,7 @@ class Engine:
                 lab = torch.empty((b.shape[0], self.H, self.W), dtype=torch.uint8, device=self.device)
                 hm = self._hip_model if hasattr(self._hip_model, "_labels_out") else None
                 B = b.shape[0]
-                P = self.model_parts if hm is not None else 1
+                P = self.model_parts if hm is not None and not self.slot_parallel else 1
                 P = P if P > 1 and B % P == 0 and B >= 2 * P else 1
                 if P > 1:
                     # P independent sub-batch model graphs, replayed on P streams: the
@@ -280,10 +290,14 @@ class Engine:
                     while len(self.model_streams) < P - 1:
                         self.model_streams.append(torch.cuda.Stream(self.device))
                 else:
+                    if hm is not None and self.slot_parallel:
+                        hm.segment(b, self.lut_x, self.lut_y, out=lab, part=self._slot_of[key])
+                        torch.cuda.synchronize(self.device)
                     gm = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(gm):  # the model writes the slot's own label maps
                         if hm is not None:
-                            hm.segment(b, self.lut_x, self.lut_y, out=lab)
+                            hm.segment(b, self.lut_x, self.lut_y, out=lab,
+                                       part=self._slot_of[key] if self.slot_parallel else 0)
                         else:
                             lab.copy_(self._infer_eager(b))
                     gp = torch.cuda.CUDAGraph()
@@ -316,6 +330,26 @@ class Engine:
                     return labels, post
                 cur = torch.cuda.current_stream(self.device)
                 cur.wait_event(post_done)  # this slot's previous post-processing read `labels`
+                if self.slot_parallel:
+                    # this slot's model on its own stream: the previous step (other slot,
+                    # other stream, other plan copy) may still be running
+                    i = self._slot_of[frames.data_ptr()]
+                    while len(self.slot_streams) <= i:
+                        self.slot_streams.append(torch.cuda.Stream(self.device))
+                    ms, rs = self.slot_streams[i], self.result_stream
+                    fork = torch.cuda.Event()
+                    fork.record(cur)  # cur waited for this slot's frames (H2D)
+                    ms.wait_event(fork)
+                    with torch.cuda.stream(ms):
+                        g.replay()
+                    ready = torch.cuda.Event()
+                    ready.record(ms)
+                    self.last_consumed = ready  # the staging slot may be refilled after this
+                    rs.wait_event(ready)
+                    with torch.cuda.stream(rs):
+                        gpost.replay()
+                    post_done.record(rs)
+                    return labels, post
                 if isinstance(g, list):
                     # model parts on cur + model_streams, each part's post-processing on
                     # the result stream as soon as its labels exist; cur joins every part

@@ -634,7 +634,7 @@ def test_dp_pipeline_records_match_eager(lag):
     assert sorted(got_all) == sorted(x for w in want for x in w)
 
 
-@pytest.mark.parametrize("parts", [2, 4])
+@pytest.mark.parametrize("parts", [2, 4, "slot"])
 def test_dp_pipeline_model_parts_match_eager(monkeypatch, parts):
     """SSA_MODEL_PARTS=P: each step's model runs as P concurrent sub-batch graphs on P
     streams and each part's post-processing starts as soon as its labels exist; the
@@ -644,6 +644,10 @@ def test_dp_pipeline_model_parts_match_eager(monkeypatch, parts):
     from semantic_segmentation_server_amd.parallel.dp import DataParallelPipeline
     from semantic_segmentation_server_amd.runtime.engine import Engine
     from semantic_segmentation_server_amd.runtime.sources import SyntheticSource
+    slot = parts == "slot"  # SSA_SLOT_PARALLEL: one plan copy + model stream per staging slot
+    if slot:
+        parts = 1
+        monkeypatch.setenv("SSA_SLOT_PARALLEL", "1")
     monkeypatch.setenv("SSA_MODEL_PARTS", str(parts))
     n = 2 * parts  # two frames per part
     kw = dict(batch=n, input_size=257, min_area_ratio=0.002)
@@ -672,7 +676,10 @@ def test_dp_pipeline_model_parts_match_eager(monkeypatch, parts):
     last = pipe.flush()
     got.extend(zip(last["frame"].tolist(), last["label"].tolist(), last["area"].round(6).tolist()))
     torch.cuda.synchronize()
-    assert len(eng.model_streams) == parts - 1  # the parts path ran
+    if slot:
+        assert len(eng.slot_streams) == 2  # each staging slot ran on its own stream
+    else:
+        assert len(eng.model_streams) == parts - 1  # the parts path ran
     assert len(want) > 0
     assert sorted(got) == sorted(want)
 
