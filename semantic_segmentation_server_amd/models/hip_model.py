@@ -169,6 +169,19 @@ def _copy_picks(src: List[Callable], dst: List[Callable]) -> None:
                 _copy_picks(va, vb)
 
 
+def _run_variants(ops: List[Callable], args) -> None:
+    """Run every variant of every Choice once (nested first), then the picked ones in
+    plan order -- the buffer side effects of ``Choice.autotune`` without the timing."""
+    for op in ops:
+        if isinstance(op, Choice):
+            for _, vops in op.variants:
+                _run_variants(vops, args)
+                for o in vops:
+                    o(*args)
+    for op in ops:
+        op(*args)
+
+
 class HipDeepLab:
     def __init__(self, model: DeepLabV3, device: torch.device, cfg=None):
         if device.type != "cuda":
@@ -270,7 +283,9 @@ class HipDeepLab:
         ops: List[Callable] = []
 
         def buf(name, *shape, dtype=torch.bfloat16):
-            t = torch.empty(shape, dtype=dtype, device=dev)
+            # zeroed: a plan copy must start from the same bytes as the plan it copies
+            # (channel / tile padding that some variant reads but only others write)
+            t = torch.zeros(shape, dtype=dtype, device=dev)
             bufs[name] = t
             return t
 
@@ -428,6 +443,7 @@ class HipDeepLab:
             args = self._tune_inputs(B, Hc, Wc)
             for op in ops:  # populate every buffer once, outside any capture
                 op(*args)
+            _run_variants(ops, args)  # as part 0's autotune did: identical buffer state
         return self._plans[key]
 
     def _tune_inputs(self, B: int, Hc: int, Wc: int):

@@ -645,9 +645,9 @@ def test_dp_pipeline_model_parts_match_eager(monkeypatch, parts):
     from semantic_segmentation_server_amd.runtime.engine import Engine
     from semantic_segmentation_server_amd.runtime.sources import SyntheticSource
     slot = parts == "slot"  # SSA_SLOT_PARALLEL: one plan copy + model stream per staging slot
+    monkeypatch.setenv("SSA_SLOT_PARALLEL", "1" if slot else "0")
     if slot:
         parts = 1
-        monkeypatch.setenv("SSA_SLOT_PARALLEL", "1")
     monkeypatch.setenv("SSA_MODEL_PARTS", str(parts))
     n = 2 * parts  # two frames per part
     kw = dict(batch=n, input_size=257, min_area_ratio=0.002)
