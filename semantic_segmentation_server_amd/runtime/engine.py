@@ -234,7 +234,10 @@ class Engine:
         # step k's. Latency-bound kernels of one step fill the other's tails: B = 32
         # 26.9k / 27.3k frames/s vs 25.9k / 25.6k for 2 sub-batch parts, batch 1 0.39 /
         # 0.38 ms per frame vs 0.52 / 0.48 (profiles/r2_slot_ab.txt)
-        self.slot_parallel = os.environ.get("SSA_SLOT_PARALLEL", "1") == "1" and self._split
+        # (needs plan copies: the MobileNetV2 HIP model; the int8 / torch paths keep one
+        # plan, so their slots stay on the caller's stream)
+        self.slot_parallel = (os.environ.get("SSA_SLOT_PARALLEL", "1") == "1" and self._split
+                              and hasattr(getattr(self, "_hip_model", None), "_labels_out"))
         self.slot_streams: List[torch.cuda.Stream] = []
         self.last_consumed = None
         self._bound_graphs = {}
