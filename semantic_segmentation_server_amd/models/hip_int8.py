@@ -89,9 +89,12 @@ class HipDeepLabInt8:
         self.pool_b = qb.to(dev, torch.float32)
         self.logits_p = pack_int8(model.logits, S["aspp.proj"], dev)
         self._plans: Dict[tuple, Tuple[List[Callable], Dict[str, torch.Tensor]]] = {}
+        self._labels_out: Optional[torch.Tensor] = None  # segment(out=): caller's label maps
 
-    def _plan(self, B: int, Hc: int, Wc: int):
-        key = (B, Hc, Wc)
+    def _plan(self, B: int, Hc: int, Wc: int, part: int = 0):
+        """``part`` > 0: an independent copy of the plan (own buffers, part 0's picks) for
+        the engine's slot-parallel execution (hip_model.HipDeepLab._plan)."""
+        key = (B, Hc, Wc) if part == 0 else (B, Hc, Wc, part)
         if key in self._plans:
             return self._plans[key]
         dev, S = self.device, self.scales
@@ -99,7 +102,7 @@ class HipDeepLabInt8:
         ops: List[Callable] = []
 
         def buf(name, *shape, dtype=torch.int8):
-            t = torch.empty(shape, dtype=dtype, device=dev)
+            t = torch.zeros(shape, dtype=dtype, device=dev)  # plan copies start identical
             bufs[name] = t
             return t
 
@@ -161,10 +164,20 @@ class HipDeepLabInt8:
             Cout=self.num_classes, ldo=self.ldk, act=None))
         labels = buf("labels", B, H, W, dtype=torch.uint8)
         ops.append(lambda *_, h=h, w=w: K.upsample_argmax(
-            logits, labels, B=B, h=h, w=w, K=self.num_classes, ldk=self.ldk, H=H, W=W,
-            variant=K.UPSAMPLE_VARIANTS["lane"]))
+            logits, self._labels_out if self._labels_out is not None else labels, B=B, h=h, w=w,
+            K=self.num_classes, ldk=self.ldk, H=H, W=W, variant=K.UPSAMPLE_VARIANTS["lane"]))
         self._plans[key] = (ops, bufs)
-        self._autotune(ops, B, Hc, Wc)
+        if part == 0:
+            self._autotune(ops, B, Hc, Wc)
+        else:
+            from .hip_model import _copy_picks, _run_variants
+            _copy_picks(self._plan(B, Hc, Wc)[0], ops)
+            dev = self.device
+            args = (torch.zeros((B, Hc, Wc, 3), dtype=torch.uint8, device=dev),
+                    torch.zeros(self.W, dtype=torch.int32, device=dev),
+                    torch.zeros(self.H, dtype=torch.int32, device=dev))
+            _run_variants(ops, args)
+            torch.cuda.synchronize(dev)
         return self._plans[key]
 
     def _autotune(self, ops, B, Hc, Wc) -> None:
@@ -222,13 +235,20 @@ class HipDeepLabInt8:
             act="relu", res=idt, res_scale=d["s_res"], out_scale=S[f"b{i}.out"]))
         return out, OH, OW, cout
 
-    def segment(self, frames, lut_x, lut_y):
+    def segment(self, frames, lut_x, lut_y, out: Optional[torch.Tensor] = None, part: int = 0):
         B, Hc, Wc, _ = frames.shape
-        ops, bufs = self._plan(B, Hc, Wc)
+        ops, bufs = self._plan(B, Hc, Wc, part)
+        if out is not None and (out.shape != bufs["labels"].shape or out.dtype != torch.uint8
+                                or not out.is_contiguous()):
+            raise ValueError("segment: out must match the (B, H, W) uint8 label buffer")
         frames = frames.contiguous()
-        for op in ops:
-            op(frames, lut_x, lut_y)
-        return bufs["labels"]
+        self._labels_out = out
+        try:
+            for op in ops:
+                op(frames, lut_x, lut_y)
+        finally:
+            self._labels_out = None
+        return bufs["labels"] if out is None else out
 
     def logits(self, frames, lut_x, lut_y):
         self.segment(frames, lut_x, lut_y)
