@@ -100,7 +100,13 @@ class DataParallelPipeline:
         if gather not in ("host", "rccl"):
             raise ValueError("gather must be 'host' or 'rccl'")
         self.ctx = ctx
-        self.lag = 1 if lag else 0
+        # lag L >= 1: step k collects step k-L's records, with L + 1 staging slots (so L + 1
+        # steps can be in flight on a slot-parallel engine); SSA_PIPE_LAG overrides a
+        # non-zero lag (experiments: 2 = three slots)
+        self.lag = max(0, min(3, int(lag)))
+        if self.lag and os.environ.get("SSA_PIPE_LAG"):
+            self.lag = max(1, min(3, int(os.environ["SSA_PIPE_LAG"])))
+        self.nslots = max(2, self.lag + 1)
         self.gather_mode = gather
         self.engine = engine
         self.B = int(batch)
@@ -114,8 +120,9 @@ class DataParallelPipeline:
         self.cuda = dev.type == "cuda"
         shape = (self.B, cam_h, cam_w, 3)
         self.copy_stream = torch.cuda.Stream(dev) if self.cuda else None
-        self.staging = [torch.empty(shape, dtype=torch.uint8, device=dev) for _ in range(2)]
-        self.ready = [torch.cuda.Event() if self.cuda else None for _ in range(2)]
+        NS = self.nslots
+        self.staging = [torch.empty(shape, dtype=torch.uint8, device=dev) for _ in range(NS)]
+        self.ready = [torch.cuda.Event() if self.cuda else None for _ in range(NS)]
         self.slot = 0
         if ingest == "scatter" and ctx.is_root:
             self.node_batch = torch.empty((ctx.world * self.B,) + shape[1:], dtype=torch.uint8,
@@ -131,22 +138,22 @@ class DataParallelPipeline:
         # host-side buffers are double-buffered: with lag=1 step k+1 refills them
         # while step k's async copies may still be queued behind its compute
         self.meta_host = [torch.zeros((self.B, 3), dtype=torch.float64, pin_memory=self.cuda)
-                          for _ in range(2)]
+                          for _ in range(NS)]
         self.host_rec = [torch.empty((ctx.world, self.B, self.rec_width), dtype=torch.float32,
-                                     pin_memory=self.cuda) for _ in range(2)]
+                                     pin_memory=self.cuda) for _ in range(NS)]
         # host gather: this rank's records (D2H target) and the rank-0 landing buffers
         self.local_rec = [torch.empty((self.B, self.rec_width), dtype=torch.float32,
-                                      pin_memory=self.cuda) for _ in range(2)]
-        self.local_meta = [torch.empty((self.B, 3), dtype=torch.float64) for _ in range(2)]
+                                      pin_memory=self.cuda) for _ in range(NS)]
+        self.local_meta = [torch.empty((self.B, 3), dtype=torch.float64) for _ in range(NS)]
         self.host_meta_all = torch.empty((ctx.world, self.B, 3), dtype=torch.float64)
         if ctx.is_root and ctx.initialized:
             self.host_meta = [torch.empty((ctx.world, self.B, 3), dtype=torch.float64,
-                                          pin_memory=self.cuda) for _ in range(2)]
+                                          pin_memory=self.cuda) for _ in range(NS)]
         self._rslot = 0
-        self._pending = None  # (slot, event, fids, streams, ts) of the step not yet collected
+        self._pending = []  # (slot, event, fids, streams, ts) of the steps not yet collected
         self.frames_done = 0
         self.records_out = 0
-        self._prev_done = None  # compute-done event of the previous step
+        self._consumed = [None] * NS  # per staging slot: its last model finished reading it
         self.tracer = NULL_TRACER  # the serving loop installs its own (--profile)
         hm = getattr(engine, "_hip_model", None)
         if hm is not None and hasattr(hm, "pick_sync") and ctx.world > 1 and ctx.initialized:
@@ -165,7 +172,7 @@ class DataParallelPipeline:
     # ---------------------------------------------------------------- ingest
     def prefetch(self, host_frames: torch.Tensor) -> None:
         """Start the H2D of the next step's frames (pinned host tensor)."""
-        s = self.slot ^ 1
+        s = (self.slot + 1) % self.nslots
         if not self.cuda:
             if self.ingest == "scatter":
                 if self.ctx.is_root:
@@ -182,7 +189,7 @@ class DataParallelPipeline:
             self.ready[s].record(self.copy_stream)
 
     def _frames_for_step(self) -> torch.Tensor:
-        s = self.slot ^ 1
+        s = (self.slot + 1) % self.nslots
         self.slot = s
         if self.cuda:
             torch.cuda.current_stream(self.dev).wait_event(self.ready[s])
@@ -232,23 +239,23 @@ class DataParallelPipeline:
             fids, tss, strm = self._scatter_meta(fids, tss, strm)
         frames = self._frames_for_step()
         labels, packed = self.engine.run_device(frames)
-        if next_frames is not None:
-            if self.cuda:  # the staging slot being refilled was last read one step ago
-                self.copy_stream.wait_stream(torch.cuda.current_stream(self.dev)) \
-                    if self._prev_done is None else self.copy_stream.wait_event(self._prev_done)
-            self.prefetch(next_frames)
         if self.cuda:
             consumed = getattr(self.engine, "last_consumed", None)
-            if consumed is not None:  # slot-parallel engine: the model ran on its own stream
-                self._prev_done = consumed
-            else:
-                self._prev_done = torch.cuda.Event()
-                self._prev_done.record(torch.cuda.current_stream(self.dev))
+            if consumed is None:  # the model ran on the caller's stream
+                consumed = torch.cuda.Event()
+                consumed.record(torch.cuda.current_stream(self.dev))
+            self._consumed[self.slot] = consumed
+        if next_frames is not None:
+            if self.cuda:  # the staging slot being refilled was last read nslots - 1 steps ago
+                ev = self._consumed[(self.slot + 1) % self.nslots]
+                self.copy_stream.wait_stream(torch.cuda.current_stream(self.dev)) \
+                    if ev is None else self.copy_stream.wait_event(ev)
+            self.prefetch(next_frames)
         if packed is None:  # host post-processing path (torch backend / exact mode)
             self.frames_done += B * self.ctx.world
             return self.engine.records_from_labels(labels, fids, tss, strm)
         slot = self._rslot
-        self._rslot ^= 1
+        self._rslot = (self._rslot + 1) % self.nslots
         # the packed records are produced on the engine's result stream when its
         # post-processing runs on a stream of its own: gather + D2H go there too
         rs = getattr(self.engine, "result_stream", None) if self.cuda else None
@@ -260,11 +267,7 @@ class DataParallelPipeline:
                     ev = torch.cuda.Event()
                     ev.record(torch.cuda.current_stream(self.dev))
             self.frames_done += B * self.ctx.world
-            cur = (slot, ev, fids, strm, tss)
-            if not self.lag:
-                return self._collect(cur)
-            prev, self._pending = self._pending, cur
-            return self._collect(prev) if prev is not None else np.zeros(0, RECORD_DTYPE)
+            return self._enqueue((slot, ev, fids, strm, tss))
         with (torch.cuda.stream(rs) if rs is not None else contextlib.nullcontext()):
             if self.ctx.initialized:
                 mh = self.meta_host[slot]
@@ -290,16 +293,21 @@ class DataParallelPipeline:
             if self.cuda:
                 ev = torch.cuda.Event()
                 ev.record(torch.cuda.current_stream(self.dev))
-        cur = (slot, ev, fids, strm, tss)
-        if not self.lag:
-            return self._collect(cur)
-        prev, self._pending = self._pending, cur
-        return self._collect(prev) if prev is not None else np.zeros(0, RECORD_DTYPE)
+        return self._enqueue((slot, ev, fids, strm, tss))
+
+    def _enqueue(self, cur) -> np.ndarray:
+        """Queue this step's records; collect the step ``lag`` steps back (if any)."""
+        self._pending.append(cur)
+        if len(self._pending) > self.lag:
+            return self._collect(self._pending.pop(0))
+        return np.zeros(0, RECORD_DTYPE)
 
     def flush(self) -> np.ndarray:
-        """Collect the records of the last step (lag=1); no-op otherwise."""
-        prev, self._pending = self._pending, None
-        return self._collect(prev) if prev is not None else np.zeros(0, RECORD_DTYPE)
+        """Collect the records of every step not collected yet (lag >= 1)."""
+        out = [self._collect(p) for p in self._pending]
+        self._pending = []
+        out = [r for r in out if len(r)]
+        return np.concatenate(out) if out else np.zeros(0, RECORD_DTYPE)
 
     def _collect(self, pending) -> np.ndarray:
         with self.tracer.stage("collect"):

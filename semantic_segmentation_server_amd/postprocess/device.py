@@ -27,7 +27,7 @@ class DevicePostprocess:
     def _buffers(self, B: int):
         if B not in self._bufs:
             nbytes = hip_ops.post_workspace_bytes(B, self.H, self.W, self.K, self.bins)
-            ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            ws = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)  # deterministic start
             rec = torch.zeros((B, 1 + 5 * self.K), dtype=torch.float32, device=self.device)
             self._bufs[B] = (ws, rec)
         return self._bufs[B]

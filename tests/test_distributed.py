@@ -70,13 +70,19 @@ def _worker(rank, world, port, ingest, q, lag=0, gather="host"):
     # default frame ids advance per step by the frames of one rank (local ingest) or of
     # the whole node (scatter: ids are rank 0's node-level capture ids)
     adv = B * world if ingest == "scatter" else B
-    if lag:  # records arrive one step late; the second step's come with flush()
+    if lag:  # records arrive `lag` steps late; the later steps' come with flush()
         assert len(recs) == 0
-        pipe.prefetch(frames)
-        recs = pipe.step()
+        for k in range(lag):
+            pipe.prefetch(frames)
+            recs = pipe.step()
+            assert len(recs) == 0 or k == lag - 1
         last = pipe.flush()
         if ctx.is_root:
-            assert np.array_equal(last["cx"], recs["cx"]) and np.all(last["frame"] == recs["frame"] + adv)
+            n = len(recs)
+            assert n > 0 and len(last) == lag * n
+            for j in range(lag):
+                part = last[j * n:(j + 1) * n]
+                assert np.array_equal(part["cx"], recs["cx"]) and np.all(part["frame"] == recs["frame"] + (j + 1) * adv)
     t = D.allreduce_max(ctx, float(rank))
     if ctx.is_root:
         q.put((recs["cx"].tolist(), recs["stream"].tolist(), t, hub.depth))
@@ -87,7 +93,7 @@ def _worker(rank, world, port, ingest, q, lag=0, gather="host"):
 @pytest.mark.parametrize("world,ingest,lag,gather", [
     (2, "local", 0, "host"), (2, "scatter", 0, "host"), (3, "scatter", 0, "host"),
     (2, "local", 1, "host"), (2, "scatter", 1, "host"), (2, "local", 1, "rccl"),
-    (3, "scatter", 0, "rccl")])
+    (3, "scatter", 0, "rccl"), (2, "local", 2, "host"), (2, "scatter", 2, "host")])
 def test_dp_gather_and_scatter(world, ingest, lag, gather):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -105,7 +111,7 @@ def test_dp_gather_and_scatter(world, ingest, lag, gather):
     assert np.allclose(cx, exp, atol=1e-6)          # frame i went to rank i // B, came back in order
     assert streams == [i // B for i in range(world * B)]
     assert tmax == world - 1
-    assert depth == world * B * (2 if lag else 1)
+    assert depth == world * B * (lag + 1)
 
 
 def _scatter_meta_worker(rank, world, port, q):
