@@ -180,18 +180,23 @@ class DataParallelPipeline:
             else:
                 self.staging[s].copy_(host_frames)
             return
-        with torch.cuda.stream(self.copy_stream):
+        up = self.engine.upload_stream(self.staging[s]) \
+            if self.ingest != "scatter" and hasattr(self.engine, "upload_stream") else None
+        st = up if up is not None else self.copy_stream
+        with torch.cuda.stream(st):
             if self.ingest == "scatter":
                 if self.ctx.is_root:
                     self.node_batch.copy_(host_frames, non_blocking=True)
             else:
                 self.staging[s].copy_(host_frames, non_blocking=True)
-            self.ready[s].record(self.copy_stream)
+            self.ready[s].record(st)
 
     def _frames_for_step(self) -> torch.Tensor:
         s = (self.slot + 1) % self.nslots
         self.slot = s
-        if self.cuda:
+        on_slot = self.cuda and self.ingest != "scatter" and hasattr(self.engine, "upload_stream") \
+            and self.engine.upload_stream(self.staging[s]) is not None
+        if self.cuda and not on_slot:  # (uploads on the slot's own stream are ordered already)
             torch.cuda.current_stream(self.dev).wait_event(self.ready[s])
         if self.ingest == "scatter" and self.ctx.initialized:
             chunks = list(self.node_batch.chunk(self.ctx.world)) if self.ctx.is_root else None
@@ -246,8 +251,11 @@ class DataParallelPipeline:
                 consumed.record(torch.cuda.current_stream(self.dev))
             self._consumed[self.slot] = consumed
         if next_frames is not None:
-            if self.cuda:  # the staging slot being refilled was last read nslots - 1 steps ago
-                ev = self._consumed[(self.slot + 1) % self.nslots]
+            nxt = (self.slot + 1) % self.nslots
+            on_slot = self.cuda and hasattr(self.engine, "upload_stream") and \
+                self.engine.upload_stream(self.staging[nxt]) is not None and self.ingest != "scatter"
+            if self.cuda and not on_slot:  # the slot being refilled was last read nslots - 1 steps ago
+                ev = self._consumed[nxt]
                 self.copy_stream.wait_stream(torch.cuda.current_stream(self.dev)) \
                     if ev is None else self.copy_stream.wait_event(ev)
             self.prefetch(next_frames)
