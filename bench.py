@@ -102,9 +102,10 @@ def main() -> int:
     else:
         engine = Engine(cfg, ctx.device)
     hub = ResultHub(ctx.world * a.streams, maxlen=4096) if ctx.is_root else None
-    # lag=1: step k collects step k-1's records, so the next graph launch and the host
-    # unpack overlap the GPU instead of idling it; run_steps flushes the last step
-    # inside the timed region (every timed step's records reach the hub)
+    # lag=1 (raised to 2 by a slot-parallel engine, Engine.preferred_lag): step k collects
+    # step k-lag's records, so the next graph launches and the host unpack overlap the GPU
+    # instead of idling it; run_steps flushes the last steps inside the timed region (every
+    # timed step's records reach the hub)
     pipe = DataParallelPipeline(ctx, engine, cam_w, cam_h, a.batch, a.ingest, hub, a.streams,
                                 lag=1, gather=a.gather)
 
@@ -192,6 +193,8 @@ def main() -> int:
                 "streams_per_gpu": a.streams,
                 "stream_mode": "per-stream graphs" if (a.streams > 1 and a.per_stream_graphs)
                 else "batched",
+                "pipeline_lag": pipe.lag,
+                "slot_parallel": bool(getattr(engine, "slot_parallel", False)),
             },
             "p50_get_segmented_objects_ms": rpc.get("p50_ms") if rpc else None,
             "p99_get_segmented_objects_ms": rpc.get("p99_ms") if rpc else None,
@@ -268,7 +271,7 @@ def _serve_bench(a) -> int:
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
             "data": f"synthetic {a.camera} BGR frames, random-init weights",
             "config": {"model": _model_name(a), "global_batch": a.batch * world, "seq_len": a.input_size,
-                       "parallelism": f"dp{world}", "mode": "served (feeder + lag-1 pipeline + gRPC)",
+                       "parallelism": f"dp{world}", "mode": "served (feeder + lagged pipeline + gRPC)",
                        "streams_per_gpu": a.streams},
             "p50_get_segmented_objects_ms": rpc.get("p50_ms") if rpc else None,
             "p99_get_segmented_objects_ms": rpc.get("p99_ms") if rpc else None,

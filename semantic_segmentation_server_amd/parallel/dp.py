@@ -102,10 +102,12 @@ class DataParallelPipeline:
         self.ctx = ctx
         # lag L >= 1: step k collects step k-L's records, with L + 1 staging slots (so L + 1
         # steps can be in flight on a slot-parallel engine); SSA_PIPE_LAG overrides a
-        # non-zero lag (experiments: 2 = three slots)
+        # non-zero lag, else the engine may ask for more depth (slot-parallel: 2)
         self.lag = max(0, min(3, int(lag)))
         if self.lag and os.environ.get("SSA_PIPE_LAG"):
             self.lag = max(1, min(3, int(os.environ["SSA_PIPE_LAG"])))
+        elif self.lag and hasattr(engine, "preferred_lag"):
+            self.lag = max(self.lag, int(engine.preferred_lag()))
         self.nslots = max(2, self.lag + 1)
         self.gather_mode = gather
         self.engine = engine

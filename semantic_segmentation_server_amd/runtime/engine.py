@@ -323,6 +323,19 @@ class Engine:
             self._bound_graphs[key] = ent
         return ent
 
+    def preferred_lag(self) -> int:
+        """Pipeline lag this engine runs best at: 2 (three staging slots, three steps in
+        flight) when it will run slot-parallel with uploads on the slot streams -- 3 slot
+        streams + the result stream fit the 4 hardware queues. Measured: B = 32 30.9k /
+        29.2k vs 28.3k / 28.0k frames/s at lag 1; batch 1 0.236 vs 0.351 ms per frame
+        (profiles/r2_lag_ab.txt). Otherwise 1."""
+        ok = (self.is_cuda and self.cfg.graph and self._use_device_post()
+              and hasattr(self._hip_model, "_labels_out")
+              and os.environ.get("SSA_SPLIT_POST", "1") != "0"
+              and os.environ.get("SSA_SLOT_PARALLEL", "1") == "1"
+              and os.environ.get("SSA_H2D_ON_SLOT", "1") == "1")
+        return 2 if ok else 1
+
     def upload_stream(self, buf: torch.Tensor):
         """Stream to upload a bound staging slot's frames on (SSA_H2D_ON_SLOT), else None."""
         if not getattr(self, "h2d_on_slot", False):
