@@ -106,7 +106,7 @@ class DataParallelPipeline:
         self.lag = max(0, min(3, int(lag)))
         if self.lag and os.environ.get("SSA_PIPE_LAG"):
             self.lag = max(1, min(3, int(os.environ["SSA_PIPE_LAG"])))
-        elif self.lag and hasattr(engine, "preferred_lag"):
+        elif self.lag and hasattr(engine, "preferred_lag") and ingest != "scatter":
             self.lag = max(self.lag, int(engine.preferred_lag()))
         self.nslots = max(2, self.lag + 1)
         self.gather_mode = gather
@@ -125,6 +125,7 @@ class DataParallelPipeline:
         NS = self.nslots
         self.staging = [torch.empty(shape, dtype=torch.uint8, device=dev) for _ in range(NS)]
         self.ready = [torch.cuda.Event() if self.cuda else None for _ in range(NS)]
+        self.last_upload = None  # event of the most recent prefetch's H2D copy
         self.slot = 0
         if ingest == "scatter" and ctx.is_root:
             self.node_batch = torch.empty((ctx.world * self.B,) + shape[1:], dtype=torch.uint8,
@@ -170,6 +171,10 @@ class DataParallelPipeline:
             # stream, concurrently with step k+1's model
             split = bool(self.lag) and os.environ.get("SSA_SPLIT_POST", "1") != "0"
             engine.bind_inputs(self.staging, split_post=split)
+            if ingest == "scatter" and getattr(engine, "h2d_on_slot", False):
+                # scattered frames land on the caller's stream (RCCL / gloo), not on a slot
+                # stream: the slot's model must fork from the caller's stream
+                engine.h2d_on_slot = False
 
     # ---------------------------------------------------------------- ingest
     def prefetch(self, host_frames: torch.Tensor) -> None:
@@ -191,7 +196,12 @@ class DataParallelPipeline:
                     self.node_batch.copy_(host_frames, non_blocking=True)
             else:
                 self.staging[s].copy_(host_frames, non_blocking=True)
-            self.ready[s].record(st)
+            # a fresh event per upload: the serving driver hands the pinned host batch back
+            # to its feeder only once THIS copy has completed (last_upload)
+            ev = torch.cuda.Event()
+            ev.record(st)
+            self.ready[s] = ev
+            self.last_upload = ev
 
     def _frames_for_step(self) -> torch.Tensor:
         s = (self.slot + 1) % self.nslots

@@ -46,10 +46,14 @@ class PipelineDriver:
 
     # ------------------------------------------------------------------ helpers
     def _h2d_event(self) -> Optional["torch.cuda.Event"]:
+        """Completion event of the H2D copy the pipeline just issued for this batch (on the
+        copy stream or, slot-parallel, on the slot's model stream)."""
         if not self.pipe.cuda:
             return None
-        ev = torch.cuda.Event()
-        ev.record(self.pipe.copy_stream)
+        ev = getattr(self.pipe, "last_upload", None)
+        if ev is None:
+            ev = torch.cuda.Event()
+            ev.record(self.pipe.copy_stream)
         return ev
 
     def _release_done(self, force: bool = False) -> None:
