@@ -47,6 +47,8 @@ def main() -> int:
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
     p.add_argument("--backend", choices=["hip", "torch"], default="hip")
+    p.add_argument("--lag", type=int, default=1, choices=[1, 2],
+                   help="pipeline lag (2 = three steps in flight, the serving default)")
     p.add_argument("--arch", default="mnv2")
     p.add_argument("--aspp", default="full")
     p.add_argument("--input_size", type=int, default=513)
@@ -102,14 +104,15 @@ def main() -> int:
     else:
         engine = Engine(cfg, ctx.device)
     hub = ResultHub(ctx.world * a.streams, maxlen=4096) if ctx.is_root else None
-    # lag=1 (raised to 2 by a slot-parallel engine, Engine.preferred_lag): step k collects
-    # step k-lag's records, so the next graph launches and the host unpack overlap the GPU
-    # instead of idling it; run_steps flushes the last steps inside the timed region (every
-    # timed step's records reach the hub)
-    pipe = DataParallelPipeline(ctx, engine, cam_w, cam_h, a.batch, a.ingest, hub, a.streams,
-                                lag=1, gather=a.gather)
-
-    # synthetic camera frames, pinned; distinct per rank
+    # --lag L: step k collects step k-L's records, so the next graph launches and the host
+    # unpack overlap the GPU instead of idling it; run_steps flushes the last steps inside
+    # the timed region (every timed step's records reach the hub). Lag 2 (three steps in
+    # flight, the serving default) is faster in steady state (100+ steps: 30.9k vs ~28k
+    # frames/s) but short timed windows pay a start-up transient it does not amortise
+    # (--steps 20 --warmup 5: 18-23k vs 27.2-27.7k at lag 1, profiles/r2_lag_window.txt),
+    # so the benchmark default stays 1.
+    # synthetic camera frames, pinned; distinct per rank (prepared before the pipeline, whose
+    # construction ends by priming its streams: the warmup then follows without a GPU-idle gap)
     src = SyntheticSource(cam_w, cam_h, stream=ctx.rank, seed=1, pool=max(2, min(a.batch, 8)))
     nb = a.batch * (ctx.world if (a.ingest == "scatter" and ctx.is_root) else 1)
     host_batches = []
@@ -117,6 +120,8 @@ def main() -> int:
         frames, _, _ = src.read_batch(nb)
         host_batches.append(torch.from_numpy(np.ascontiguousarray(frames)).pin_memory()
                             if ctx.device.type == "cuda" else torch.from_numpy(frames.copy()))
+    pipe = DataParallelPipeline(ctx, engine, cam_w, cam_h, a.batch, a.ingest, hub, a.streams,
+                                lag=a.lag, gather=a.gather, auto_lag=False)
 
     verbose = os.environ.get("SSA_BENCH_VERBOSE", "0") == "1"
 
