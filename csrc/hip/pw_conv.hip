@@ -84,9 +84,7 @@ __global__ __launch_bounds__(256) void pw_conv_kernel(PwArgs a) {
 
   // Output through a range-checked buffer descriptor: a store whose offset lies
   // beyond num_records is dropped by the hardware, so masked lanes (M tail,
-  // channel padding) need no branch and every wave issues exactly 2*MT stores per
-  // chunk. That fixed count is what lets the chunk wait below leave the previous
-  // chunk's stores in flight (vmcnt(2*MT)) instead of draining them (vmcnt(0)).
+  // channel padding) need no branch.
   const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, a.out_bytes, 0x00020000);
   // activation as a branch-free clamp
   const float lo = a.act == ACT_NONE ? -INFINITY : 0.f;
@@ -96,8 +94,13 @@ __global__ __launch_bounds__(256) void pw_conv_kernel(PwArgs a) {
     // chunk c has landed (this wave's DMA + everyone's, via the barrier), and every
     // wave is done reading the other buffer (chunk c-1): refill it with chunk c+1.
     // VMEM ops younger than chunk c's DMA: only the previous chunk's 2*MT stores.
-    if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * MT) : "memory");
+    // vmcnt(0): the chunk's LDS-DMA must have landed. A counted wait that left the previous
+    // chunk's 2*MT stores in flight (vmcnt(2*MT)) assumed the stores retire after the older
+    // DMA; under memory pressure from concurrent kernels they can retire first, the count
+    // then passes with DMA pieces still in flight and the MFMAs read stale weights
+    // (label maps differed in ~7 % of runs with plan copies on three streams,
+    // scripts/debug_race.py).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // raw s_barrier: __syncthreads() carries a workgroup release that makes the
     // compiler drain every outstanding store (vmcnt(0)) first. LDS reads of the
     // previous chunk are all consumed by MFMAs already, so none is pending here.

@@ -269,6 +269,7 @@ class HipDeepLab:
         self._plans: Dict[tuple, Tuple[List[Callable], Dict[str, torch.Tensor]]] = {}
         self._span_tables: Dict[tuple, dict] = {}
         self._labels_out: Optional[torch.Tensor] = None
+        self._guards: list = []  # SSA_GUARD_BYTES debug bands (name, raw, guard, nbytes)
 
     # ------------------------------------------------------------------ plan
     def _plan(self, B: int, Hc: int, Wc: int, part: int = 0):
@@ -282,9 +283,22 @@ class HipDeepLab:
         bufs: Dict[str, torch.Tensor] = {}
         ops: List[Callable] = []
 
+        guard = int(os.environ.get("SSA_GUARD_BYTES", "0"))  # debug: sentinel bands
+
         def buf(name, *shape, dtype=torch.bfloat16):
             # zeroed: a plan copy must start from the same bytes as the plan it copies
             # (channel / tile padding that some variant reads but only others write)
+            if guard:  # debug (scripts/debug_guard.py): 0x5A bands before and after
+                n = 1
+                for d_ in shape:
+                    n *= d_
+                nb = n * torch.tensor([], dtype=dtype).element_size()
+                raw = torch.full((nb + 2 * guard,), 0x5A, dtype=torch.uint8, device=dev)
+                raw[guard:guard + nb].zero_()
+                t = raw[guard:guard + nb].view(dtype).view(*shape)
+                self._guards.append((name, raw, guard, nb))
+                bufs[name] = t
+                return t
             t = torch.zeros(shape, dtype=dtype, device=dev)
             bufs[name] = t
             return t
