@@ -31,7 +31,7 @@ def pin(ops):
     for op in ops:
         if isinstance(op, Choice):
             for pre, var in force:
-                if op.name.startswith(pre):
+                if op.name == pre or (pre.endswith("*") and op.name.startswith(pre[:-1])):
                     idx = [n for n, _ in op.variants]
                     if var in idx:
                         op.pick = idx.index(var)
