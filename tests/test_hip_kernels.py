@@ -497,6 +497,38 @@ def _small_cfg(**kw):
     return C.Config(**base)
 
 
+def test_hip_model_headline_shape_matches_torch():
+    """The headline shape (513^2, 640x480 camera) at B = 16 with the committed MI355X picks:
+    grids large enough that several workgroups of a kernel share a CU (the small-shape test
+    below runs most kernels at one workgroup per CU). Bound relative to stock PyTorch bf16
+    on the same GPU, as below."""
+    from semantic_segmentation_server_amd.models.deeplab import build_model
+    from semantic_segmentation_server_amd.models.hip_model import HipDeepLab
+    from semantic_segmentation_server_amd.ops import reference_ops as R
+    S, B = 513, 16
+    model = build_model("mnv2", 21, calibrate_hw=129)
+    cfg = _small_cfg(input_size=S)
+    hm = HipDeepLab(model, torch.device(DEV), cfg)
+    lx, ly, *_ = R.letterbox_luts(640, 480, S, S)
+    rng = np.random.default_rng(9)
+    frames = torch.from_numpy(rng.integers(0, 256, (B, 480, 640, 3), dtype=np.uint8))
+    x = R.preprocess(frames, lx, ly).to(DEV)
+    import copy
+    with torch.no_grad():
+        ref_logits = copy.deepcopy(model).to(DEV)(x).float().cpu()
+        bf_logits = copy.deepcopy(model).to(DEV, torch.bfloat16)(x.to(torch.bfloat16)).float().cpu()
+    dl = hm.logits(frames.to(DEV), torch.tensor(lx, device=DEV), torch.tensor(ly, device=DEV))
+    torch.cuda.synchronize()
+    got = _nchw(dl.float()).cpu()
+    e_hip, e_bf = _rel(got, ref_logits), _rel(bf_logits, ref_logits)
+    print(f"headline shape B={B}: rel err hip={e_hip:.4f} torch-bf16={e_bf:.4f}")
+    assert e_hip < 1.5 * e_bf + 0.01, (e_hip, e_bf)
+    # deterministic: a second run of the same plan gives the same logits bit for bit
+    dl2 = hm.logits(frames.to(DEV), torch.tensor(lx, device=DEV), torch.tensor(ly, device=DEV))
+    torch.cuda.synchronize()
+    assert torch.equal(_nchw(dl2.float()).cpu(), got)
+
+
 @pytest.mark.parametrize("arch,aspp", [("mnv2", "full"), ("mnv2", "mobile"), ("resnet50", "full")])
 def test_hip_model_matches_torch(arch, aspp):
     """Whole network vs the fp32 torch model. bf16 activations drift over ~60
