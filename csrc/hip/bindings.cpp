@@ -291,10 +291,13 @@ PYBIND11_MODULE(_hip, m) {
   });
 
   m.def("aspp_pool", [](uintptr_t in, uintptr_t ws, uintptr_t w1t, uintptr_t b1, uintptr_t w2t,
-                        uintptr_t img_bias, int B, int HW, int C, int N, uintptr_t stream) {
+                        uintptr_t img_bias, int B, int HW, int C, int N, uintptr_t stream,
+                        uintptr_t dbg, int mode) {
     aspp_pool(P<const bf16>(in), P<float>(ws), P<const float>(w1t), P<const float>(b1), P<const float>(w2t),
-              P<float>(img_bias), B, HW, C, N, S(stream));
-  });
+              P<float>(img_bias), B, HW, C, N, S(stream), P<float>(dbg), mode);
+  }, py::arg("in"), py::arg("ws"), py::arg("w1t"), py::arg("b1"), py::arg("w2t"), py::arg("img_bias"),
+     py::arg("B"), py::arg("HW"), py::arg("C"), py::arg("N"), py::arg("stream"), py::arg("dbg") = 0,
+     py::arg("mode") = 0);
 
   m.def("upsample_argmax", [](uintptr_t logits, uintptr_t labels, int B, int h, int w, int K,
                               int ldk, int H, int W, uintptr_t stream, int variant) {
@@ -303,6 +306,10 @@ PYBIND11_MODULE(_hip, m) {
   });
 
   m.def("post_workspace_bytes", &post_workspace_bytes);
+  m.def("poison_lds", [](uint32_t pat, int blocks, uintptr_t stream) {
+    poison_lds(pat, blocks, S(stream));
+  });
+  m.def("poison_regs", [](int blocks, uintptr_t stream) { poison_regs(blocks, S(stream)); });
   m.def("postprocess",
         [](uintptr_t labels, int B, int H, int W, int crop_h, int crop_w, uintptr_t palette,
            int thr, double min_area, int num_bins, int K, uintptr_t ws, uintptr_t records,

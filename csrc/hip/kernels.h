@@ -245,7 +245,8 @@ void global_avgpool(const bf16* in, float* out, float* ws, int B, int HW, int C,
 void bias_act(const bf16* in, const float* bias, const float* img_bias, bf16* out, long long M, int N,
               int HW, int act, hipStream_t s);
 void aspp_pool(const bf16* in, float* ws, const float* w1t, const float* b1, const float* w2t,
-               float* img_bias, int B, int HW, int C, int N, hipStream_t s);
+               float* img_bias, int B, int HW, int C, int N, hipStream_t s, float* dbg = nullptr,
+               int mode = 0);
 void matvec(const float* x, const float* w, const float* bias, float* out, int B, int N, int K,
             int act, hipStream_t s);
 
@@ -271,6 +272,11 @@ struct PostParams {
   float* records = nullptr;         // [B, 1 + 5K] packed output
 };
 size_t post_workspace_bytes(int B, int H, int W, int K, int num_bins);
+
+// Debug only (debug_poison.hip): NaN-pattern fill of every CU's LDS / every SIMD's
+// VGPR+AGPR file, to expose kernels that read on-chip state they did not write.
+void poison_lds(uint32_t pat, int blocks, hipStream_t s);
+void poison_regs(int blocks, hipStream_t s);
 void postprocess(const PostParams& p, hipStream_t s);
 
 }  // namespace ssa

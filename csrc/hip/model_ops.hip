@@ -554,8 +554,9 @@ __global__ __launch_bounds__(kPoolThreads) void aspp_pool_kernel(const float* __
                                                                  const float* __restrict__ b1,
                                                                  const float* __restrict__ w2t,
                                                                  float* __restrict__ img_bias, int HW,
-                                                                 int C, int N) {
+                                                                 int C, int N, float* dbg, int mode) {
   __shared__ float s_gap[kPoolMaxC];
+  if (mode & 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   __shared__ float s_pool[kPoolMaxN];
   __shared__ float4 s_red[kPoolThreads];
   const int b = blockIdx.x, tid = threadIdx.x;
@@ -571,6 +572,8 @@ __global__ __launch_bounds__(kPoolThreads) void aspp_pool_kernel(const float* __
   const int nks = kPoolThreads / nq;        // K slices
   const int q = tid % nq, ks = tid / nq;
   __syncthreads();
+  if (dbg)  // debug (scripts/debug_stress.py): what this workgroup reduced from part
+    for (int k = tid; k < C; k += kPoolThreads) dbg[(size_t)b * (C + N) + k] = s_gap[k];
   {
     const int per = (C + nks - 1) / nks;
     const int k0 = min(C, ks * per), k1 = min(C, k0 + per);
@@ -589,6 +592,8 @@ __global__ __launch_bounds__(kPoolThreads) void aspp_pool_kernel(const float* __
     s_pool[4 * tid + 3] = fmaxf(s.w + b1[4 * tid + 3], 0.f);
   }
   __syncthreads();
+  if (dbg)
+    for (int k = tid; k < N; k += kPoolThreads) dbg[(size_t)b * (C + N) + C + k] = s_pool[k];
   {
     const int per = (N + nks - 1) / nks;
     const int k0 = min(N, ks * per), k1 = min(N, k0 + per);
@@ -606,12 +611,14 @@ __global__ __launch_bounds__(kPoolThreads) void aspp_pool_kernel(const float* __
 }
 
 void aspp_pool(const bf16* in, float* ws, const float* w1t, const float* b1, const float* w2t,
-               float* img_bias, int B, int HW, int C, int N, hipStream_t s) {
+               float* img_bias, int B, int HW, int C, int N, hipStream_t s, float* dbg, int mode) {
   if (C > kPoolMaxC || N > kPoolMaxN || C % 8 || N % 4)
     throw std::invalid_argument("aspp_pool: C <= 2048, C % 8, N <= 512, N % 4");
-  hipLaunchKernelGGL(gap_partial_kernel, dim3(B, kGapSlices, cdiv(C / 8, 64)), dim3(256), 0, s, in,
-                     ws, HW, C);
-  hipLaunchKernelGGL(aspp_pool_kernel, dim3(B), dim3(kPoolThreads), 0, s, ws, w1t, b1, w2t, img_bias, HW, C, N);
+  if (!(mode & 2))  // bit 1 (debug): reuse the partial sums already in ws
+    hipLaunchKernelGGL(gap_partial_kernel, dim3(B, kGapSlices, cdiv(C / 8, 64)), dim3(256), 0, s, in,
+                       ws, HW, C);
+  hipLaunchKernelGGL(aspp_pool_kernel, dim3(B), dim3(kPoolThreads), 0, s, ws, w1t, b1, w2t, img_bias, HW,
+                     C, N, dbg, mode);
   check_launch("aspp_pool");
 }
 

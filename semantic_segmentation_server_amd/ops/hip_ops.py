@@ -834,3 +834,13 @@ def postprocess(labels, palette, ws, records, *, B, H, W, crop_h, crop_w, min_ar
                            float(min_area), bins, K, _ptr(ws), _ptr(records), _stream())
     _dbg('postprocess')
     return records
+
+
+def poison_chip(lds: bool = True, regs: bool = True, pat: int = 0x7FC07FC0) -> None:
+    """Debug (scripts/debug_poison.py): fill every CU's LDS and every SIMD's register
+    file with a NaN pattern, so the next kernel sees poison wherever it reads on-chip
+    state it did not write itself."""
+    if lds:
+        _hip_mod().poison_lds(pat, 256 * 8, _stream())
+    if regs:
+        _hip_mod().poison_regs(256 * 4 * 8, _stream())
