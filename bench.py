@@ -54,15 +54,14 @@ def main() -> int:
     p.add_argument("--input_size", type=int, default=513)
     p.add_argument("--camera", default="640x480")
     p.add_argument("--ingest", choices=["local", "scatter"], default="local")
-    p.add_argument("--gather", choices=["host", "rccl"], default="host",
-                   help="record gather to rank 0: pinned-host + gloo (default) or RCCL")
+    p.add_argument("--gather", choices=["auto", "host", "rccl"], default="auto",
+                   help="record gather to rank 0: auto = RCCL over xGMI when N > 1 (the "
+                        "multi-GPU data path), else none needed; host = pinned host + gloo")
     p.add_argument("--pg", choices=["auto", "nccl", "gloo"], default="auto",
-                   help="process-group backend; auto: RCCL when an RCCL data path is requested "
-                        "(--ingest scatter / --gather rccl), else gloo. Measured on one MI355X "
-                        "(world-size-1 groups, profiles/r2_pg_ab.txt): no group 24.33k, gloo + "
-                        "host gather 24.42k, RCCL + host gather 23.60k, RCCL + RCCL gather "
-                        "24.07k frames/s -- equal within noise; the host gather stays the "
-                        "default (no collective kernel in the GPU stream, rehearsed at dp8)")
+                   help="process-group backend; auto: RCCL (+ a gloo control group) when "
+                        "N > 1 on GPUs or an RCCL data path is requested, else gloo. Measured on "
+                        "one MI355X (world-size-1 groups, profiles/r2_pg_ab.txt): RCCL + RCCL "
+                        "gather 24.07k vs gloo + host gather 24.42k frames/s, equal within noise")
     p.add_argument("--contour_mode", choices=["fast", "exact", "none"], default="fast")
     p.add_argument("--no-graph", dest="graph", action="store_false")
     p.add_argument("--rpc", type=int, default=2000, help="GetSegmentedObjects calls to time (0: skip)")
@@ -89,8 +88,12 @@ def main() -> int:
     from semantic_segmentation_server_amd.runtime.results import ResultHub
     from semantic_segmentation_server_amd.runtime.sources import SyntheticSource
 
-    pg = a.pg if a.pg != "auto" else ("nccl" if (a.ingest == "scatter" or a.gather == "rccl") else "gloo")
     import torch as _t
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    gpu = _t.cuda.is_available() and a.backend != "cpu"
+    pg = a.pg if a.pg != "auto" else (
+        "nccl" if gpu and (a.ingest == "scatter" or a.gather == "rccl" or
+                           (a.gather == "auto" and world > 1)) else "gloo")
     ctx = D.init(pg, device="cuda" if _t.cuda.is_available() and a.backend != "cpu" else "auto")
     cam_w, cam_h = (int(v) for v in a.camera.split("x"))
     cfg = C.Config(arch=a.arch, aspp=a.aspp, input_size=a.input_size, backend=a.backend,
@@ -190,7 +193,7 @@ def main() -> int:
                 "classes": cfg.num_classes,
                 "parallelism": f"dp{ctx.world}",
                 "ingest": a.ingest,
-                "gather": a.gather,
+                "gather": pipe.gather_mode,
                 "process_group": ctx.backend,
                 "backend": a.backend,
                 "hipgraph": bool(a.graph and ctx.device.type == "cuda"),

@@ -277,6 +277,7 @@ size_t post_workspace_bytes(int B, int H, int W, int K, int num_bins);
 // VGPR+AGPR file, to expose kernels that read on-chip state they did not write.
 void poison_lds(uint32_t pat, int blocks, hipStream_t s);
 void poison_regs(int blocks, hipStream_t s);
+void lds_canary(int iters, unsigned* bad, int blocks, hipStream_t s);
 void postprocess(const PostParams& p, hipStream_t s);
 
 }  // namespace ssa

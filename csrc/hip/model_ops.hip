@@ -528,7 +528,7 @@ void matvec(const float* x, const float* w, const float* bias, float* out, int B
 // outputs (one float4 weight load per k) and a K slice; the slices are summed through
 // LDS. A first version gave each thread whole K=320 dot products: ~80 dependent L2
 // round trips per thread, 30 us for one image (profiles/r2_b1 trace).
-constexpr int kPoolMaxC = 2048, kPoolMaxN = 512, kPoolThreads = 1024;
+constexpr int kPoolMaxC = 2048, kPoolMaxN = 512;
 
 __device__ __forceinline__ float4 pool_slice(const float* __restrict__ wt, const float* s_x, int k0,
                                              int k1, int N, int q) {
@@ -549,6 +549,7 @@ __device__ __forceinline__ float4 pool_slice(const float* __restrict__ wt, const
   return make_float4(a0.x + a1.x, a0.y + a1.y, a0.z + a1.z, a0.w + a1.w);
 }
 
+template <int kPoolThreads>
 __global__ __launch_bounds__(kPoolThreads) void aspp_pool_kernel(const float* __restrict__ part,
                                                                  const float* __restrict__ w1t,
                                                                  const float* __restrict__ b1,
@@ -572,18 +573,28 @@ __global__ __launch_bounds__(kPoolThreads) void aspp_pool_kernel(const float* __
   const int nks = kPoolThreads / nq;        // K slices
   const int q = tid % nq, ks = tid / nq;
   __syncthreads();
-  if (dbg)  // debug (scripts/debug_stress.py): what this workgroup reduced from part
-    for (int k = tid; k < C; k += kPoolThreads) dbg[(size_t)b * (C + N) + k] = s_gap[k];
+  // debug (scripts/debug_pool.py): per image [C gap | N pool | 4 x 1024 float4 stage views]
+  const size_t dstride = (size_t)C + N + 4 * 4 * kPoolThreads;
+  float* dimg = dbg ? dbg + (size_t)b * dstride : nullptr;
+  float4* dv = dbg ? reinterpret_cast<float4*>(dimg + C + N) : nullptr;
+  if (dbg)
+    for (int k = tid; k < C; k += kPoolThreads) dimg[k] = s_gap[k];
   {
     const int per = (C + nks - 1) / nks;
     const int k0 = min(C, ks * per), k1 = min(C, k0 + per);
-    if (ks < nks) s_red[ks * nq + q] = pool_slice(w1t, s_gap, k0, k1, N, q);
+    if (ks < nks) {
+      const float4 r = pool_slice(w1t, s_gap, k0, k1, N, q);
+      s_red[ks * nq + q] = r;
+      if (dbg) dv[tid] = r;
+    }
   }
   __syncthreads();
   if (tid < nq) {
     float4 s = s_red[tid];
+    if (dbg) dv[kPoolThreads + tid] = s;
     for (int j = 1; j < nks; ++j) {
       const float4 v = s_red[j * nq + tid];
+      if (dbg) dv[kPoolThreads + j * nq + tid] = v;
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
     s_pool[4 * tid + 0] = fmaxf(s.x + b1[4 * tid + 0], 0.f);
@@ -593,17 +604,23 @@ __global__ __launch_bounds__(kPoolThreads) void aspp_pool_kernel(const float* __
   }
   __syncthreads();
   if (dbg)
-    for (int k = tid; k < N; k += kPoolThreads) dbg[(size_t)b * (C + N) + C + k] = s_pool[k];
+    for (int k = tid; k < N; k += kPoolThreads) dimg[C + k] = s_pool[k];
   {
     const int per = (N + nks - 1) / nks;
     const int k0 = min(N, ks * per), k1 = min(N, k0 + per);
-    if (ks < nks) s_red[ks * nq + q] = pool_slice(w2t, s_pool, k0, k1, N, q);
+    if (ks < nks) {
+      const float4 r = pool_slice(w2t, s_pool, k0, k1, N, q);
+      s_red[ks * nq + q] = r;
+      if (dbg) dv[2 * kPoolThreads + tid] = r;
+    }
   }
   __syncthreads();
   if (tid < nq) {
     float4 s = s_red[tid];
+    if (dbg) dv[3 * kPoolThreads + tid] = s;
     for (int j = 1; j < nks; ++j) {
       const float4 v = s_red[j * nq + tid];
+      if (dbg) dv[3 * kPoolThreads + j * nq + tid] = v;
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
     *reinterpret_cast<float4*>(img_bias + (size_t)b * N + 4 * tid) = s;
@@ -617,8 +634,16 @@ void aspp_pool(const bf16* in, float* ws, const float* w1t, const float* b1, con
   if (!(mode & 2))  // bit 1 (debug): reuse the partial sums already in ws
     hipLaunchKernelGGL(gap_partial_kernel, dim3(B, kGapSlices, cdiv(C / 8, 64)), dim3(256), 0, s, in,
                        ws, HW, C);
-  hipLaunchKernelGGL(aspp_pool_kernel, dim3(B), dim3(kPoolThreads), 0, s, ws, w1t, b1, w2t, img_bias, HW,
-                     C, N, dbg, mode);
+  // mode bits 2/3 (debug): 256 / 512 threads per workgroup instead of 1024
+  if (mode & 4)
+    hipLaunchKernelGGL(aspp_pool_kernel<256>, dim3(B), dim3(256), 0, s, ws, w1t, b1, w2t, img_bias, HW, C,
+                       N, dbg, mode);
+  else if (mode & 8)
+    hipLaunchKernelGGL(aspp_pool_kernel<512>, dim3(B), dim3(512), 0, s, ws, w1t, b1, w2t, img_bias, HW, C,
+                       N, dbg, mode);
+  else
+    hipLaunchKernelGGL(aspp_pool_kernel<1024>, dim3(B), dim3(1024), 0, s, ws, w1t, b1, w2t, img_bias, HW,
+                       C, N, dbg, mode);
   check_launch("aspp_pool");
 }
 

@@ -35,6 +35,11 @@ ws, ib = bufs["gap_ws"], bufs["img_bias"]
 w1t, w2t, b1 = bufs["pool_w1t"], bufs["pool_w2t"], hm.pool_b
 Bq, h, w, Cc = x.shape
 N = ib.shape[1]
+NT = 256 if MODE & 4 else 512 if MODE & 8 else 1024
+# reference: this mode's own kernel, run alone (summation order differs between modes)
+H().aspp_pool(x.data_ptr(), ws.data_ptr(), w1t.data_ptr(), b1.data_ptr(), w2t.data_ptr(),
+              ib.data_ptr(), B, h * w, Cc, N, torch.cuda.current_stream().cuda_stream, 0, MODE)
+torch.cuda.synchronize()
 ib_ref = ib.clone()
 ws_ref = ws.clone()
 part = ws_ref.view(B, 16, Cc).double().sum(1) / (h * w)
@@ -52,7 +57,8 @@ for k in (1, 2):
     noise.append((s, g))
 torch.cuda.synchronize()
 main = torch.cuda.Stream()
-dbg = torch.zeros((REPS, B, Cc + N), dtype=torch.float32, device="cuda")
+DS = Cc + N + 4 * 4 * NT
+dbg = torch.zeros((REPS, B, DS), dtype=torch.float32, device="cuda")
 outs = torch.zeros((REPS, B, N), dtype=torch.float32, device="cuda")
 wss = torch.zeros((REPS,) + tuple(ws.shape), dtype=torch.float32, device="cuda")
 done = 0
@@ -74,19 +80,41 @@ bad_out = (outs != ib_ref).any(2).any(1)
 print(f"mode {MODE}: runs with wrong img_bias {int(bad_out.sum())} / {REPS}; ws ever wrong: "
       f"{int((wss != ws_ref).any(1).sum())}", flush=True)
 gap_ref32 = (ws_ref.view(B, 16, Cc).sum(1) / (h * w))  # fp32 order differs: tolerance
-for r in bad_out.nonzero().view(-1).tolist()[:8]:
-    g = dbg[r, :, :Cc].double()
-    pl = dbg[r, :, Cc:].double()
-    gd = (g - part).abs()
-    pd = (pl - pool_ref).abs()
+w1d, w2d = w1t.double(), w2t.double()
+
+
+def stage_expect(x, wt, K_):
+    """per-thread float4 slice sums of stage with input vector x (K_ long), NT threads"""
+    nq, nks = N // 4, NT // (N // 4)
+    per = (K_ + nks - 1) // nks
+    out = torch.zeros(NT, 4, dtype=torch.float64)
+    for t in range(NT):
+        ks, q = t // nq, t % nq
+        k0 = min(K_, ks * per)
+        k1 = min(K_, k0 + per)
+        if k1 > k0:
+            out[t] = (x[k0:k1, None] * wt[k0:k1, 4 * q:4 * q + 4]).sum(0)
+    return out
+
+
+for r in bad_out.nonzero().view(-1).tolist()[:6]:
     bi = (outs[r] != ib_ref).any(1).nonzero().view(-1).tolist()
-    worst = gd.max(1)
-    print(f"  run {r}: bad images {bi}; max |gap - ref| per image {[f'{v:.2e}' for v in worst.values.tolist()]} "
-          f"at ch {worst.indices.tolist()}; max |pool - ref| {[f'{v:.2e}' for v in pd.max(1).values.tolist()]}",
-          flush=True)
     for b in bi:
-        bad_ch = (gd[b] > 1e-4).nonzero().view(-1).tolist()
-        print(f"    image {b}: gap channels off {len(bad_ch)}: {bad_ch[:40]}", flush=True)
-ok = (~bad_out).nonzero().view(-1).tolist()[:1]
-for r in ok:
-    print(f"  good run {r}: max |gap - ref| {(dbg[r, :, :Cc].double() - part).abs().max().item():.2e}")
+        d = dbg[r, b].double().cpu()
+        gap, pool = d[:Cc], d[Cc:Cc + N]
+        v = d[Cc + N:Cc + N + 4 * NT * 4].view(4, NT, 4)
+        e1 = stage_expect(gap, w1d.cpu(), Cc)
+        e2 = stage_expect(pool, w2d.cpu(), N)
+        reg1 = (v[0] - e1).abs().max(1).values
+        lds1 = (v[1] - v[0]).abs().max(1).values
+        reg2 = (v[2] - e2).abs().max(1).values
+        lds2 = (v[3] - v[2]).abs().max(1).values
+        def where(x, tol=1e-4):
+            idx = (x > tol).nonzero().view(-1).tolist()
+            return f"{len(idx)} threads (waves {sorted(set(i // 64 for i in idx))}) {idx[:8]}"
+        print(f"  run {r} image {b}: stage1 reg-vs-expected {where(reg1)}; stage1 lds-view-vs-reg "
+              f"{where(lds1)}; stage2 reg-vs-expected {where(reg2)}; stage2 lds-vs-reg {where(lds2)}",
+              flush=True)
+        bad_t = (reg1 > 1e-4).nonzero().view(-1).tolist()[:2] + (reg2 > 1e-4).nonzero().view(-1).tolist()[:2]
+        for t in bad_t[:2]:
+            print(f"     thread {t}: stage1 got {v[0][t].tolist()} want {e1[t].tolist()}", flush=True)

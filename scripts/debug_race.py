@@ -18,11 +18,14 @@ from semantic_segmentation_server_amd.runtime.sources import SyntheticSource  # 
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 60
 force = [kv.split("=") for kv in sys.argv[2].split(",")] if len(sys.argv) > 2 and sys.argv[2] else []
-eng = Engine(T._small_cfg(graph=True, batch=2, input_size=257, min_area_ratio=0.002), torch.device("cuda"))
-src = SyntheticSource(160, 120, seed=7, pool=4)
-eng.set_camera(160, 120)
+B = int(os.environ.get("RACE_B", "2"))
+S = int(os.environ.get("RACE_S", "257"))
+CW, CH = (int(v) for v in os.environ.get("RACE_CAM", "160x120").split("x"))
+eng = Engine(T._small_cfg(graph=True, batch=B, input_size=S, min_area_ratio=0.002), torch.device("cuda"))
+src = SyntheticSource(CW, CH, seed=7, pool=4)
+eng.set_camera(CW, CH)
 hm = eng._hip_model
-fr = [torch.from_numpy(np.ascontiguousarray(src.read_batch(2)[0])).cuda() for _ in range(3)]
+fr = [torch.from_numpy(np.ascontiguousarray(src.read_batch(B)[0])).cuda() for _ in range(3)]
 for part in range(3):
     hm.segment(fr[0], eng.lut_x, eng.lut_y, part=part)
 
@@ -41,7 +44,7 @@ def pin(ops):
 
 picks = []
 for part in range(3):
-    ops = hm._plan(2, 120, 160, part)[0]
+    ops = hm._plan(B, CH, CW, part)[0]
     pin(ops)
     picks.append({op.name: op.variants[op.pick][0] for op in ops if isinstance(op, Choice)})
 assert picks[0] == picks[1] == picks[2]

@@ -170,13 +170,14 @@ class HipDeepLabInt8:
         if part == 0:
             self._autotune(ops, B, Hc, Wc)
         else:
-            from .hip_model import _copy_picks, _run_variants
+            from .hip_model import _copy_picks
             _copy_picks(self._plan(B, Hc, Wc)[0], ops)
             dev = self.device
             args = (torch.zeros((B, Hc, Wc, 3), dtype=torch.uint8, device=dev),
                     torch.zeros(self.W, dtype=torch.int32, device=dev),
                     torch.zeros(self.H, dtype=torch.int32, device=dev))
-            _run_variants(ops, args)
+            for op in ops:  # first launches outside any capture
+                op(*args)
             torch.cuda.synchronize(dev)
         return self._plans[key]
 

@@ -56,9 +56,10 @@ def init(backend: Optional[str] = None, timeout_s: float = 300.0,
 
     ``device``: "auto" (the local GPU unless ``backend`` is gloo), "cuda" (the local
     GPU whatever the backend: a gloo group driving GPU ranks) or "cpu".
-    ``backend`` (or env SSA_PG_BACKEND): "nccl" (RCCL) or "gloo". The GPU data path
-    only needs RCCL for the frame scatter / device record gather; the default serving
-    and bench path gathers host records over gloo (see DataParallelPipeline)."""
+    ``backend`` (or env SSA_PG_BACKEND): "nccl" (RCCL) or "gloo". With RCCL a gloo
+    ``cpu_group`` is created beside it for host-side control traffic (heartbeat, pick
+    broadcast, metadata); the per-step data (record gather, frame scatter) goes over
+    RCCL (DataParallelPipeline)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -100,8 +101,7 @@ def init(backend: Optional[str] = None, timeout_s: float = 300.0,
         store = dist.TCPStore(os.environ["MASTER_ADDR"], port, world, rank == 0, timeout=timeout,
                               wait_for_workers=False)
     dist.init_process_group(backend, rank=rank, world_size=world, timeout=timeout, **kw)
-    # host-memory collectives (the per-step record gather) go over gloo, so the step
-    # loop never enqueues an RCCL kernel beside the compute graphs
+    # host-memory control collectives (heartbeat, picks, metadata) go over gloo
     cpu_group = dist.new_group(backend="gloo") if backend == "nccl" else None
     return DistContext(rank, world, local, device, backend, cpu_group, list(range(world)), 0, store)
 
@@ -223,12 +223,15 @@ def allreduce_max(ctx: DistContext, v: float, poll_s: float = 0.05) -> float:
     connection drop)."""
     if not ctx.initialized:
         return v
-    t = torch.tensor([v], dtype=torch.float64, device=ctx.device if ctx.backend == "nccl" else "cpu")
-    if ctx.store is None or ctx.backend == "nccl":
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    # host flag over the gloo group (the CPU group beside an RCCL default group): the
+    # heartbeat never puts an RCCL kernel or a device sync into the step loop
+    t = torch.tensor([v], dtype=torch.float64)
+    grp = ctx.cpu_group
+    if ctx.store is None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=grp)
         return float(t.item())
     import time
-    work = dist.all_reduce(t, op=dist.ReduceOp.MAX, async_op=True)
+    work = dist.all_reduce(t, op=dist.ReduceOp.MAX, async_op=True, group=grp)
     t_next = time.perf_counter() + poll_s
     while not work.is_completed():
         now = time.perf_counter()
@@ -254,8 +257,8 @@ def broadcast_obj(ctx: DistContext, obj):
 def allreduce_sum(ctx: DistContext, v: float) -> float:
     if not ctx.initialized:
         return v
-    t = torch.tensor([v], dtype=torch.float64, device=ctx.device if ctx.backend == "nccl" else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    t = torch.tensor([v], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=ctx.cpu_group)
     return float(t.item())
 
 

@@ -82,7 +82,7 @@ def unpack_records(packed: np.ndarray, K: int, frame_ids, ts, streams) -> np.nda
 class DataParallelPipeline:
     def __init__(self, ctx: DistContext, engine, cam_w: int, cam_h: int, batch: int,
                  ingest: str = "local", hub: Optional[ResultHub] = None,
-                 streams_per_rank: int = 1, lag: int = 0, gather: str = "host",
+                 streams_per_rank: int = 1, lag: int = 0, gather: str = "auto",
                  auto_lag: bool = True):
         """``lag=1``: step k returns (and pushes) the records of step k-1, so the host
         never waits for the step it just enqueued -- the next graph launch and the
@@ -91,18 +91,24 @@ class DataParallelPipeline:
         records (synchronous).
 
         ``gather``: how the per-rank records reach rank 0.
-          * ``host`` (default): every rank copies its packed records (B x 1.3 KB) to
-            pinned host memory on the stream that produced them, and the host buffers
-            are gathered over the gloo CPU group when the step is collected. No
-            collective is enqueued on the GPU, so nothing in the step loop can queue
-            an RCCL kernel behind (or in front of) the model and post-processing
-            graphs; with ``lag=1`` the gather overlaps the next step's compute.
-            Measured on one MI355X with a real world-size-1 RCCL group: the RCCL
-            gather path ran 15.9-17.6k frames/s against 22.7k without collectives.
-          * ``rccl``: RCCL gather of the device records to rank 0's GPU, then D2H
-            there (the X2 collective of SURVEY.md §2.5)."""
+          * ``rccl`` (the default with an RCCL group, i.e. every multi-GPU run): RCCL
+            gather of the device records to rank 0's GPU on the stream that produced
+            them, then one D2H there (the X2 collective of SURVEY.md §2.5). The
+            frame metadata (ids, streams, capture times) travels the same way. The
+            communicator is created lazily by the first gather, after the engine's
+            streams exist (eager creation shifted the engine's streams onto a worse
+            hardware-queue mapping: 17.6k vs 21.4k frames/s at world size 1).
+          * ``host``: every rank copies its packed records (B x 1.3 KB) to pinned host
+            memory on the stream that produced them, and the host buffers are
+            gathered over the gloo group when the step is collected (the fallback,
+            and the CPU/gloo test path). At world size 1 the two measured equal
+            within noise (profiles/r2_pg_ab.txt: RCCL group + RCCL gather 24.07k,
+            gloo + host gather 24.42k frames/s).
+          * ``auto``: ``rccl`` when the process group is RCCL, else ``host``."""
+        if gather == "auto":
+            gather = "rccl" if (ctx.backend == "nccl" and engine.device.type == "cuda") else "host"
         if gather not in ("host", "rccl"):
-            raise ValueError("gather must be 'host' or 'rccl'")
+            raise ValueError("gather must be 'auto', 'host' or 'rccl'")
         self.ctx = ctx
         # lag L >= 1: step k collects step k-L's records, with L + 1 staging slots (so L + 1
         # steps can be in flight on a slot-parallel engine); SSA_PIPE_LAG overrides a

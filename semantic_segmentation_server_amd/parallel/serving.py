@@ -7,9 +7,11 @@ Every rank owns ``--streams`` frame sources (global stream id = launch rank * S 
 one engine on its GPU. Each rank's loop is the measured pipeline (``runtime/driver.py``):
 a feeder thread fills a ring of pinned batches, ``DataParallelPipeline`` (lag 1, bound
 per-slot hipGraphs, post-processing on its own stream) runs the step and gathers the
-packed records plus frame metadata to rank 0, which pushes them into the per-stream
-result hub behind the v1/v2 services. With ``--ingest scatter`` rank 0 owns the sources
-for the whole node and scatters frames (RCCL) and their metadata (gloo) instead.
+packed records plus frame metadata to rank 0 over RCCL (``--gather host``: pinned host
+memory over gloo), which pushes them into the per-stream result hub behind the v1/v2
+services. With ``--ingest scatter`` rank 0 owns the sources for the whole node and
+scatters frames (RCCL) and their metadata (gloo) instead. The per-step heartbeat is a
+gloo all-reduce of a host flag.
 
 Failure handling: every step starts with a tiny all-reduce carrying the
 stop flag; a source error is retried by the feeder (the rank keeps stepping). When a
@@ -53,9 +55,11 @@ class DistributedServer:
     def __init__(self, cfg: Config, ctx: Optional[D.DistContext] = None,
                  max_steps: Optional[int] = None):
         self.cfg = cfg
-        # RCCL only for the rank-0 frame scatter; otherwise a gloo group (records are
-        # gathered from pinned host memory; see DataParallelPipeline)
-        pg = "nccl" if cfg.ingest == "scatter" else "gloo"
+        # multi-GPU data path over RCCL (record gather, frame scatter) with a gloo group
+        # beside it for the heartbeat / control traffic; gloo alone on CPU ranks or when
+        # the host gather is asked for
+        gpu = torch.cuda.is_available() and cfg.device != "cpu"
+        pg = "nccl" if gpu and (cfg.ingest == "scatter" or cfg.gather in ("auto", "rccl")) else "gloo"
         self.ctx = ctx or D.init(pg, timeout_s=cfg.rank_timeout,
                                  device="cuda" if torch.cuda.is_available() and cfg.device != "cpu"
                                  else "auto")
@@ -100,7 +104,8 @@ class DistributedServer:
         if self.feeder is not None:
             self.feeder.start()
         pipe = DataParallelPipeline(ctx, self.engine, self.camera_res[0], self.camera_res[1],
-                                    self.cfg.batch, self._ingest, self.hub, self.S, lag=1)
+                                    self.cfg.batch, self._ingest, self.hub, self.S, lag=1,
+                                    gather=self.cfg.gather)
         pipe.tracer = self.tracer
         self.driver = PipelineDriver(pipe, self.feeder, self.tracer, self.metrics)
         self._started = False

