@@ -47,7 +47,7 @@ def main() -> int:
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
     p.add_argument("--backend", choices=["hip", "torch"], default="hip")
-    p.add_argument("--lag", type=int, default=1, choices=[1, 2],
+    p.add_argument("--lag", type=int, default=2, choices=[1, 2],
                    help="pipeline lag (2 = three steps in flight, the serving default)")
     p.add_argument("--arch", default="mnv2")
     p.add_argument("--aspp", default="full")
@@ -110,10 +110,11 @@ def main() -> int:
     # --lag L: step k collects step k-L's records, so the next graph launches and the host
     # unpack overlap the GPU instead of idling it; run_steps flushes the last steps inside
     # the timed region (every timed step's records reach the hub). Lag 2 (three steps in
-    # flight, the serving default) is faster in steady state (100+ steps: 30.9k vs ~28k
-    # frames/s) but short timed windows pay a start-up transient it does not amortise
-    # (--steps 20 --warmup 5: 18-23k vs 27.2-27.7k at lag 1, profiles/r2_lag_window.txt),
-    # so the benchmark default stays 1.
+    # flight on three slot-parallel plan copies, the serving default) is the default. Round
+    # 2 kept lag 1 because short windows lost 20-45 % at lag 2; round 3 found the cause (a
+    # D2H hipMemcpyAsync of the records blocking the host for ~6 ms every ~20 steps,
+    # profiles/r3_lag_stall.txt) and writes the records to pinned memory with a kernel:
+    # --steps 20 --warmup 5 now 29.8-29.9k frames/s at lag 2 vs 27.5-27.7k at lag 1.
     # synthetic camera frames, pinned; distinct per rank (prepared before the pipeline, whose
     # construction ends by priming its streams: the warmup then follows without a GPU-idle gap)
     src = SyntheticSource(cam_w, cam_h, stream=ctx.rank, seed=1, pool=max(2, min(a.batch, 8)))

@@ -306,6 +306,9 @@ PYBIND11_MODULE(_hip, m) {
   });
 
   m.def("post_workspace_bytes", &post_workspace_bytes);
+  m.def("copy_to_host", [](uintptr_t src, uintptr_t dst, long long nbytes, uintptr_t stream) {
+    copy_to_host(P<const void>(src), P<void>(dst), nbytes, S(stream));
+  });
   m.def("poison_lds", [](uint32_t pat, int blocks, uintptr_t stream) {
     poison_lds(pat, blocks, S(stream));
   });

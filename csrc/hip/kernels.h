@@ -273,6 +273,9 @@ struct PostParams {
 };
 size_t post_workspace_bytes(int B, int H, int W, int K, int num_bins);
 
+// device buffer -> pinned (hipHostMalloc) host buffer by a kernel on stream s (no host block)
+void copy_to_host(const void* src, void* dst, long long nbytes, hipStream_t s);
+
 // Debug only (debug_poison.hip): NaN-pattern fill of every CU's LDS / every SIMD's
 // VGPR+AGPR file, to expose kernels that read on-chip state they did not write.
 void poison_lds(uint32_t pat, int blocks, hipStream_t s);

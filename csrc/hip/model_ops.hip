@@ -447,6 +447,36 @@ __global__ void gap_reduce_kernel(const float* __restrict__ part, float* __restr
 
 size_t gap_workspace_floats(int B, int C) { return (size_t)B * kGapSlices * C; }
 
+// ---------------------------------------------------------------- device -> pinned host
+// The per-step packed records (B x 1.3 KB) are written straight into pinned host memory
+// (hipHostMalloc: device-addressable, coherent) by a kernel on the stream that produced
+// them. hipMemcpyAsync D2H here stalled the host thread for up to ~6 ms in the lag-2
+// pipeline (scripts/lag_timeline.py: one copy_ call per ~20 steps blocked until the
+// result stream drained); a kernel launch never blocks the host.
+__global__ __launch_bounds__(256) void copy_to_host_kernel(const uint4* __restrict__ src,
+                                                           uint4* __restrict__ dst, long long n16,
+                                                           const uint32_t* __restrict__ src4,
+                                                           uint32_t* __restrict__ dst4, long long n4) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long k = i; k < n16; k += stride) dst[k] = src[k];
+  for (long long k = i; k < n4; k += stride) dst4[k] = src4[k];
+}
+
+void copy_to_host(const void* src, void* dst, long long nbytes, hipStream_t s) {
+  if (nbytes % 4) throw std::invalid_argument("copy_to_host: nbytes % 4 == 0 required");
+  const bool al = ((uintptr_t)src % 16 == 0) && ((uintptr_t)dst % 16 == 0);
+  const long long n16 = al ? nbytes / 16 : 0;
+  const long long tail = nbytes - n16 * 16;
+  const auto* s4 = reinterpret_cast<const uint32_t*>(static_cast<const char*>(src) + n16 * 16);
+  auto* d4 = reinterpret_cast<uint32_t*>(static_cast<char*>(dst) + n16 * 16);
+  const long long work = n16 > tail / 4 ? n16 : tail / 4;
+  const int grid = (int)std::min<long long>(64, std::max<long long>(1, cdiv(work, 256)));
+  hipLaunchKernelGGL(copy_to_host_kernel, dim3(grid), dim3(256), 0, s, static_cast<const uint4*>(src),
+                     static_cast<uint4*>(dst), n16, s4, d4, tail / 4);
+  check_launch("copy_to_host");
+}
+
 void global_avgpool(const bf16* in, float* out, float* ws, int B, int HW, int C, hipStream_t s) {
   hipLaunchKernelGGL(gap_partial_kernel, dim3(B, kGapSlices, cdiv(C / 8, 64)), dim3(256), 0, s, in,
                      ws, HW, C);

@@ -844,3 +844,19 @@ def poison_chip(lds: bool = True, regs: bool = True, pat: int = 0x7FC07FC0) -> N
         _hip_mod().poison_lds(pat, 256 * 8, _stream())
     if regs:
         _hip_mod().poison_regs(256 * 4 * 8, _stream())
+
+
+def copy_to_host(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
+    """src (contiguous CUDA tensor) -> dst (contiguous PINNED host tensor of the same byte
+    size), by a kernel on the current stream: unlike a D2H hipMemcpyAsync it never blocks
+    the launching thread (profiles/r3_lag_stall.txt). Ordering as for any kernel: the
+    host may read dst once an event recorded after this call has completed."""
+    if not src.is_cuda or dst.is_cuda or not dst.is_pinned():
+        raise ValueError("copy_to_host: CUDA source, pinned host destination")
+    if not (src.is_contiguous() and dst.is_contiguous()):
+        raise ValueError("copy_to_host: contiguous tensors required")
+    nb = src.numel() * src.element_size()
+    if dst.numel() * dst.element_size() != nb:
+        raise ValueError("copy_to_host: byte sizes differ")
+    _hip_mod().copy_to_host(src.data_ptr(), dst.data_ptr(), nb, _stream())
+    return dst

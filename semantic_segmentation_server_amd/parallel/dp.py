@@ -313,7 +313,7 @@ class DataParallelPipeline:
         rs = getattr(self.engine, "result_stream", None) if self.cuda else None
         if self.gather_mode == "host":
             with (torch.cuda.stream(rs) if rs is not None else contextlib.nullcontext()):
-                self.local_rec[slot].copy_(packed, non_blocking=self.cuda)
+                self._d2h(packed, self.local_rec[slot])
                 ev = None
                 if self.cuda:
                     ev = torch.cuda.Event()
@@ -338,14 +338,25 @@ class DataParallelPipeline:
             self.frames_done += B * self.ctx.world
             if not self.ctx.is_root:
                 return np.zeros(0, RECORD_DTYPE)
-            self.host_rec[slot].copy_(src, non_blocking=True)
+            self._d2h(src, self.host_rec[slot])
             if self.ctx.initialized:
-                self.host_meta[slot].copy_(self.meta_buf, non_blocking=True)
+                self._d2h(self.meta_buf, self.host_meta[slot])
             ev = None
             if self.cuda:
                 ev = torch.cuda.Event()
                 ev.record(torch.cuda.current_stream(self.dev))
         return self._enqueue((slot, ev, fids, strm, tss))
+
+    def _d2h(self, src: torch.Tensor, dst: torch.Tensor) -> None:
+        """Device records -> pinned host buffer on the current stream. On the HIP build a
+        kernel writes the pinned memory directly: a D2H hipMemcpyAsync blocked the host
+        thread for up to ~6 ms every ~20 steps at lag 2 (profiles/r3_lag_stall.txt)."""
+        if self.cuda and src.is_cuda and dst.is_pinned() and src.is_contiguous() \
+                and getattr(self.engine, "backend", "hip") == "hip":
+            from ..ops import hip_ops
+            hip_ops.copy_to_host(src, dst)
+        else:
+            dst.copy_(src, non_blocking=self.cuda)
 
     def _enqueue(self, cur) -> np.ndarray:
         """Queue this step's records; collect the step ``lag`` steps back (if any)."""
