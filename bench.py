@@ -153,6 +153,7 @@ def main() -> int:
     warm_s = time.perf_counter() - t_w0
     D.barrier(ctx)
     sync()
+    rec0, fr0 = pipe.records_out, pipe.frames_done
     t0 = time.perf_counter()
     run_steps(a.steps, a.warmup)
     sync()
@@ -163,7 +164,8 @@ def main() -> int:
 
     frames_total = a.steps * a.batch * ctx.world
     fps = frames_total / dt
-    records = pipe.records_out
+    # records that reached the hub from the timed steps (rank 0 collects every rank's)
+    timed_records, timed_frames = pipe.records_out - rec0, pipe.frames_done - fr0
 
     rpc = None
     if a.rpc > 0:
@@ -207,7 +209,9 @@ def main() -> int:
             },
             "p50_get_segmented_objects_ms": rpc.get("p50_ms") if rpc else None,
             "p99_get_segmented_objects_ms": rpc.get("p99_ms") if rpc else None,
-            "records_per_frame": round(records / max(1, pipe.frames_done), 4),
+            "records_per_frame": round(timed_records / max(1, timed_frames), 4),
+            "records_per_frame_under_rpc_load": (round(rpc["records"] / max(1, rpc["frames"]), 4)
+                                                 if rpc and "records" in rpc else None),
             "warmup_s": round(warm_s, 2),
         }
         print(json.dumps(out), flush=True)
@@ -321,6 +325,7 @@ def _rpc_under_load(ctx, pipe, hub, run_steps, n_calls, D):
         proc = mpctx.Process(target=_client_proc, args=(port, n_calls, child), daemon=True)
         proc.start()
     k = 0
+    rec0, fr0 = pipe.records_out, pipe.frames_done
     t_end = time.time() + 120
     while True:
         done = 1.0 if (ctx.is_root and (parent.poll() or time.time() > t_end)) else 0.0
@@ -334,6 +339,7 @@ def _rpc_under_load(ctx, pipe, hub, run_steps, n_calls, D):
         proc.join(10)
         server.stop(0)
         res["load_steps"] = k
+        res["records"], res["frames"] = pipe.records_out - rec0, pipe.frames_done - fr0
     return res
 
 

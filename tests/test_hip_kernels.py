@@ -628,7 +628,29 @@ def test_engine_bound_input_graphs(split):
     assert len(eng._bound_graphs) == 2
 
 
-@pytest.mark.parametrize("lag", [0, 1])
+def test_rccl_world1_pipeline_records_match_eager():
+    """The multi-GPU default data path (RCCL process group + gloo control group, RCCL
+    record gather, lag 2 slot-parallel) rehearsed at world size 1 on this GPU
+    (SSA_FORCE_PG=1): records equal the eager engine's (scripts/rccl_world1_check.py,
+    in a child process so its process group does not leak into other tests)."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SSA_FORCE_PG="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+               WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "rccl_world1_check.py")],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "OK gather=rccl pg=nccl lag=2" in r.stdout, r.stdout
+
+
+@pytest.mark.parametrize("lag", [0, 1, 2])
 def test_dp_pipeline_records_match_eager(lag):
     """The DP pipeline (bound per-slot graphs; lag 1: split model / post graphs on two
     streams, records collected one step late) returns, over many steps of two
