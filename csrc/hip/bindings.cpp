@@ -115,6 +115,24 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("residual"), py::arg("nspan"), py::arg("WR"), py::arg("WCP"), py::arg("hstride"),
         py::arg("npi"), py::arg("xg"), py::arg("xslots"), py::arg("stream"), py::arg("trace") = 0);
   m.def("fused_ir_span_lds", &fused_ir_span_lds);
+  m.def("fused_ir_stream",
+        [](uintptr_t in, uintptr_t w, uintptr_t bp, uintptr_t table, uintptr_t out, int B, int H,
+           int W, int Cin, int hidP, int Cout, int dil, int residual, int nspan, int WR, int WCP,
+           int hstride, int nh_max, uintptr_t stream, uintptr_t trace) {
+          FusedSpanParams p;
+          p.trace = P<long long>(trace);
+          p.in = P<const bf16>(in); p.w = P<const void>(w); p.bp = P<const float>(bp);
+          p.table = P<const int>(table); p.out = P<bf16>(out);
+          p.B = B; p.H = H; p.W = W; p.Cin = Cin; p.hidP = hidP; p.Cout = Cout; p.dil = dil;
+          p.residual = residual; p.S = nspan; p.WR = WR; p.WCP = WCP; p.hstride = hstride;
+          p.nh_max = nh_max;
+          fused_ir_stream(p, S(stream));
+        },
+        py::arg("in"), py::arg("w"), py::arg("bp"), py::arg("table"), py::arg("out"), py::arg("B"),
+        py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("hidP"), py::arg("Cout"), py::arg("dil"),
+        py::arg("residual"), py::arg("nspan"), py::arg("WR"), py::arg("WCP"), py::arg("hstride"),
+        py::arg("nh_max"), py::arg("stream"), py::arg("trace") = 0);
+  m.def("fused_ir_stream_lds", &fused_ir_stream_lds);
   m.def("fused_ir_band",
         [](uintptr_t in, uintptr_t blob, uintptr_t out, int B, int IH, int IW, int Cin, int OH, int OW,
            int Cout, int hidP, int stride, int residual, int R, int nslot, int blob_bytes, int o_be,

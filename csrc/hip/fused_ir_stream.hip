@@ -1,0 +1,435 @@
+// Fused MobileNetV2 inverted residual for the output-stride-16 stage, wave-specialised
+// (blocks 7-15 of DeepLabv3-MobileNetV2 at 513^2: 33x33 maps, stride 1, dilation 1 or 2,
+// hidden 384..960 channels), gfx950.
+//
+//   out = project( relu6( dw3x3_dil( relu6( expand(x) ) ) ) ) [+ x]
+//
+// The expanded tensor never leaves the CU (the reference runs the whole
+// network as one Edge TPU call, /root/reference/sem_seg_server.py:162). Same span
+// decomposition, halo table and chunk images as fused_ir_span.hip (ops/fused_span.py),
+// but a different schedule, built from that kernel's s_memtime timeline
+// (scripts/bench_span.py --trace, profiles/r3_span_trace.txt): there every 32-channel
+// step cost ~3,900 cycles against ~400 cycles of MFMA work, because each of the eight
+// waves ran all three stages back to back (LDS read -> MFMA -> LDS write chains with a
+// full lgkmcnt drain between them), staged weights through VGPRs with a vmcnt(0) drain
+// per step, and the dilation-2 / Cin-160 variants spilled (VGPRs 256 + 35..157 spilled).
+//
+// Here:
+//   * waves 0-3 ("A", one per SIMD) only EXPAND: chunk t of the hidden channels for the
+//     span's halo pixels, X fragments resident in VGPRs (halo group a + 4q, q < 5),
+//     E[t&1] (fp16, relu6) written to LDS octet planes (the span kernel's bank-conflict
+//     free window layout);
+//   * waves 4-7 ("BC", the SIMD partners of 3..0) run depthwise + projection of chunk
+//     t-1: each lane computes the depthwise result for 8 channels of ONE output pixel --
+//     exactly its B fragment of v_mfma_f32_16x16x32_f16 -- so D never touches LDS, and
+//     accumulate [pixels x Cout] in fp32 VGPRs (output groups 3-b, 7-b, 11-b);
+//   * the two roles run separate loops with the same barrier count, so the compiler
+//     keeps X (A) and the accumulators (BC) in the same physical registers;
+//   * chunk images (We fragments | Wp fragments | dw weights/biases, 1 KiB pieces) are
+//     streamed by LDS-DMA (global_load_lds_dwordx4) into a 4-slot ring, two chunks
+//     ahead; every wave waits only for its own pieces of the NEXT chunk (counted vmcnt)
+//     before the step's single s_barrier (no __syncthreads: its fence drains vmcnt).
+// One step = one barrier; the matrix pipe of each SIMD is shared by an expansion wave
+// (MFMA-heavy) and a depthwise+projection wave (VALU/LDS-heavy + MFMA), so one wave's
+// LDS latency hides under the other's MFMAs.
+#include "common.h"
+#include "kernels.h"
+
+namespace ssa {
+
+namespace {
+
+typedef _Float16 f16;
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+constexpr int kNW = 8;     // waves per workgroup
+constexpr int kNT = 64 * kNW;
+constexpr int kHdr = 4;    // span table header: p0, p1, wy0, nh
+constexpr int kXQ = 5;     // halo groups per expansion wave (<= 20 groups = 320 halo px)
+constexpr int kGB = 3;     // output groups per depthwise+projection wave (<= 12 groups)
+constexpr int kNSL = 4;    // chunk-image ring slots (DMA two chunks ahead)
+
+struct StreamArgs {
+  const bf16* in; const char* w; const float* bp; const int* table; bf16* out;
+  int B, H, W, Cin, Cout, NC, S, dil, residual, WCP, WR, hstride;
+  long long* trace;  // debug: s_memtime stamps [block][wave 0 / 4][64], nullptr normally
+};
+
+// Debug timeline (a.trace != nullptr): lane 0 of waves 0 (expansion) and 4 (its SIMD
+// partner's role, depthwise+projection) stamps s_memtime (vector stores to the trace buffer)
+#define STREAM_STAMP(slot)                                                                           \
+  do {                                                                                               \
+    if (a.trace && (wid == 0 || wid == 4) && lane == 0 && (slot) < 64)                               \
+      a.trace[((size_t)blockIdx.x * 2 + (wid >> 2)) * 64 + (slot)] = (long long)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+
+__host__ __device__ inline int stream_plane_bytes(int WR, int WCP) { return (WR * WCP + 15) / 16 * 16 * 16; }
+
+__device__ __forceinline__ void wait_vm(int n) {
+  // n is wave-uniform; a counted wait leaves the newer chunk's DMA pieces in flight
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+__device__ __forceinline__ void step_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS writes landed
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// ---- expansion of one chunk for NQ halo rounds (compile-time: no branches inside)
+template <int KS, int NQ, int NR>
+__device__ __forceinline__ void expand_chunk(const char* Wc, const char* misc, char* Eb, int PLANE,
+                                             const f32x4 (&R)[NR], const int (&hpos)[kXQ],
+                                             int lane, int kq) {
+  const f16x4 z4 = {0, 0, 0, 0}, s4 = {6, 6, 6, 6};
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub) {
+    const f32x4 be4 = *reinterpret_cast<const f32x4*>(misc + 640 + (sub * 16 + kq * 4) * 4);
+    bf16x8 wf[KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) wf[k] = *reinterpret_cast<const bf16x8*>(Wc + (sub * KS + k) * 1024 + lane * 16);
+    f32x4 e[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) e[q] = be4;
+#pragma unroll
+    for (int k = 0; k < KS; ++k)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) e[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[k], __builtin_bit_cast(bf16x8, R[q * KS + k]), e[q], 0, 0, 0);
+    char* ep = Eb + (sub * 2 + (kq >> 1)) * PLANE + (kq & 1) * 8;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      f16x4 o = {(f16)e[q][0], (f16)e[q][1], (f16)e[q][2], (f16)e[q][3]};
+      o = __builtin_elementwise_min(__builtin_elementwise_max(o, z4), s4);
+      *reinterpret_cast<f16x4*>(ep + hpos[q] * 16) = o;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// ---- depthwise + projection of one chunk: output groups g0, g1 over all NS Cout subtiles
+// and g2 over NS3 subtiles starting at n3 (NS3 = NS / 2 for the wide blocks: the ninth
+// group of a span is split over two waves so the accumulators fit 256 VGPRs).
+// Tap offsets are template constants (dilation, window pitch): the 9 taps of a group are
+// one base VGPR + ds_read immediates, not 27 loop-invariant addresses.
+template <int NS, int NS3, int DIL, int WCP, int NR, bool PIPE>
+__device__ __forceinline__ void dwproj_chunk(const char* Wp, const char* misc, const char* Ek,
+                                             const int (&dpos)[kGB], int n3, f32x4 (&R)[NR],
+                                             int lane, int kq) {
+  const f16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0}, s8 = {6, 6, 6, 6, 6, 6, 6, 6};
+  f16x8 wt[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) wt[t] = *reinterpret_cast<const f16x8*>(misc + t * 64 + kq * 16);
+  const f16x8 bd = *reinterpret_cast<const f16x8*>(misc + 576 + kq * 16);
+  auto taps = [&](int g, f16x8 (&v)[9]) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+      v[t] = *reinterpret_cast<const f16x8*>(Ek + dpos[g] * 16 + ((t / 3 - 1) * DIL * WCP + (t % 3 - 1) * DIL) * 16);
+  };
+  auto dw = [&](const f16x8 (&v)[9]) {
+    // three independent row chains, then their sum (shorter dependency chain than 9)
+    f16x8 r0 = v[0] * wt[0] + bd, r1 = v[3] * wt[3], r2 = v[6] * wt[6];
+    r0 = v[1] * wt[1] + r0; r1 = v[4] * wt[4] + r1; r2 = v[7] * wt[7] + r2;
+    r0 = v[2] * wt[2] + r0; r1 = v[5] * wt[5] + r1; r2 = v[8] * wt[8] + r2;
+    const f16x8 sum = r0 + r1 + r2;
+    return __builtin_elementwise_min(__builtin_elementwise_max(sum, z8), s8);
+  };
+  f16x8 dv[kGB];
+  if (PIPE) {
+    // the next group's 9 taps are in flight while this group's depthwise runs (the
+    // timeline of the unpipelined form: ~2,600 cycles per step, LDS latency exposed 3x)
+    f16x8 va[9], vb[9];
+    taps(0, va);
+    __builtin_amdgcn_sched_barrier(0);
+    taps(1, vb);
+    dv[0] = dw(va);
+    __builtin_amdgcn_sched_barrier(0);
+    taps(2, va);
+    dv[1] = dw(vb);
+    __builtin_amdgcn_sched_barrier(0);
+    dv[2] = dw(va);
+  } else {
+#pragma unroll
+    for (int g = 0; g < kGB; ++g) {
+      f16x8 v[9];
+      taps(g, v);
+      dv[g] = dw(v);
+      __builtin_amdgcn_sched_barrier(0);  // one group's 9 taps live at a time (VGPR budget)
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < NS; ++n) {
+    const f16x8 af = *reinterpret_cast<const f16x8*>(Wp + n * 1024 + lane * 16);
+    R[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, dv[0], R[n], 0, 0, 0);
+    R[NS + n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, dv[1], R[NS + n], 0, 0, 0);
+    if (NS3 == NS) R[2 * NS + n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, dv[2], R[2 * NS + n], 0, 0, 0);
+  }
+  if (NS3 != NS) {
+#pragma unroll
+    for (int n = 0; n < NS3; ++n) {
+      const f16x8 af = *reinterpret_cast<const f16x8*>(Wp + (n3 + n) * 1024 + lane * 16);
+      R[2 * NS + n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, dv[2], R[2 * NS + n], 0, 0, 0);
+    }
+  }
+}
+
+template <int KS, int NS, int XQ, int DIL, int WCP>
+__global__ __launch_bounds__(kNT) void fused_ir_stream_kernel(StreamArgs a) {
+  constexpr int NPC = 2 * KS + NS + 1;          // 1 KiB pieces per chunk image
+  constexpr int CHB = NPC * 1024;
+  constexpr int WEB = 2 * KS * 1024, WPB = NS * 1024;
+  constexpr int LAG = kNSL - 2;
+  // every wave issues MP pieces per chunk (the last piece duplicated where NPC % 8 != 0:
+  // identical bytes to the same slot), so the counted waits are compile-time constants
+  constexpr int MP = (NPC + kNW - 1) / kNW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int PLANE = stream_plane_bytes(a.WR, WCP);
+  char* ring = smem;                   // [kNSL][CHB]
+  char* sE = smem + kNSL * CHB;        // [2][4 octet planes][PLANE]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r16 = lane & 15, kq = lane >> 4;
+  const int b = blockIdx.x / a.S, j = blockIdx.x - (blockIdx.x / a.S) * a.S;
+  const int* tb = a.table + (size_t)j * a.hstride;
+  const int p0 = tb[0], p1 = tb[1], wy0 = tb[2], nh = tb[3];
+  const int HW = a.H * a.W, d = DIL, NC = a.NC;
+  const bf16* inb = a.in + (size_t)b * HW * a.Cin;
+
+  auto issue = [&](int c) {
+    const char* src = a.w + (size_t)c * CHB + lane * 16;
+    char* dst = ring + (c % kNSL) * CHB;
+#pragma unroll
+    for (int q = 0; q < MP; ++q) {
+      const int piece = min(wid + q * kNW, NPC - 1);
+      __builtin_amdgcn_global_load_lds(src + piece * 1024, (lds_ptr_t)(dst + piece * 1024), 16, 0, 0);
+    }
+  };
+  // end of step t: chunk t+1 must have landed; chunk t+LAG (issued this step) may fly on
+
+  // ---- prologue: X fragments (A waves), first LAG chunk images, E zeroed (padding taps)
+  const int dummy = a.WR * WCP - 1;  // window slot never read by the depthwise
+  // ONE register array for both roles: the expansion waves keep their X fragments in it,
+  // the depthwise+projection waves their fp32 accumulators (the allocator does not share
+  // two role-private arrays by itself: 190..256 VGPRs + spills against max(A, BC))
+  constexpr int NS3 = NS >= 10 ? NS / 2 : NS;
+  constexpr int NR = XQ * KS > 2 * NS + NS3 ? XQ * KS : 2 * NS + NS3;
+  f32x4 R[NR];
+  int hpos[kXQ];
+  if (wid < 4) {
+    int ent[XQ];
+#pragma unroll
+    for (int q = 0; q < XQ; ++q) ent[q] = tb[kHdr + min((wid + 4 * q) * 16 + r16, nh - 1)];
+#pragma unroll
+    for (int q = 0; q < XQ; ++q) {
+      const bool hv = (wid + 4 * q) * 16 + r16 < nh;
+      hpos[q] = hv ? (ent[q] & 4095) : dummy;
+      const bf16* src = inb + (size_t)(ent[q] >> 12) * a.Cin + kq * 8;
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        const bf16x8 v = ld8(src + k * 32);
+        R[q * KS + k] = __builtin_bit_cast(f32x4, hv ? v : zero8());
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < LAG; ++c)
+    if (c < NC) issue(c);
+  for (int i = tid; i < 8 * PLANE / 16; i += kNT) *reinterpret_cast<i32x4*>(sE + i * 16) = i32x4{0, 0, 0, 0};
+  // chunk 0 (and the X loads, issued earlier) landed; chunk 1 may stay in flight
+  STREAM_STAMP(0);
+  if (LAG < NC) wait_vm(MP * (LAG - 1));
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  step_barrier();
+  STREAM_STAMP(1);
+
+  if (wid < 4) {
+    // ================= expansion waves: step t expands chunk t (XQ rounds, every round
+    // computed: rounds past the span's halo write the dummy slot)
+    // main steps (issue chunk t+LAG, counted wait) and tail steps (no issue, full wait):
+    // two branch-free loop bodies instead of per-step conditions
+    auto a_step = [&](int t) {
+      const char* Wc = ring + (t % kNSL) * CHB;
+      expand_chunk<KS, XQ, NR>(Wc, Wc + WEB + WPB, sE + (t & 1) * 4 * PLANE, PLANE, R, hpos, lane, kq);
+      STREAM_STAMP(2 + 3 * t);
+    };
+    int t = 0;
+    for (; t + LAG < NC; ++t) {
+      issue(t + LAG);
+      a_step(t);
+      wait_vm(MP * (LAG - 1));
+      STREAM_STAMP(3 + 3 * t);
+      step_barrier();
+      STREAM_STAMP(4 + 3 * t);
+    }
+    for (; t < NC; ++t) {
+      a_step(t);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      STREAM_STAMP(3 + 3 * t);
+      step_barrier();
+      STREAM_STAMP(4 + 3 * t);
+    }
+    step_barrier();  // step NC: the depthwise+projection waves finish chunk NC-1
+    step_barrier();  // the output tile is staged in LDS
+  } else {
+    // ================= depthwise + projection waves: step t runs chunk t-1. Wave bw
+    // (= wid - 4, the SIMD partner of expansion wave 3 - bw) owns output groups 3-bw and
+    // 7-bw over all Cout subtiles, and group 8 (the ninth 16-pixel group of a 129..144
+    // pixel span) over subtiles [n3, n3 + NS3): waves bw 0/1 split it for the wide
+    // blocks, waves 2/3 compute a copy that is never stored (branch-free steps).
+    const int bw = wid - 4;
+    const int og[kGB] = {3 - bw, 7 - bw, 8};
+    const int n3 = NS3 == NS ? 0 : (bw & 1) * NS3;
+    const bool own3 = NS3 == NS ? bw == 0 : bw < 2;
+    int dpos[kGB];
+#pragma unroll
+    for (int g = 0; g < kGB; ++g) {
+      const int p = p0 + og[g] * 16 + r16;
+      dpos[g] = d * WCP + d;  // padding lanes: any in-window centre
+      if (p < p1) {
+        const int y = p / a.W, x = p - (p / a.W) * a.W;
+        dpos[g] = (y - wy0) * WCP + x + d;
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NR; ++n) R[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto bc_step = [&](int t) {
+      const int c = t - 1;
+      const char* Wp = ring + (c % kNSL) * CHB + WEB;
+      dwproj_chunk<NS, NS3, DIL, WCP, NR, (NS <= 6 && KS == 2)>(Wp, Wp + WPB, sE + (c & 1) * 4 * PLANE + kq * PLANE, dpos,
+                                                     n3, R, lane, kq);
+      STREAM_STAMP(2 + 3 * c);
+    };
+    // step 0: nothing to compute yet
+    if (LAG < NC) {
+      issue(LAG);
+      wait_vm(MP * (LAG - 1));
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    step_barrier();
+    int t = 1;
+    for (; t + LAG < NC; ++t) {
+      issue(t + LAG);
+      bc_step(t);
+      wait_vm(MP * (LAG - 1));
+      STREAM_STAMP(3 + 3 * (t - 1));
+      step_barrier();
+      STREAM_STAMP(4 + 3 * (t - 1));
+    }
+    for (; t <= NC; ++t) {
+      bc_step(t);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      STREAM_STAMP(3 + 3 * (t - 1));
+      step_barrier();
+      STREAM_STAMP(4 + 3 * (t - 1));
+    }
+    STREAM_STAMP(62);
+    // ---- epilogue, part 1: accumulators -> fp32 output tile [span pixel][Cout] in LDS
+    // (ring and E are free: every DMA was waited for and every read is behind the last
+    // barrier); a row pitch of Cout + 4 floats keeps the 16 pixel rows of a ds_write_b128
+    // lane group on distinct banks
+    float* O = reinterpret_cast<float*>(smem);
+    const int OS = a.Cout + 4;
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int n = 0; n < NS; ++n)
+        *reinterpret_cast<f32x4*>(O + (og[g] * 16 + r16) * OS + n * 16 + kq * 4) = R[g * NS + n];
+    if (own3) {
+#pragma unroll
+      for (int n = 0; n < NS3; ++n)
+        *reinterpret_cast<f32x4*>(O + (og[2] * 16 + r16) * OS + (n3 + n) * 16 + kq * 4) = R[2 * NS + n];
+    }
+    step_barrier();
+  }
+  // ---- epilogue, part 2 (all waves): + bias (+ residual), bf16, fully coalesced 16-byte
+  // stores of the span's contiguous output rows (the per-fragment 8-byte stores took
+  // 5-21k cycles per workgroup: 16 pixels x 32 B segments per store instruction)
+  {
+    const float* O = reinterpret_cast<const float*>(smem);
+    const int OS = a.Cout + 4, C8 = a.Cout / 8;
+    const int units = (p1 - p0) * C8;
+    bf16* outb = a.out + ((size_t)b * HW + p0) * a.Cout;
+    const bf16* resb = inb + (size_t)p0 * a.Cin;
+    for (int u = tid; u < units; u += kNT) {
+      const int px = u / C8, c = (u - px * C8) * 8;
+      const f32x4 o0 = *reinterpret_cast<const f32x4*>(O + px * OS + c);
+      const f32x4 o1 = *reinterpret_cast<const f32x4*>(O + px * OS + c + 4);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bp + c);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(a.bp + c + 4);
+      bf16x8 r = zero8();
+      if (a.residual) r = ld8(resb + (size_t)px * a.Cin + c);
+      bf16x8 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        o[q] = (bf16)(o0[q] + b0[q] + (float)r[q]);
+        o[q + 4] = (bf16)(o1[q] + b1[q] + (float)r[q + 4]);
+      }
+      st8(outb + (size_t)px * a.Cout + c, o);
+    }
+  }
+  STREAM_STAMP(63);
+}
+
+template <int KS, int NS, int XQ, int DIL, int WCP>
+void launch_stream(const StreamArgs& a, hipStream_t st) {
+  const size_t lds = fused_ir_stream_lds(a.Cin, a.Cout, a.WR, a.WCP);
+  if (lds > 160 * 1024) throw std::invalid_argument("fused_ir_stream: LDS over 160 KiB");
+  static bool attr = false;
+  if (!attr) {
+    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_ir_stream_kernel<KS, NS, XQ, DIL, WCP>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
+          "fused_ir_stream attr");
+    attr = true;
+  }
+  hipLaunchKernelGGL((fused_ir_stream_kernel<KS, NS, XQ, DIL, WCP>), dim3(a.B * a.S), dim3(kNT), lds, st, a);
+  check_launch("fused_ir_stream");
+}
+
+}  // namespace
+
+size_t fused_ir_stream_lds(int Cin, int Cout, int WR, int WCP) {
+  const int KS = Cin / 32, NS = (Cout + 15) / 16;
+  const size_t main = (size_t)kNSL * (2 * KS + NS + 1) * 1024 + 8 * (size_t)stream_plane_bytes(WR, WCP);
+  const size_t otile = (size_t)kGB * 4 * 16 * (Cout + 4) * 4;  // epilogue fp32 output tile
+  return main > otile ? main : otile;
+}
+
+void fused_ir_stream(const FusedSpanParams& p, hipStream_t st) {
+  if (p.Cin % 32 || p.Cout % 16 || p.hidP % 32 || p.hidP <= 0)
+    throw std::invalid_argument("fused_ir_stream: Cin % 32, Cout % 16, hidP % 32");
+  if (p.residual && p.Cin != p.Cout) throw std::invalid_argument("fused_ir_stream: residual needs Cin == Cout");
+  if (p.dil < 1 || 2 * p.dil + 1 > 16 || p.WCP != p.W + 16 || p.WR < 2 * p.dil + 1 || p.WR * p.WCP > 4096)
+    throw std::invalid_argument("fused_ir_stream: bad window geometry");
+  if (p.S < 1 || (p.H * p.W + p.S - 1) / p.S > kGB * 4 * 16) throw std::invalid_argument("fused_ir_stream: span too long");
+  if (p.H * p.W >= (1 << 19)) throw std::invalid_argument("fused_ir_stream: map too large for the halo table");
+  if (p.nh_max > kXQ * 4 * 16) throw std::invalid_argument("fused_ir_stream: halo over 320 pixels");
+  StreamArgs a{p.in, reinterpret_cast<const char*>(p.w), p.bp, p.table, p.out, p.B, p.H, p.W, p.Cin,
+               p.Cout, p.hidP / 32, p.S, p.dil, p.residual, p.WCP, p.WR, p.hstride, p.trace};
+  const int KS = p.Cin / 32, NS = p.Cout / 16;
+  // instantiated for the 33-wide maps of the headline (window pitch W + 16 = 49) at
+  // dilation 1 (halo <= 16 groups: 4 rounds per expansion wave) and 2 (<= 20: 5 rounds)
+  if (p.W != 33 || p.dil > 2 || p.nh_max > (p.dil == 1 ? 4 : 5) * 64)
+    throw std::invalid_argument("fused_ir_stream: W 33, dilation 1/2, halo <= 256/320 px");
+#define STREAM(K_, N_)                                   \
+  if (KS == K_ && NS == N_) {                            \
+    if (p.dil == 1) launch_stream<K_, N_, 4, 1, 49>(a, st);  \
+    else launch_stream<K_, N_, 5, 2, 49>(a, st);             \
+    return;                                              \
+  }
+  // blocks 7-9 (64->64), 10 (64->96), 11-12 (96->96), 13 (96->160), 14-15 (160->160)
+  STREAM(2, 4) STREAM(2, 6) STREAM(3, 6) STREAM(3, 10) STREAM(5, 10)
+#undef STREAM
+  throw std::invalid_argument("fused_ir_stream: no instantiation for this (Cin, Cout)");
+}
+
+}  // namespace ssa

@@ -134,9 +134,14 @@ struct FusedSpanParams {
   int npi = 4, xg = 2;        // pixel-group wave sets; halo groups per wave (instantiation)
   int xslots = 0;             // halo groups beyond 16 (their X lives in LDS; xg == 3 only)
   long long* trace = nullptr; // debug s_memtime timeline [B*S][2][64]
+  int nh_max = 0;             // largest halo of the table (fused_ir_stream: <= 320)
 };
 void fused_ir_span(const FusedSpanParams& p, hipStream_t s);
 size_t fused_ir_span_lds(int Cin, int Cout, int WR, int WCP, int xslots);
+// Wave-specialised variant over the same spans / chunk images (fused_ir_stream.hip):
+// expansion waves 0-3, depthwise+projection waves 4-7, LDS-DMA chunk ring.
+void fused_ir_stream(const FusedSpanParams& p, hipStream_t s);
+size_t fused_ir_stream_lds(int Cin, int Cout, int WR, int WCP);
 // Row-streaming fused inverted residual (fused_ir_band.hip): blocks with Cin <= 32,
 // stride 1/2, dilation 1. blob: host-packed weights (hip_ops.pack_fused_band) with the
 // section offsets below; R output rows per band, nslot E row buffers (1 or 2).

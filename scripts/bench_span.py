@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--trace", action="store_true")
     ap.add_argument("--only", type=int, default=0, help="run only this block index")
     ap.add_argument("--S", type=int, default=0, help="run only this span count")
+    ap.add_argument("--stream", action="store_true", help="time fused_ir_stream (wave-specialised)")
     a = ap.parse_args()
     dev = "cuda"
     B, H = a.B, a.H
@@ -44,8 +45,14 @@ def main():
                 tab = FS.span_table(H, H, S, dil, dev)
             except ValueError:
                 continue
-            for npi in FS.span_npi_options(cout):
-                run = lambda: FS.fused_ir_span(x, packed, tab, out, B=B, residual=spec.residual, npi=npi)
+            opts = [None] if a.stream else FS.span_npi_options(cout)
+            if a.stream and not FS.stream_supported(cin, cout, 1, H, H, S, dil):
+                continue
+            for npi in opts:
+                if a.stream:
+                    run = lambda: FS.fused_ir_stream(x, packed, tab, out, B=B, residual=spec.residual)
+                else:
+                    run = lambda: FS.fused_ir_span(x, packed, tab, out, B=B, residual=spec.residual, npi=npi)
                 for _ in range(3):
                     run()
                 st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -55,10 +62,29 @@ def main():
                 en.record()
                 en.synchronize()
                 us = st.elapsed_time(en) / a.reps * 1e3
-                print(f"block{idx:2d} {cin:3d}->{spec.hidden:3d}->{cout:3d} d{dil} S={S:2d} npi={npi}: "
+                print(f"block{idx:2d} {cin:3d}->{spec.hidden:3d}->{cout:3d} d{dil} S={S:2d} "
+                      f"{'stream' if a.stream else f'npi={npi}'}: "
                       f"{us:7.1f} us  {flop / us / 1e6:7.1f} TFLOP/s  (xg={tab['xg']}, nh_max={tab['nh_max']})",
                       flush=True)
-                if a.trace:
+                if a.trace and a.stream:
+                    tr = torch.zeros(B * S * 2 * 64, dtype=torch.int64, device=dev)
+                    FS.fused_ir_stream(x, packed, tab, out, B=B, residual=spec.residual, trace=tr)
+                    torch.cuda.synchronize()
+                    t = tr.view(B * S, 2, 64).cpu().numpy().astype(np.int64)
+                    NC = packed["hidP"] // 32
+                    steps = min(NC, 19)
+                    for w, role in ((0, "expand"), (1, "dw+proj")):
+                        tt = t[:, w]
+                        # per step: compute, wait (vmcnt), barrier  (stamps 1 + 3c .. 4 + 3c)
+                        ph = np.array([[np.median(tt[:, 2 + 3 * k + i] - tt[:, 1 + 3 * k + i]) for i in range(3)]
+                                       for k in range(1, steps - 1)])
+                        end = 63 if w == 1 else 1 + 3 * steps
+                        print(f"   {role:8s}: prologue {np.median(tt[:, 1] - tt[:, 0]):.0f} cyc; steady step "
+                              f"[compute, wait, barrier] = {np.median(ph, axis=0).round(0).tolist()}; "
+                              f"step-0 {np.median(tt[:, 4] - tt[:, 1]):.0f}"
+                              + (f"; epilogue {np.median(tt[:, 63] - tt[:, 62]):.0f}" if w == 1 else ""),
+                              flush=True)
+                if a.trace and not a.stream:
                     tr = torch.zeros(B * S * 2 * 64, dtype=torch.int64, device=dev)
                     FS.fused_ir_span(x, packed, tab, out, B=B, residual=spec.residual, npi=npi, trace=tr)
                     torch.cuda.synchronize()

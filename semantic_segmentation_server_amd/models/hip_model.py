@@ -484,14 +484,22 @@ class HipDeepLab:
             with open(path) as f:
                 saved = json.load(f).get(key, {})
         rank0 = int(os.environ.get("RANK", "0")) == 0
+        # SSA_RETUNE_ONLY=block7,block8,...: re-time just these choices (exact names) on top
+        # of the saved picks (a new kernel variant for a few plan steps)
+        only = {n for n in os.environ.get("SSA_RETUNE_ONLY", "").split(",") if n}
+        retimed = False
         if saved:
             for op in every:
                 want = saved.get(op.name)
                 hit = next((i for i, (n, _) in enumerate(op.variants) if n == want), None)
-                if hit is not None:
+                if op.name in only and op in choices and len(op.variants) > 1:
+                    op.autotune(args)
+                    retimed = True
+                elif hit is not None:
                     op.pick = hit
                 elif op in choices and len(op.variants) > 1:
                     op.autotune(args)  # a variant set the saved plan does not know: time it
+                    retimed = True
         else:
             if self.pick_sync is None or rank0:
                 for op in choices:
@@ -502,7 +510,7 @@ class HipDeepLab:
                     op.pick = picks.get(op.name, op.pick)
         torch.cuda.synchronize(dev)
         self.choices = {op.name: op.variants[op.pick][0] for op in every}
-        if env_path and not saved and rank0:
+        if env_path and (not saved or retimed) and rank0:
             import json
             allp = {}
             if os.path.exists(env_path):
@@ -618,6 +626,11 @@ class HipDeepLab:
                     variants.insert(0, (f"span{S}n{npi}", [
                         lambda *_, x=inp, out=out, tab=tab, npi=npi, sp=blk["span"]: FS.fused_ir_span(
                             x, sp, tab, out, B=B, residual=s.residual, npi=npi)]))
+                if FS.stream_supported(s.cin, s.cout, 1, h, w, S, s.dilation):
+                    # wave-specialised: expansion waves | depthwise+projection waves
+                    variants.insert(0, (f"stream{S}", [
+                        lambda *_, x=inp, out=out, tab=tab, sp=blk["span"]: FS.fused_ir_stream(
+                            x, sp, tab, out, B=B, residual=s.residual)]))
         if blk["expand"] is not None and FB.band_supported(s.cin, hid, s.cout, s.stride, s.dilation, OW):
             # row-streaming bands: every input row expanded once into an on-chip fp16 row
             if "band" not in blk:

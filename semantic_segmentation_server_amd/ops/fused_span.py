@@ -146,6 +146,50 @@ def fused_ir_span(x: torch.Tensor, packed: Dict, table: Dict, out: torch.Tensor,
     return out
 
 
+def fused_ir_stream(x: torch.Tensor, packed: Dict, table: Dict, out: torch.Tensor, *, B: int,
+                    residual: bool, trace: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Launch fused_ir_stream_kernel (csrc/hip/fused_ir_stream.hip): the same spans and
+    chunk images as fused_ir_span, run by wave-specialised expansion / depthwise+projection
+    waves over an LDS-DMA chunk ring. x [B, H, W, Cin] bf16, out [B, H, W, Cout] bf16."""
+    from .hip_ops import _chk, _dbg, _hip_mod, _ptr, _stream
+    H, W = table["H"], table["W"]
+    Cin, Cout = packed["Cin"], packed["Cout"]
+    if residual and Cin != Cout:
+        raise ValueError("fused_ir_stream: residual needs Cin == Cout")
+    _chk(x, torch.bfloat16, "x", B * H * W * Cin)
+    _chk(out, torch.bfloat16, "out", B * H * W * Cout)
+    _chk(packed["w"], torch.uint8, "w", (packed["hidP"] // 32) * chunk_bytes(Cin, Cout))
+    _chk(packed["bp"], torch.float32, "bp", Cout)
+    _chk(table["table"], torch.int32, "table", table["S"] * table["hstride"])
+    if trace is not None:
+        _chk(trace, torch.int64, "trace", B * table["S"] * 2 * 64)
+    _hip_mod().fused_ir_stream(_ptr(x), _ptr(packed["w"]), _ptr(packed["bp"]), _ptr(table["table"]),
+                               _ptr(out), B, H, W, Cin, packed["hidP"], Cout, table["dil"],
+                               int(bool(residual)), table["S"], table["WR"], table["WCP"],
+                               table["hstride"], table["nh_max"], _stream(),
+                               0 if trace is None else _ptr(trace))
+    _dbg("fused_ir_stream")
+    return out
+
+
+STREAM_SHAPES = ((64, 64), (64, 96), (96, 96), (96, 160), (160, 160))
+
+
+def stream_supported(Cin: int, Cout: int, stride: int, H: int, W: int, S: int, dil: int) -> bool:
+    """fused_ir_stream instantiations: the 33-wide maps of the headline, dilation 1 (halo
+    <= 256 px) or 2 (<= 320 px), spans <= 144 px, LDS within 160 KiB."""
+    if stride != 1 or (Cin, Cout) not in STREAM_SHAPES or W != 33 or dil not in (1, 2):
+        return False
+    try:
+        t = span_table(H, W, S, dil)
+    except ValueError:
+        return False
+    if t["nh_max"] > (4 if dil == 1 else 5) * 64:
+        return False
+    from .hip_ops import _hip_mod
+    return int(_hip_mod().fused_ir_stream_lds(Cin, Cout, t["WR"], t["WCP"])) <= 160 * 1024
+
+
 def span_npi_options(Cout: int):
     """Wave splits (pixel-group sets NPI x Cout slices 8/NPI) instantiated per Cout."""
     return {64: (2, 4), 96: (4, 8), 160: (4, 8), 320: (2,)}.get(Cout, ())

@@ -1178,6 +1178,47 @@ def test_fused_ir_span(cin, cout, dil, H, S):
         assert _rel(out.cpu().float(), torch.from_numpy(emu)) < 5e-3, npi
 
 
+@pytest.mark.parametrize("cin,cout,dil,H,S", [
+    (64, 64, 1, 33, 8),     # blocks 7-9 (residual)
+    (64, 96, 1, 33, 8),     # block 10
+    (96, 96, 1, 33, 8),     # blocks 11-12 (residual)
+    (96, 160, 1, 33, 8),    # block 13
+    (160, 160, 2, 33, 8),   # blocks 14-15 (dilation 2, residual)
+    (160, 160, 2, 33, 16),  # 16 spans per image
+    (64, 64, 1, 33, 32),    # batch-1 span counts
+    (96, 96, 1, 29, 7),     # odd map height / span sizes
+])
+def test_fused_ir_stream(cin, cout, dil, H, S):
+    """Wave-specialised fused IR kernel vs the fp32 torch block and vs the numpy
+    re-execution of the span kernel's data flow from the same packed chunk images."""
+    from semantic_segmentation_server_amd.ops import fused_span as FS
+    from test_fused_span_cpu import _block, pack_block  # tests/ is on sys.path (prepend mode)
+    W = 33
+    if not FS.stream_supported(cin, cout, 1, H, W, S, dil):
+        pytest.fail("shape expected to be supported")
+    blk, spec = _block(cin, cout, dil, seed=cin * 5 + cout + dil)
+    g = torch.Generator().manual_seed(23)
+    B = 3
+    x = torch.randn(B, cin, H, W, generator=g).to(torch.bfloat16)
+    with torch.no_grad():
+        ref = blk(x.float())
+    packed = pack_block(blk, spec, device=DEV)
+    table = FS.span_table(H, W, S, dil, DEV)
+    xd = _nhwc(x).to(DEV)
+    emu = FS.emulate_fused_span(_nhwc(x).float().numpy(), packed, table, residual=spec.residual)
+    out = torch.full((B, H, W, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
+    FS.fused_ir_stream(xd, packed, table, out, B=B, residual=spec.residual)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    assert _rel(_nchw(out).cpu(), ref) < 2e-2
+    assert _rel(out.cpu().float(), torch.from_numpy(emu)) < 5e-3
+    # bit-exact rerun (no read of bytes another run or wave left behind)
+    out2 = torch.full_like(out, float("nan"))
+    FS.fused_ir_stream(xd, packed, table, out2, B=B, residual=spec.residual)
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int16), out2.view(torch.int16))
+
+
 @pytest.mark.parametrize("M,HW,ncls,ldo,img", [
     (32 * 33 * 33, 33 * 33, 21, 24, True),   # the B = 32 headline head (G = 9)
     (33 * 33, 33 * 33, 21, 24, True),        # batch 1 (G = 1)
