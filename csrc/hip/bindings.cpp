@@ -118,9 +118,10 @@ PYBIND11_MODULE(_hip, m) {
   m.def("fused_ir_stream",
         [](uintptr_t in, uintptr_t w, uintptr_t bp, uintptr_t table, uintptr_t out, int B, int H,
            int W, int Cin, int hidP, int Cout, int dil, int residual, int nspan, int WR, int WCP,
-           int hstride, int nh_max, uintptr_t stream, uintptr_t trace) {
+           int hstride, int nh_max, uintptr_t stream, uintptr_t trace, int variant) {
           FusedSpanParams p;
           p.trace = P<long long>(trace);
+          p.npi = variant == 1 ? 1 : 0;  // 1: group 8 on the expansion waves (G8A)
           p.in = P<const bf16>(in); p.w = P<const void>(w); p.bp = P<const float>(bp);
           p.table = P<const int>(table); p.out = P<bf16>(out);
           p.B = B; p.H = H; p.W = W; p.Cin = Cin; p.hidP = hidP; p.Cout = Cout; p.dil = dil;
@@ -131,7 +132,7 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("in"), py::arg("w"), py::arg("bp"), py::arg("table"), py::arg("out"), py::arg("B"),
         py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("hidP"), py::arg("Cout"), py::arg("dil"),
         py::arg("residual"), py::arg("nspan"), py::arg("WR"), py::arg("WCP"), py::arg("hstride"),
-        py::arg("nh_max"), py::arg("stream"), py::arg("trace") = 0);
+        py::arg("nh_max"), py::arg("stream"), py::arg("trace") = 0, py::arg("variant") = 0);
   m.def("fused_ir_stream_lds", &fused_ir_stream_lds);
   m.def("fused_ir_band",
         [](uintptr_t in, uintptr_t blob, uintptr_t out, int B, int IH, int IW, int Cin, int OH, int OW,

@@ -49,7 +49,11 @@ constexpr int kNT = 64 * kNW;
 constexpr int kHdr = 4;    // span table header: p0, p1, wy0, nh
 constexpr int kXQ = 5;     // halo groups per expansion wave (<= 20 groups = 320 halo px)
 constexpr int kGB = 3;     // output groups per depthwise+projection wave (<= 12 groups)
-constexpr int kNSL = 4;    // chunk-image ring slots (DMA two chunks ahead)
+// chunk-image ring slots: 4 (DMA two chunks ahead) or, for Cout 320 (31 KiB chunk images), 3
+__host__ __device__ constexpr int stream_nsl(int NS) { return NS > 10 ? 3 : 4; }
+// epilogue passes over Cout (the fp32 output tile of a 144-pixel span at Cout 320 would
+// need 186 KiB of LDS)
+__host__ __device__ constexpr int stream_npass(int NS) { return NS > 10 ? 2 : 1; }
 
 struct StreamArgs {
   const bf16* in; const char* w; const float* bp; const int* table; bf16* out;
@@ -181,11 +185,64 @@ __device__ __forceinline__ void dwproj_chunk(const char* Wp, const char* misc, c
   }
 }
 
-template <int KS, int NS, int XQ, int DIL, int WCP>
+// ---- generic form: NG output groups (taps at dpos[g]) x NN Cout subtiles starting at n0
+// (indices past nlast clamp to it: duplicated work that is never stored), accumulating
+// into R[r0 + g * NN + j]. Used with group 8 moved to the expansion waves (G8A): those run
+// one group x ceil(NS/4) subtiles each, the projection waves two groups x NS.
+template <int NG, int NN, int DIL, int WCP, int NR, bool PIPE = true>
+__device__ __forceinline__ void dwproj_groups(const char* Wp, const char* misc, const char* Ek,
+                                              const int (&dpos)[NG], int n0, int nlast, f32x4 (&R)[NR],
+                                              int r0, int lane, int kq) {
+  const f16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0}, s8 = {6, 6, 6, 6, 6, 6, 6, 6};
+  f16x8 wt[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) wt[t] = *reinterpret_cast<const f16x8*>(misc + t * 64 + kq * 16);
+  const f16x8 bd = *reinterpret_cast<const f16x8*>(misc + 576 + kq * 16);
+  auto taps = [&](int g, f16x8 (&v)[9]) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+      v[t] = *reinterpret_cast<const f16x8*>(Ek + dpos[g] * 16 + ((t / 3 - 1) * DIL * WCP + (t % 3 - 1) * DIL) * 16);
+  };
+  auto dw = [&](const f16x8 (&v)[9]) {
+    f16x8 r0_ = v[0] * wt[0] + bd, r1 = v[3] * wt[3], r2 = v[6] * wt[6];
+    r0_ = v[1] * wt[1] + r0_; r1 = v[4] * wt[4] + r1; r2 = v[7] * wt[7] + r2;
+    r0_ = v[2] * wt[2] + r0_; r1 = v[5] * wt[5] + r1; r2 = v[8] * wt[8] + r2;
+    const f16x8 sum = r0_ + r1 + r2;
+    return __builtin_elementwise_min(__builtin_elementwise_max(sum, z8), s8);
+  };
+  f16x8 dv[NG];
+  if (NG == 2 && PIPE) {  // the second group's taps in flight while the first one's depthwise runs
+    f16x8 va[9], vb[9];
+    taps(0, va);
+    __builtin_amdgcn_sched_barrier(0);
+    taps(NG - 1, vb);
+    dv[0] = dw(va);
+    dv[NG - 1] = dw(vb);
+  } else {
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      f16x8 v[9];
+      taps(g, v);
+      dv[g] = dw(v);
+      if (NG > 1) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NN; ++j) {
+    const int n = min(n0 + j, nlast);
+    const f16x8 af = *reinterpret_cast<const f16x8*>(Wp + n * 1024 + lane * 16);
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+      R[r0 + g * NN + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, dv[g], R[r0 + g * NN + j], 0, 0, 0);
+  }
+}
+
+template <int KS, int NS, int XQ, int DIL, int WCP, bool G8A>
 __global__ __launch_bounds__(kNT) void fused_ir_stream_kernel(StreamArgs a) {
   constexpr int NPC = 2 * KS + NS + 1;          // 1 KiB pieces per chunk image
   constexpr int CHB = NPC * 1024;
   constexpr int WEB = 2 * KS * 1024, WPB = NS * 1024;
+  constexpr int kNSL = stream_nsl(NS);
   constexpr int LAG = kNSL - 2;
   // every wave issues MP pieces per chunk (the last piece duplicated where NPC % 8 != 0:
   // identical bytes to the same slot), so the counted waits are compile-time constants
@@ -221,7 +278,9 @@ __global__ __launch_bounds__(kNT) void fused_ir_stream_kernel(StreamArgs a) {
   // the depthwise+projection waves their fp32 accumulators (the allocator does not share
   // two role-private arrays by itself: 190..256 VGPRs + spills against max(A, BC))
   constexpr int NS3 = NS >= 10 ? NS / 2 : NS;
-  constexpr int NR = XQ * KS > 2 * NS + NS3 ? XQ * KS : 2 * NS + NS3;
+  constexpr int Q8 = (NS + 3) / 4;  // G8A: group-8 subtiles per expansion wave
+  constexpr int NRA = XQ * KS + (G8A ? Q8 : 0), NRB = G8A ? 2 * NS : 2 * NS + NS3;
+  constexpr int NR = NRA > NRB ? NRA : NRB;
   f32x4 R[NR];
   int hpos[kXQ];
   if (wid < 4) {
@@ -251,121 +310,117 @@ __global__ __launch_bounds__(kNT) void fused_ir_stream_kernel(StreamArgs a) {
   step_barrier();
   STREAM_STAMP(1);
 
-  if (wid < 4) {
-    // ================= expansion waves: step t expands chunk t (XQ rounds, every round
-    // computed: rounds past the span's halo write the dummy slot)
-    // main steps (issue chunk t+LAG, counted wait) and tail steps (no issue, full wait):
-    // two branch-free loop bodies instead of per-step conditions
-    auto a_step = [&](int t) {
-      const char* Wc = ring + (t % kNSL) * CHB;
-      expand_chunk<KS, XQ, NR>(Wc, Wc + WEB + WPB, sE + (t & 1) * 4 * PLANE, PLANE, R, hpos, lane, kq);
-      STREAM_STAMP(2 + 3 * t);
-    };
-    int t = 0;
-    for (; t + LAG < NC; ++t) {
-      issue(t + LAG);
-      a_step(t);
-      wait_vm(MP * (LAG - 1));
-      STREAM_STAMP(3 + 3 * t);
-      step_barrier();
-      STREAM_STAMP(4 + 3 * t);
-    }
-    for (; t < NC; ++t) {
-      a_step(t);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      STREAM_STAMP(3 + 3 * t);
-      step_barrier();
-      STREAM_STAMP(4 + 3 * t);
-    }
-    step_barrier();  // step NC: the depthwise+projection waves finish chunk NC-1
-    step_barrier();  // the output tile is staged in LDS
-  } else {
-    // ================= depthwise + projection waves: step t runs chunk t-1. Wave bw
-    // (= wid - 4, the SIMD partner of expansion wave 3 - bw) owns output groups 3-bw and
-    // 7-bw over all Cout subtiles, and group 8 (the ninth 16-pixel group of a 129..144
-    // pixel span) over subtiles [n3, n3 + NS3): waves bw 0/1 split it for the wide
-    // blocks, waves 2/3 compute a copy that is never stored (branch-free steps).
-    const int bw = wid - 4;
-    const int og[kGB] = {3 - bw, 7 - bw, 8};
-    const int n3 = NS3 == NS ? 0 : (bw & 1) * NS3;
-    const bool own3 = NS3 == NS ? bw == 0 : bw < 2;
-    int dpos[kGB];
+  // ONE loop for both roles, R carried around it: the loop-header phi is what makes the
+  // register allocator keep the expansion waves' X fragments and the projection waves'
+  // accumulators in the same VGPRs (two role-private loops got the sum of both roles'
+  // registers, 190..256 VGPRs + spills, instead of the max).
+  // Step t: expansion waves expand chunk t (t < NC); depthwise+projection waves run chunk
+  // t-1 (t >= 1). Wave bw = wid - 4 of the latter (the SIMD partner of expansion wave
+  // 3 - bw) owns output groups 3-bw and 7-bw over all Cout subtiles, and group 8 (the ninth
+  // 16-pixel group of a 129..144 pixel span) over subtiles [n3, n3 + NS3): waves bw 0/1
+  // split it for the wide blocks, waves 2/3 compute a copy that is never stored.
+  const bool expander = wid < 4;
+  const int bw = wid - 4;
+  const int og[kGB] = {3 - bw, 7 - bw, 8};
+  const int n3 = NS3 == NS ? 0 : (bw & 1) * NS3;
+  const bool own3 = NS3 == NS ? bw == 0 : bw < 2;
+  int dpos[kGB];
 #pragma unroll
-    for (int g = 0; g < kGB; ++g) {
-      const int p = p0 + og[g] * 16 + r16;
-      dpos[g] = d * WCP + d;  // padding lanes: any in-window centre
-      if (p < p1) {
-        const int y = p / a.W, x = p - (p / a.W) * a.W;
-        dpos[g] = (y - wy0) * WCP + x + d;
-      }
+  for (int g = 0; g < kGB; ++g) {
+    const int p = p0 + (expander ? 8 : og[g]) * 16 + r16;  // G8A: expansion waves own group 8
+    dpos[g] = d * WCP + d;  // padding lanes: any in-window centre
+    if (p < p1) {
+      const int y = p / a.W, x = p - (p / a.W) * a.W;
+      dpos[g] = (y - wy0) * WCP + x + d;
     }
+  }
+  const int dpos8[1] = {dpos[0]};
+  const int dpos01[2] = {dpos[0], dpos[1]};
+  if (!expander) {
 #pragma unroll
     for (int n = 0; n < NR; ++n) R[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto bc_step = [&](int t) {
+  } else if (G8A) {
+#pragma unroll
+    for (int j = 0; j < Q8; ++j) R[XQ * KS + j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int t = 0; t <= NC; ++t) {
+    const bool more = t + LAG < NC;
+    if (more) issue(t + LAG);
+    if (expander) {
+      if (t < NC) {
+        const char* Wc = ring + (t % kNSL) * CHB;
+        expand_chunk<KS, XQ, NR>(Wc, Wc + WEB + WPB, sE + (t & 1) * 4 * PLANE, PLANE, R, hpos, lane, kq);
+      }
+      if (G8A && t >= 1) {
+        const int c = t - 1;
+        const char* Wp = ring + (c % kNSL) * CHB + WEB;
+        dwproj_groups<1, Q8, DIL, WCP, NR>(Wp, Wp + WPB, sE + (c & 1) * 4 * PLANE + kq * PLANE, dpos8,
+                                           wid * Q8, NS - 1, R, XQ * KS, lane, kq);
+      }
+    } else if (t >= 1) {
       const int c = t - 1;
       const char* Wp = ring + (c % kNSL) * CHB + WEB;
-      dwproj_chunk<NS, NS3, DIL, WCP, NR, (NS <= 6 && KS == 2)>(Wp, Wp + WPB, sE + (c & 1) * 4 * PLANE + kq * PLANE, dpos,
-                                                     n3, R, lane, kq);
-      STREAM_STAMP(2 + 3 * c);
-    };
-    // step 0: nothing to compute yet
-    if (LAG < NC) {
-      issue(LAG);
-      wait_vm(MP * (LAG - 1));
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (G8A)
+        dwproj_groups<2, NS, DIL, WCP, NR, (NS <= 10)>(Wp, Wp + WPB, sE + (c & 1) * 4 * PLANE + kq * PLANE, dpos01, 0,
+                                           NS - 1, R, 0, lane, kq);
+      else
+        dwproj_chunk<NS, NS3, DIL, WCP, NR, true>(Wp, Wp + WPB, sE + (c & 1) * 4 * PLANE + kq * PLANE,
+                                                  dpos, n3, R, lane, kq);
     }
+    STREAM_STAMP(2 + 3 * t);
+    // end of step t: chunk t+1 landed; chunk t+LAG (issued this step) may fly on
+    if (more) wait_vm(MP * (LAG - 1));
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    STREAM_STAMP(3 + 3 * t);
     step_barrier();
-    int t = 1;
-    for (; t + LAG < NC; ++t) {
-      issue(t + LAG);
-      bc_step(t);
-      wait_vm(MP * (LAG - 1));
-      STREAM_STAMP(3 + 3 * (t - 1));
-      step_barrier();
-      STREAM_STAMP(4 + 3 * (t - 1));
-    }
-    for (; t <= NC; ++t) {
-      bc_step(t);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      STREAM_STAMP(3 + 3 * (t - 1));
-      step_barrier();
-      STREAM_STAMP(4 + 3 * (t - 1));
-    }
-    STREAM_STAMP(62);
-    // ---- epilogue, part 1: accumulators -> fp32 output tile [span pixel][Cout] in LDS
-    // (ring and E are free: every DMA was waited for and every read is behind the last
-    // barrier); a row pitch of Cout + 4 floats keeps the 16 pixel rows of a ds_write_b128
-    // lane group on distinct banks
-    float* O = reinterpret_cast<float*>(smem);
-    const int OS = a.Cout + 4;
-#pragma unroll
-    for (int g = 0; g < 2; ++g)
-#pragma unroll
-      for (int n = 0; n < NS; ++n)
-        *reinterpret_cast<f32x4*>(O + (og[g] * 16 + r16) * OS + n * 16 + kq * 4) = R[g * NS + n];
-    if (own3) {
-#pragma unroll
-      for (int n = 0; n < NS3; ++n)
-        *reinterpret_cast<f32x4*>(O + (og[2] * 16 + r16) * OS + (n3 + n) * 16 + kq * 4) = R[2 * NS + n];
-    }
-    step_barrier();
+    STREAM_STAMP(4 + 3 * t);
   }
-  // ---- epilogue, part 2 (all waves): + bias (+ residual), bf16, fully coalesced 16-byte
-  // stores of the span's contiguous output rows (the per-fragment 8-byte stores took
-  // 5-21k cycles per workgroup: 16 pixels x 32 B segments per store instruction)
-  {
-    const float* O = reinterpret_cast<const float*>(smem);
-    const int OS = a.Cout + 4, C8 = a.Cout / 8;
+  // ---- epilogue, per pass over a Cout slice [h * NSP, (h + 1) * NSP) subtiles:
+  // part 1, accumulators -> fp32 output tile [span pixel][slice] in LDS (ring and E are
+  // free: every DMA was waited for and every read is behind the last barrier); a row pitch
+  // of slice + 4 floats keeps the 16 pixel rows of a ds_write_b128 lane group on distinct
+  // banks. Part 2 (all waves): + bias (+ residual), bf16, fully coalesced 16-byte stores of
+  // the span's contiguous output rows (the per-fragment 8-byte stores of the first version
+  // took 5-21k cycles per workgroup: 16 pixels x 32 B segments per store instruction).
+  STREAM_STAMP(62);
+  constexpr int NPASS = stream_npass(NS), NSP = NS / NPASS;
+  float* O = reinterpret_cast<float*>(smem);
+  const int OS = NSP * 16 + 4;
+#pragma unroll
+  for (int h = 0; h < NPASS; ++h) {
+    if (h > 0) step_barrier();  // the previous pass's tile has been copied out
+    if (!expander) {
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int n = 0; n < NS; ++n)
+          if (n / NSP == h)
+            *reinterpret_cast<f32x4*>(O + (og[g] * 16 + r16) * OS + (n - h * NSP) * 16 + kq * 4) = R[g * NS + n];
+      if (own3 && !G8A) {
+#pragma unroll
+        for (int n = 0; n < NS3; ++n)
+          if ((n3 + n) / NSP == h)
+            *reinterpret_cast<f32x4*>(O + (og[2] * 16 + r16) * OS + (n3 + n - h * NSP) * 16 + kq * 4) = R[2 * NS + n];
+      }
+    } else if (G8A) {
+#pragma unroll
+      for (int j = 0; j < Q8; ++j) {
+        const int n = wid * Q8 + j;
+        if (n < NS && n / NSP == h)
+          *reinterpret_cast<f32x4*>(O + (8 * 16 + r16) * OS + (n - h * NSP) * 16 + kq * 4) = R[XQ * KS + j];
+      }
+    }
+    step_barrier();
+    const int C8 = NSP * 2, c0 = h * NSP * 16;  // 8-channel units per pixel in the slice
     const int units = (p1 - p0) * C8;
-    bf16* outb = a.out + ((size_t)b * HW + p0) * a.Cout;
-    const bf16* resb = inb + (size_t)p0 * a.Cin;
+    bf16* outb = a.out + ((size_t)b * HW + p0) * a.Cout + c0;
+    const bf16* resb = inb + (size_t)p0 * a.Cin + c0;
     for (int u = tid; u < units; u += kNT) {
       const int px = u / C8, c = (u - px * C8) * 8;
       const f32x4 o0 = *reinterpret_cast<const f32x4*>(O + px * OS + c);
       const f32x4 o1 = *reinterpret_cast<const f32x4*>(O + px * OS + c + 4);
-      const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bp + c);
-      const f32x4 b1 = *reinterpret_cast<const f32x4*>(a.bp + c + 4);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bp + c0 + c);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(a.bp + c0 + c + 4);
       bf16x8 r = zero8();
       if (a.residual) r = ld8(resb + (size_t)px * a.Cin + c);
       bf16x8 o;
@@ -380,18 +435,18 @@ __global__ __launch_bounds__(kNT) void fused_ir_stream_kernel(StreamArgs a) {
   STREAM_STAMP(63);
 }
 
-template <int KS, int NS, int XQ, int DIL, int WCP>
+template <int KS, int NS, int XQ, int DIL, int WCP, bool G8A>
 void launch_stream(const StreamArgs& a, hipStream_t st) {
   const size_t lds = fused_ir_stream_lds(a.Cin, a.Cout, a.WR, a.WCP);
   if (lds > 160 * 1024) throw std::invalid_argument("fused_ir_stream: LDS over 160 KiB");
   static bool attr = false;
   if (!attr) {
-    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_ir_stream_kernel<KS, NS, XQ, DIL, WCP>),
+    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_ir_stream_kernel<KS, NS, XQ, DIL, WCP, G8A>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
           "fused_ir_stream attr");
     attr = true;
   }
-  hipLaunchKernelGGL((fused_ir_stream_kernel<KS, NS, XQ, DIL, WCP>), dim3(a.B * a.S), dim3(kNT), lds, st, a);
+  hipLaunchKernelGGL((fused_ir_stream_kernel<KS, NS, XQ, DIL, WCP, G8A>), dim3(a.B * a.S), dim3(kNT), lds, st, a);
   check_launch("fused_ir_stream");
 }
 
@@ -399,8 +454,8 @@ void launch_stream(const StreamArgs& a, hipStream_t st) {
 
 size_t fused_ir_stream_lds(int Cin, int Cout, int WR, int WCP) {
   const int KS = Cin / 32, NS = (Cout + 15) / 16;
-  const size_t main = (size_t)kNSL * (2 * KS + NS + 1) * 1024 + 8 * (size_t)stream_plane_bytes(WR, WCP);
-  const size_t otile = (size_t)kGB * 4 * 16 * (Cout + 4) * 4;  // epilogue fp32 output tile
+  const size_t main = (size_t)stream_nsl(NS) * (2 * KS + NS + 1) * 1024 + 8 * (size_t)stream_plane_bytes(WR, WCP);
+  const size_t otile = (size_t)kGB * 4 * 16 * (NS / stream_npass(NS) * 16 + 4) * 4;  // epilogue tile
   return main > otile ? main : otile;
 }
 
@@ -422,12 +477,20 @@ void fused_ir_stream(const FusedSpanParams& p, hipStream_t st) {
     throw std::invalid_argument("fused_ir_stream: W 33, dilation 1/2, halo <= 256/320 px");
 #define STREAM(K_, N_)                                   \
   if (KS == K_ && NS == N_) {                            \
-    if (p.dil == 1) launch_stream<K_, N_, 4, 1, 49>(a, st);  \
-    else launch_stream<K_, N_, 5, 2, 49>(a, st);             \
+    if (p.dil == 1 && p.npi == 1) launch_stream<K_, N_, 4, 1, 49, true>(a, st);   \
+    else if (p.dil == 1) launch_stream<K_, N_, 4, 1, 49, false>(a, st);           \
+    else if (p.npi == 1) launch_stream<K_, N_, 5, 2, 49, true>(a, st);            \
+    else launch_stream<K_, N_, 5, 2, 49, false>(a, st);                           \
     return;                                              \
   }
   // blocks 7-9 (64->64), 10 (64->96), 11-12 (96->96), 13 (96->160), 14-15 (160->160)
   STREAM(2, 4) STREAM(2, 6) STREAM(3, 6) STREAM(3, 10) STREAM(5, 10)
+  // block 16 (160->320, dilation 2): group 8 on the expansion waves only (the projection
+  // waves' accumulators for 2.5 groups x 20 subtiles would not fit 256 VGPRs)
+  if (KS == 5 && NS == 20 && p.dil == 2) {
+    launch_stream<5, 20, 5, 2, 49, true>(a, st);
+    return;
+  }
 #undef STREAM
   throw std::invalid_argument("fused_ir_stream: no instantiation for this (Cin, Cout)");
 }

@@ -45,12 +45,12 @@ def main():
                 tab = FS.span_table(H, H, S, dil, dev)
             except ValueError:
                 continue
-            opts = [None] if a.stream else FS.span_npi_options(cout)
+            opts = [0, 1] if a.stream else FS.span_npi_options(cout)
             if a.stream and not FS.stream_supported(cin, cout, 1, H, H, S, dil):
                 continue
             for npi in opts:
                 if a.stream:
-                    run = lambda: FS.fused_ir_stream(x, packed, tab, out, B=B, residual=spec.residual)
+                    run = lambda: FS.fused_ir_stream(x, packed, tab, out, B=B, residual=spec.residual, variant=npi)
                 else:
                     run = lambda: FS.fused_ir_span(x, packed, tab, out, B=B, residual=spec.residual, npi=npi)
                 for _ in range(3):
@@ -63,12 +63,12 @@ def main():
                 en.synchronize()
                 us = st.elapsed_time(en) / a.reps * 1e3
                 print(f"block{idx:2d} {cin:3d}->{spec.hidden:3d}->{cout:3d} d{dil} S={S:2d} "
-                      f"{'stream' if a.stream else f'npi={npi}'}: "
+                      f"{f'stream v{npi}' if a.stream else f'npi={npi}'}: "
                       f"{us:7.1f} us  {flop / us / 1e6:7.1f} TFLOP/s  (xg={tab['xg']}, nh_max={tab['nh_max']})",
                       flush=True)
                 if a.trace and a.stream:
                     tr = torch.zeros(B * S * 2 * 64, dtype=torch.int64, device=dev)
-                    FS.fused_ir_stream(x, packed, tab, out, B=B, residual=spec.residual, trace=tr)
+                    FS.fused_ir_stream(x, packed, tab, out, B=B, residual=spec.residual, trace=tr, variant=npi)
                     torch.cuda.synchronize()
                     t = tr.view(B * S, 2, 64).cpu().numpy().astype(np.int64)
                     NC = packed["hidP"] // 32

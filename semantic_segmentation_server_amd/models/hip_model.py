@@ -376,6 +376,8 @@ class HipDeepLab:
                 bufs[f"aspp_order{gv}"] = order
                 grouped.append((f"grouped_v{gv}", [
                     lambda *_, convs=convs, order=order, gv=gv: K.conv_gemm_grouped(convs, order, gv)]))
+                # (branch-affine XCD orders, K.grouped_tile_order_branch, measured 6-16 us
+                # slower on every variant: profiles/r3_negative_results.txt)
             ops[aspp_at:] = [Choice("aspp.branches", grouped + [seq])]
         img_bias = None
         if self.has_pool:
@@ -628,9 +630,10 @@ class HipDeepLab:
                             x, sp, tab, out, B=B, residual=s.residual, npi=npi)]))
                 if FS.stream_supported(s.cin, s.cout, 1, h, w, S, s.dilation):
                     # wave-specialised: expansion waves | depthwise+projection waves
-                    variants.insert(0, (f"stream{S}", [
-                        lambda *_, x=inp, out=out, tab=tab, sp=blk["span"]: FS.fused_ir_stream(
-                            x, sp, tab, out, B=B, residual=s.residual)]))
+                    for v in (0, 1):
+                        variants.insert(0, (f"stream{S}" + ("g" if v else ""), [
+                            lambda *_, x=inp, out=out, tab=tab, sp=blk["span"], v=v: FS.fused_ir_stream(
+                                x, sp, tab, out, B=B, residual=s.residual, variant=v)]))
         if blk["expand"] is not None and FB.band_supported(s.cin, hid, s.cout, s.stride, s.dilation, OW):
             # row-streaming bands: every input row expanded once into an on-chip fp16 row
             if "band" not in blk:

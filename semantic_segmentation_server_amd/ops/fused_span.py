@@ -147,10 +147,12 @@ def fused_ir_span(x: torch.Tensor, packed: Dict, table: Dict, out: torch.Tensor,
 
 
 def fused_ir_stream(x: torch.Tensor, packed: Dict, table: Dict, out: torch.Tensor, *, B: int,
-                    residual: bool, trace: Optional[torch.Tensor] = None) -> torch.Tensor:
+                    residual: bool, trace: Optional[torch.Tensor] = None, variant: int = 0) -> torch.Tensor:
     """Launch fused_ir_stream_kernel (csrc/hip/fused_ir_stream.hip): the same spans and
     chunk images as fused_ir_span, run by wave-specialised expansion / depthwise+projection
-    waves over an LDS-DMA chunk ring. x [B, H, W, Cin] bf16, out [B, H, W, Cout] bf16."""
+    waves over an LDS-DMA chunk ring. x [B, H, W, Cin] bf16, out [B, H, W, Cout] bf16.
+    variant 1: the span's ninth output group runs on the expansion waves (balances the two
+    roles: the depthwise+projection waves were the critical path, profiles/r3_stream_trace.txt)."""
     from .hip_ops import _chk, _dbg, _hip_mod, _ptr, _stream
     H, W = table["H"], table["W"]
     Cin, Cout = packed["Cin"], packed["Cout"]
@@ -167,18 +169,20 @@ def fused_ir_stream(x: torch.Tensor, packed: Dict, table: Dict, out: torch.Tenso
                                _ptr(out), B, H, W, Cin, packed["hidP"], Cout, table["dil"],
                                int(bool(residual)), table["S"], table["WR"], table["WCP"],
                                table["hstride"], table["nh_max"], _stream(),
-                               0 if trace is None else _ptr(trace))
+                               0 if trace is None else _ptr(trace), int(variant))
     _dbg("fused_ir_stream")
     return out
 
 
-STREAM_SHAPES = ((64, 64), (64, 96), (96, 96), (96, 160), (160, 160))
+STREAM_SHAPES = ((64, 64), (64, 96), (96, 96), (96, 160), (160, 160), (160, 320))
 
 
 def stream_supported(Cin: int, Cout: int, stride: int, H: int, W: int, S: int, dil: int) -> bool:
     """fused_ir_stream instantiations: the 33-wide maps of the headline, dilation 1 (halo
     <= 256 px) or 2 (<= 320 px), spans <= 144 px, LDS within 160 KiB."""
     if stride != 1 or (Cin, Cout) not in STREAM_SHAPES or W != 33 or dil not in (1, 2):
+        return False
+    if (Cin, Cout) == (160, 320) and dil != 2:
         return False
     try:
         t = span_table(H, W, S, dil)

@@ -197,6 +197,72 @@ def grouped_tile_order(convs: List[dict], variant: int, device=None, xcds: int =
     return torch.tensor(out, dtype=torch.int32).to(device).contiguous()
 
 
+def grouped_tile_order_branch(convs: List[dict], variant: int, device=None, xcds: int = 8) -> torch.Tensor:
+    """Branch-affine block -> tile table: every XCD (block i runs on XCD i % xcds under the
+    round-robin dispatch; speed only, never correctness) is given tiles of ONE conv, so that
+    conv's weights (1.47 MB per 3x3 ASPP branch: re-read by every row tile) stay in the XCD's
+    4 MiB L2 instead of four branches' 4.4 MB thrashing every L2 (the global LPT order mixes
+    branches on every XCD; the row-range split of ``grouped_tile_order(xcds=8)`` did too).
+    Each XCD runs the same number of blocks (positional dispatch); 3x3 convs get XCD sets
+    in proportion to their work, 1x1 tiles fill the remaining block counts of the least
+    loaded XCDs; each XCD runs its tiles heaviest first."""
+    BM, BN = GROUP_TILE[variant]
+    tiles = []  # (cost, entry, group)
+    for g, c in enumerate(convs):
+        tn = -(-c["Cout"] // BN)
+        taps = _tile_taps(c["B"], c["OH"], c["OW"], c["k"], c["dil"], BM, c.get("perm"))
+        kch = -(-c["Cin"] // 64)
+        for tm in range(taps.numel()):
+            for n in range(tn):
+                tiles.append((int(taps[tm]) * kch, (g << 24) | (tm * tn + n), g))
+    G = len(convs)
+    # the dispatcher hands block i to XCD i % xcds whatever its load, so every XCD runs the
+    # same NUMBER of blocks: the 3x3 branches get XCD sets in proportion to their work, and
+    # the light 1x1 tiles (164 KB of weights) fill every XCD's remaining block count
+    heavy = [g for g in range(G) if convs[g]["k"] > 1] or list(range(G))
+    gcost = {g: sum(t[0] for t in tiles if t[2] == g) for g in heavy}
+    tot = max(1, sum(gcost.values()))
+    share = {g: xcds * gcost[g] / tot for g in heavy}
+    cnt = {g: max(1, int(share[g])) for g in heavy}
+    while sum(cnt.values()) > xcds:
+        i = max((g for g in heavy if cnt[g] > 1), key=lambda g: cnt[g] - share[g])
+        cnt[i] -= 1
+    while sum(cnt.values()) < xcds:
+        i = max(heavy, key=lambda g: share[g] - cnt[g])
+        cnt[i] += 1
+    xs, x0 = {}, 0
+    for g in heavy:
+        xs[g] = list(range(x0, x0 + cnt[g]))
+        x0 += cnt[g]
+    T = len(tiles)
+    cap = [T // xcds + (1 if x < T % xcds else 0) for x in range(xcds)]
+    lists = [[] for _ in range(xcds)]
+    load = [0] * xcds
+    order = sorted(tiles, key=lambda t: (-t[0], t[1]))
+    for cost, ent, g in order:
+        if g not in xs:
+            continue
+        cands = [y for y in xs[g] if len(lists[y]) < cap[y]] or [y for y in range(xcds) if len(lists[y]) < cap[y]]
+        x = min(cands, key=lambda y: load[y])
+        lists[x].append((cost, ent))
+        load[x] += cost
+    for cost, ent, g in order:  # fillers: the least loaded XCD with blocks left
+        if g in xs:
+            continue
+        x = min((y for y in range(xcds) if len(lists[y]) < cap[y]), key=lambda y: load[y])
+        lists[x].append((cost, ent))
+        load[x] += cost
+    for lst in lists:
+        lst.sort(key=lambda t: (-t[0], t[1]))
+    out = []
+    for j in range(max(cap)):
+        for x in range(xcds):  # position xcds * j + x runs on XCD x
+            if j < len(lists[x]):
+                out.append(lists[x][j][1])
+    assert sorted(out) == sorted(t[1] for t in tiles)
+    return torch.tensor(out, dtype=torch.int32).to(device).contiguous()
+
+
 def conv_gemm_grouped(convs: List[dict], order: torch.Tensor, variant: int = 5) -> None:
     """Up to 4 independent stride-1 'same' NHWC convs with one Cout (the ASPP branches)
     in ONE LDS-DMA grid, tiles in the ``grouped_tile_order`` table. Each conv is a

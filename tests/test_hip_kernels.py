@@ -1185,6 +1185,7 @@ def test_fused_ir_span(cin, cout, dil, H, S):
     (96, 160, 1, 33, 8),    # block 13
     (160, 160, 2, 33, 8),   # blocks 14-15 (dilation 2, residual)
     (160, 160, 2, 33, 16),  # 16 spans per image
+    (160, 320, 2, 33, 8),   # block 16 (3-slot ring, two epilogue passes)
     (64, 64, 1, 33, 32),    # batch-1 span counts
     (96, 96, 1, 29, 7),     # odd map height / span sizes
 ])
@@ -1206,17 +1207,18 @@ def test_fused_ir_stream(cin, cout, dil, H, S):
     table = FS.span_table(H, W, S, dil, DEV)
     xd = _nhwc(x).to(DEV)
     emu = FS.emulate_fused_span(_nhwc(x).float().numpy(), packed, table, residual=spec.residual)
-    out = torch.full((B, H, W, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
-    FS.fused_ir_stream(xd, packed, table, out, B=B, residual=spec.residual)
-    torch.cuda.synchronize()
-    assert torch.isfinite(out).all()
-    assert _rel(_nchw(out).cpu(), ref) < 2e-2
-    assert _rel(out.cpu().float(), torch.from_numpy(emu)) < 5e-3
-    # bit-exact rerun (no read of bytes another run or wave left behind)
-    out2 = torch.full_like(out, float("nan"))
-    FS.fused_ir_stream(xd, packed, table, out2, B=B, residual=spec.residual)
-    torch.cuda.synchronize()
-    assert torch.equal(out.view(torch.int16), out2.view(torch.int16))
+    for variant in (0, 1):
+        out = torch.full((B, H, W, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
+        FS.fused_ir_stream(xd, packed, table, out, B=B, residual=spec.residual, variant=variant)
+        torch.cuda.synchronize()
+        assert torch.isfinite(out).all(), variant
+        assert _rel(_nchw(out).cpu(), ref) < 2e-2, variant
+        assert _rel(out.cpu().float(), torch.from_numpy(emu)) < 5e-3, variant
+        # bit-exact rerun (no read of bytes another run or wave left behind)
+        out2 = torch.full_like(out, float("nan"))
+        FS.fused_ir_stream(xd, packed, table, out2, B=B, residual=spec.residual, variant=variant)
+        torch.cuda.synchronize()
+        assert torch.equal(out.view(torch.int16), out2.view(torch.int16)), variant
 
 
 @pytest.mark.parametrize("M,HW,ncls,ldo,img", [
