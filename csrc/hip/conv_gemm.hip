@@ -888,7 +888,11 @@ void conv_gemm_grouped(const ConvParams* ps, int n, const int* order, int nblock
     case 12: launch_conv_glds_group<8, 4, 4, 2, 4, 32>(ga, nblocks, s); break;  // 256 x 256
     case 13: launch_conv_glds_group<4, 4, 4, 2, 4, 32>(ga, nblocks, s); break;  // 128 x 256
     case 14: launch_conv_glds_group<8, 4, 3, 2, 4, 32>(ga, nblocks, s); break;  // 256 x 256, 3 stages
-    default: throw std::invalid_argument("conv_gemm_grouped: variant must be 5, 6, 8, 10-14");
+    // 16 waves (4 per SIMD, 64 x 64 per wave): twice the waves of v6 to cover the LDS-DMA
+    // and LDS latency of the 1-workgroup-per-CU 256 x 256 tiles (MFMA busy ~23 % in v6)
+    case 15: launch_conv_glds_group<4, 4, 2, 4, 4>(ga, nblocks, s); break;      // 256 x 256
+    case 16: launch_conv_glds_group<4, 4, 4, 4, 4, 32>(ga, nblocks, s); break;  // 256 x 256, 32-deep
+    default: throw std::invalid_argument("conv_gemm_grouped: variant must be 5, 6, 8, 10-16");
   }
 }
 
