@@ -121,7 +121,7 @@ PYBIND11_MODULE(_hip, m) {
            int hstride, int nh_max, uintptr_t stream, uintptr_t trace, int variant) {
           FusedSpanParams p;
           p.trace = P<long long>(trace);
-          p.npi = variant == 1 ? 1 : 0;  // 1: group 8 on the expansion waves (G8A)
+          p.npi = variant;  // 0: 8 waves; 1: group 8 on the expansion waves (G8A); 2: 12 waves
           p.in = P<const bf16>(in); p.w = P<const void>(w); p.bp = P<const float>(bp);
           p.table = P<const int>(table); p.out = P<bf16>(out);
           p.B = B; p.H = H; p.W = W; p.Cin = Cin; p.hidP = hidP; p.Cout = Cout; p.dil = dil;

@@ -44,8 +44,10 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-constexpr int kNW = 8;     // waves per workgroup
-constexpr int kNT = 64 * kNW;
+// waves per workgroup: 8 (4 expansion + 4 depthwise/projection) or, for the MODE-2
+// variant, 12 (4 + 8: two depthwise/projection waves per SIMD hide each other's LDS and
+// VALU latency -- the same lever that took the grouped ASPP GEMM from 8 to 16 waves)
+__host__ __device__ constexpr int stream_waves(int mode) { return mode == 2 ? 12 : 8; }
 constexpr int kHdr = 4;    // span table header: p0, p1, wy0, nh
 constexpr int kXQ = 5;     // halo groups per expansion wave (<= 20 groups = 320 halo px)
 constexpr int kGB = 3;     // output groups per depthwise+projection wave (<= 12 groups)
@@ -237,8 +239,13 @@ __device__ __forceinline__ void dwproj_groups(const char* Wp, const char* misc, 
   }
 }
 
-template <int KS, int NS, int XQ, int DIL, int WCP, bool G8A>
-__global__ __launch_bounds__(kNT) void fused_ir_stream_kernel(StreamArgs a) {
+template <int KS, int NS, int XQ, int DIL, int WCP, int MODE>
+__global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kernel(StreamArgs a) {
+  // MODE 0: 8 waves, the ninth output group split over the projection waves;
+  // 1 (G8A): 8 waves, the ninth group on the expansion waves; 2: 12 waves, projection
+  // wave b owns group b, wave 7 also the ninth group
+  constexpr bool G8A = MODE == 1;
+  constexpr int kNW = stream_waves(MODE), kNT = 64 * kNW;
   constexpr int NPC = 2 * KS + NS + 1;          // 1 KiB pieces per chunk image
   constexpr int CHB = NPC * 1024;
   constexpr int WEB = 2 * KS * 1024, WPB = NS * 1024;
@@ -279,7 +286,7 @@ __global__ __launch_bounds__(kNT) void fused_ir_stream_kernel(StreamArgs a) {
   // two role-private arrays by itself: 190..256 VGPRs + spills against max(A, BC))
   constexpr int NS3 = NS >= 10 ? NS / 2 : NS;
   constexpr int Q8 = (NS + 3) / 4;  // G8A: group-8 subtiles per expansion wave
-  constexpr int NRA = XQ * KS + (G8A ? Q8 : 0), NRB = G8A ? 2 * NS : 2 * NS + NS3;
+  constexpr int NRA = XQ * KS + (G8A ? Q8 : 0), NRB = (G8A || MODE == 2) ? 2 * NS : 2 * NS + NS3;
   constexpr int NR = NRA > NRB ? NRA : NRB;
   f32x4 R[NR];
   int hpos[kXQ];
@@ -321,7 +328,7 @@ __global__ __launch_bounds__(kNT) void fused_ir_stream_kernel(StreamArgs a) {
   // split it for the wide blocks, waves 2/3 compute a copy that is never stored.
   const bool expander = wid < 4;
   const int bw = wid - 4;
-  const int og[kGB] = {3 - bw, 7 - bw, 8};
+  const int og[kGB] = {MODE == 2 ? bw : 3 - bw, MODE == 2 ? 8 : 7 - bw, 8};
   const int n3 = NS3 == NS ? 0 : (bw & 1) * NS3;
   const bool own3 = NS3 == NS ? bw == 0 : bw < 2;
   int dpos[kGB];
@@ -360,7 +367,14 @@ __global__ __launch_bounds__(kNT) void fused_ir_stream_kernel(StreamArgs a) {
     } else if (t >= 1) {
       const int c = t - 1;
       const char* Wp = ring + (c % kNSL) * CHB + WEB;
-      if (G8A)
+      if (MODE == 2) {
+        const char* Ek = sE + (c & 1) * 4 * PLANE + kq * PLANE;
+        dwproj_groups<1, NS, DIL, WCP, NR>(Wp, Wp + WPB, Ek, dpos8, 0, NS - 1, R, 0, lane, kq);
+        if (bw == 7) {
+          const int dposn[1] = {dpos[1]};
+          dwproj_groups<1, NS, DIL, WCP, NR>(Wp, Wp + WPB, Ek, dposn, 0, NS - 1, R, NS, lane, kq);
+        }
+      } else if (G8A)
         dwproj_groups<2, NS, DIL, WCP, NR, (NS <= 10)>(Wp, Wp + WPB, sE + (c & 1) * 4 * PLANE + kq * PLANE, dpos01, 0,
                                            NS - 1, R, 0, lane, kq);
       else
@@ -394,9 +408,9 @@ __global__ __launch_bounds__(kNT) void fused_ir_stream_kernel(StreamArgs a) {
       for (int g = 0; g < 2; ++g)
 #pragma unroll
         for (int n = 0; n < NS; ++n)
-          if (n / NSP == h)
+          if (n / NSP == h && (MODE != 2 || g == 0 || bw == 7))
             *reinterpret_cast<f32x4*>(O + (og[g] * 16 + r16) * OS + (n - h * NSP) * 16 + kq * 4) = R[g * NS + n];
-      if (own3 && !G8A) {
+      if (own3 && MODE == 0) {
 #pragma unroll
         for (int n = 0; n < NS3; ++n)
           if ((n3 + n) / NSP == h)
@@ -435,18 +449,19 @@ __global__ __launch_bounds__(kNT) void fused_ir_stream_kernel(StreamArgs a) {
   STREAM_STAMP(63);
 }
 
-template <int KS, int NS, int XQ, int DIL, int WCP, bool G8A>
+template <int KS, int NS, int XQ, int DIL, int WCP, int MODE>
 void launch_stream(const StreamArgs& a, hipStream_t st) {
   const size_t lds = fused_ir_stream_lds(a.Cin, a.Cout, a.WR, a.WCP);
   if (lds > 160 * 1024) throw std::invalid_argument("fused_ir_stream: LDS over 160 KiB");
   static bool attr = false;
   if (!attr) {
-    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_ir_stream_kernel<KS, NS, XQ, DIL, WCP, G8A>),
+    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_ir_stream_kernel<KS, NS, XQ, DIL, WCP, MODE>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
           "fused_ir_stream attr");
     attr = true;
   }
-  hipLaunchKernelGGL((fused_ir_stream_kernel<KS, NS, XQ, DIL, WCP, G8A>), dim3(a.B * a.S), dim3(kNT), lds, st, a);
+  hipLaunchKernelGGL((fused_ir_stream_kernel<KS, NS, XQ, DIL, WCP, MODE>), dim3(a.B * a.S),
+                     dim3(64 * stream_waves(MODE)), lds, st, a);
   check_launch("fused_ir_stream");
 }
 
@@ -475,12 +490,15 @@ void fused_ir_stream(const FusedSpanParams& p, hipStream_t st) {
   // dilation 1 (halo <= 16 groups: 4 rounds per expansion wave) and 2 (<= 20: 5 rounds)
   if (p.W != 33 || p.dil > 2 || p.nh_max > (p.dil == 1 ? 4 : 5) * 64)
     throw std::invalid_argument("fused_ir_stream: W 33, dilation 1/2, halo <= 256/320 px");
+  // 12-wave variant: blocks 7-12 (Cout <= 96; at Cout 160 the accumulators spill at 168 VGPRs)
+#define STREAM12(K_, N_) ((N_) <= 6 ? 2 : 0)
 #define STREAM(K_, N_)                                   \
   if (KS == K_ && NS == N_) {                            \
-    if (p.dil == 1 && p.npi == 1) launch_stream<K_, N_, 4, 1, 49, true>(a, st);   \
-    else if (p.dil == 1) launch_stream<K_, N_, 4, 1, 49, false>(a, st);           \
-    else if (p.npi == 1) launch_stream<K_, N_, 5, 2, 49, true>(a, st);            \
-    else launch_stream<K_, N_, 5, 2, 49, false>(a, st);                           \
+    if (p.dil == 1 && p.npi == 2) launch_stream<K_, N_, 4, 1, 49, STREAM12(K_, N_)>(a, st);  \
+    else if (p.dil == 1 && p.npi == 1) launch_stream<K_, N_, 4, 1, 49, 1>(a, st);        \
+    else if (p.dil == 1) launch_stream<K_, N_, 4, 1, 49, 0>(a, st);                      \
+    else if (p.npi == 1) launch_stream<K_, N_, 5, 2, 49, 1>(a, st);                      \
+    else launch_stream<K_, N_, 5, 2, 49, 0>(a, st);                                      \
     return;                                              \
   }
   // blocks 7-9 (64->64), 10 (64->96), 11-12 (96->96), 13 (96->160), 14-15 (160->160)
@@ -488,10 +506,11 @@ void fused_ir_stream(const FusedSpanParams& p, hipStream_t st) {
   // block 16 (160->320, dilation 2): group 8 on the expansion waves only (the projection
   // waves' accumulators for 2.5 groups x 20 subtiles would not fit 256 VGPRs)
   if (KS == 5 && NS == 20 && p.dil == 2) {
-    launch_stream<5, 20, 5, 2, 49, true>(a, st);
+    launch_stream<5, 20, 5, 2, 49, 1>(a, st);
     return;
   }
 #undef STREAM
+#undef STREAM12
   throw std::invalid_argument("fused_ir_stream: no instantiation for this (Cin, Cout)");
 }
 

@@ -45,7 +45,7 @@ def main():
                 tab = FS.span_table(H, H, S, dil, dev)
             except ValueError:
                 continue
-            opts = [0, 1] if a.stream else FS.span_npi_options(cout)
+            opts = ([0, 1, 2] if cout <= 96 and dil == 1 else [0, 1]) if a.stream else FS.span_npi_options(cout)
             if a.stream and not FS.stream_supported(cin, cout, 1, H, H, S, dil):
                 continue
             for npi in opts:

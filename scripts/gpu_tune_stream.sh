@@ -6,7 +6,7 @@ export SSA_NO_AUTOBUILD=1
 O=gpurun_out/tune_stream
 mkdir -p $O
 cp assets/tune_mi355x.json $O/tune.json
-ONLY=block7,block8,block9,block10,block11,block12,block13,block14,block15,block16
+ONLY=${ONLY:-block7,block8,block9,block10,block11,block12,block13,block14,block15,block16}
 for B in 32 1; do
   SSA_TUNE_FILE=$PWD/$O/tune.json SSA_RETUNE_ONLY=$ONLY SSA_LOG_AUTOTUNE=1 timeout -k 10 300 python bench.py --batch $B --steps 20 --warmup 5 --rpc 0 > $O/tune_$B.json 2> $O/tune_$B.err || { tail -5 $O/tune_$B.err; exit 1; }
   grep "autotune" $O/tune_$B.err | grep -E "block(7|8|9|1[0-6]):" | sed 's/, dwp[a-z0-9]*\.pw2x3=[0-9.]*us//g' | cut -c1-300

@@ -630,8 +630,8 @@ class HipDeepLab:
                             x, sp, tab, out, B=B, residual=s.residual, npi=npi)]))
                 if FS.stream_supported(s.cin, s.cout, 1, h, w, S, s.dilation):
                     # wave-specialised: expansion waves | depthwise+projection waves
-                    for v in (0, 1):
-                        variants.insert(0, (f"stream{S}" + ("g" if v else ""), [
+                    for v in ((0, 1, 2) if s.cout <= 96 and s.dilation == 1 else (0, 1)):
+                        variants.insert(0, (f"stream{S}" + ("", "g", "w")[v], [
                             lambda *_, x=inp, out=out, tab=tab, sp=blk["span"], v=v: FS.fused_ir_stream(
                                 x, sp, tab, out, B=B, residual=s.residual, variant=v)]))
         if blk["expand"] is not None and FB.band_supported(s.cin, hid, s.cout, s.stride, s.dilation, OW):
