@@ -137,16 +137,25 @@ PYBIND11_MODULE(_hip, m) {
   m.def("fused_ir_band",
         [](uintptr_t in, uintptr_t blob, uintptr_t out, int B, int IH, int IW, int Cin, int OH, int OW,
            int Cout, int hidP, int stride, int residual, int R, int nslot, int blob_bytes, int o_be,
-           int o_wd, int o_bd, int o_wp, int o_bp, uintptr_t stream) {
+           int o_wd, int o_bd, int o_wp, int o_bp, uintptr_t stream, int hs, int split) {
           FusedBandParams p;
+          p.hs = hs;
+          p.split = split;
           p.in = P<const bf16>(in); p.blob = P<const void>(blob); p.out = P<bf16>(out);
           p.B = B; p.IH = IH; p.IW = IW; p.Cin = Cin; p.OH = OH; p.OW = OW; p.Cout = Cout;
           p.hidP = hidP; p.stride = stride; p.residual = residual; p.R = R; p.nslot = nslot;
           p.blob_bytes = blob_bytes; p.o_be = o_be; p.o_wd = o_wd; p.o_bd = o_bd; p.o_wp = o_wp;
           p.o_bp = o_bp;
           fused_ir_band(p, S(stream));
-        });
-  m.def("fused_ir_band_lds", &fused_ir_band_lds);
+        },
+        py::arg("in"), py::arg("blob"), py::arg("out"), py::arg("B"), py::arg("IH"), py::arg("IW"),
+        py::arg("Cin"), py::arg("OH"), py::arg("OW"), py::arg("Cout"), py::arg("hidP"), py::arg("stride"),
+        py::arg("residual"), py::arg("R"), py::arg("nslot"), py::arg("blob_bytes"), py::arg("o_be"),
+        py::arg("o_wd"), py::arg("o_bd"), py::arg("o_wp"), py::arg("o_bp"), py::arg("stream"),
+        py::arg("hs") = 1, py::arg("split") = 1);
+  m.def("fused_ir_band_lds", &fused_ir_band_lds, py::arg("stride"), py::arg("hidP"), py::arg("OW"),
+        py::arg("blob_bytes"), py::arg("nslot"), py::arg("hs") = 1, py::arg("Cout") = 0,
+        py::arg("split") = 1);
   m.def("fused_ir_tile_lds", &fused_ir_tile_lds);
   m.def("fused_ir_persist_lds", &fused_ir_persist_lds, py::arg("CinP"), py::arg("hidP"), py::arg("Cout"),
         py::arg("stride"), py::arg("dil"), py::arg("TY"), py::arg("TX"), py::arg("nw") = 4);

@@ -55,6 +55,7 @@ struct BandArgs {
   const bf16* in; const char* blob; bf16* out;
   int B, IH, IW, Cin, OH, OW, Cout, residual;
   int R, nbx, nby;          // rows per band, bands across / down
+  int TW;                   // output columns per band (<= 16 * NW; < 16 * NW - 1 when split)
   int HE, P, EROW;          // stride-2 even-half entries, E pixel pitch (B), E row bytes
   int blob_bytes;           // host-packed weights, copied to LDS once
   int o_be, o_wd, o_bd, o_wp, o_bp;  // section offsets inside the blob (bytes)
@@ -75,10 +76,18 @@ __device__ __forceinline__ void lds_barrier() {
 // relu6 scale: expansion weights and bias and the depthwise bias come divided by 6, the
 // projection weights multiplied by 6, so both relu6 become [0, 1] clamps that fold into
 // the clamp bit of the instruction producing the value (E' = E / 6, D' = D / 6).
-template <int S, int NSH, int NS, int NSLOT, int NW>
-__global__ __launch_bounds__(64 * NW) void fused_ir_band_kernel(BandArgs a) {
-  constexpr int kBW = NW, kBT = 64 * NW;
+// HS = 2 (round 3): two waves per 16-column group, each owning half of the hidden
+// channels (expansion sub-tiles, depthwise chunks and the projection's K), twice the waves
+// per CU at the same LDS -- the band kernels ran 3-9 waves per CU and were latency-bound
+// (block 2: 62 % of wave cycles in s_waitcnt / barrier waits, profiles/r3_band2_pmc.txt).
+// The second half's projection partial sums reach the first half through a double-buffered
+// LDS exchange behind the next input row's barrier, and the first half stores that output
+// row one step later.
+template <int S, int NSH, int NS, int NSLOT, int NW, int HS>
+__global__ __launch_bounds__(64 * NW * HS) void fused_ir_band_kernel(BandArgs a) {
+  constexpr int kBW = NW, kBT = 64 * NW * HS;
   constexpr int NCH = NSH / 2;            // 32-channel hidden chunks
+  constexpr int NSHH = (NSH + HS - 1) / HS, NCHH = (NCH + HS - 1) / HS;  // per hidden half
   constexpr int HID = NSH * 16;
   constexpr int NDS = S == 1 ? 3 : 2;     // open output rows (D accumulator slots)
   constexpr int U = S == 1 ? 3 : 4;       // step unroll: static slot roles
@@ -86,7 +95,8 @@ __global__ __launch_bounds__(64 * NW) void fused_ir_band_kernel(BandArgs a) {
   constexpr int kTW = 16 * NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wid_all = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wid = wid_all % NW, hh = wid_all / NW;  // column wave, hidden half
   const int r16 = lane & 15, kq = lane >> 4;
 
   int blk = blockIdx.x;
@@ -94,8 +104,8 @@ __global__ __launch_bounds__(64 * NW) void fused_ir_band_kernel(BandArgs a) {
   blk /= a.nbx;
   const int by = blk % a.nby;
   const int b = blk / a.nby;
-  const int x0 = bx * kTW, y0 = by * a.R, y1 = min(y0 + a.R, a.OH);
-  const int twv = min(kTW, a.OW - x0);            // valid output columns of this band
+  const int x0 = bx * a.TW, y0 = by * a.R, y1 = min(y0 + a.R, a.OH);
+  const int twv = min(a.TW, a.OW - x0);           // valid output columns of this band
   const int iwv = (twv - 1) * S + 3;              // local input columns it reads
   const int ixb = x0 * S - 1;                     // global column of local input column 0
 
@@ -109,6 +119,8 @@ __global__ __launch_bounds__(64 * NW) void fused_ir_band_kernel(BandArgs a) {
   const char* sWp = smem + a.o_wp;
   const float* sBp = reinterpret_cast<const float*>(smem + a.o_bp);
   char* sE = smem + ((a.blob_bytes + 15) & ~15);
+  // HS = 2: projection partial-sum exchange [2 buffers][NW column waves][NS][64 lanes] f32x4
+  f32x4* sX = reinterpret_cast<f32x4*>(sE + NSLOT * a.EROW);
   __syncthreads();  // (the only full barrier: no global store is pending yet)
 
   // ---- this lane's output pixel and its three tap columns in E
@@ -170,11 +182,41 @@ __global__ __launch_bounds__(64 * NW) void fused_ir_band_kernel(BandArgs a) {
     }
   };
 
-  f16x8 D[NDS][NCH];
+  f16x8 D[NDS][NCHH];
 #pragma unroll
   for (int s = 0; s < NDS; ++s)
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) D[s][c] = f16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    for (int c = 0; c < NCHH; ++c) D[s][c] = f16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  // HS = 2, first half: the output row completed last step, waiting for the second half's
+  // partial sums (stored after this step's barrier)
+  f32x4 pend[NS];
+  int pend_o = -1, pend_buf = 0;
+  auto store_row = [&](int o, const f32x4 (&acc)[NS]) {
+    if (!xv) return;
+    const size_t opix = ((size_t)b * a.OH + o) * a.OW + x0 + xl;
+#pragma unroll
+    for (int n = 0; n < NS; ++n) {
+      const int ch = n * 16 + kq * 4;
+      if (ch >= a.Cout) continue;
+      f32x4 v = acc[n];
+      if (a.residual) {  // stride 1, Cin == Cout: same pixel of the input
+        const bf16x4 r = *reinterpret_cast<const bf16x4*>(a.in + opix * a.Cin + ch);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] += (float)r[q];
+      }
+      const bf16x4 ob = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      *reinterpret_cast<bf16x4*>(a.out + opix * a.Cout + ch) = ob;
+    }
+  };
+  auto flush_pending = [&]() {  // first half, behind a barrier after the exchange write
+    if (HS == 2 && hh == 0 && pend_o >= 0) {
+      const f32x4* xs = sX + ((size_t)(pend_buf * NW + wid) * NS) * 64 + lane;
+#pragma unroll
+      for (int n = 0; n < NS; ++n) pend[n] += xs[n * 64];
+      store_row(pend_o, pend);
+      pend_o = -1;
+    }
+  };
   const f16x8 h0 = {0, 0, 0, 0, 0, 0, 0, 0}, h1 = {1, 1, 1, 1, 1, 1, 1, 1};
 
   const int iy0 = y0 * S - 1;
@@ -196,7 +238,9 @@ __global__ __launch_bounds__(64 * NW) void fused_ir_band_kernel(BandArgs a) {
       // ---- [expand] input row iy -> E (fp16, relu6; zero at image columns outside)
       if (rowin) {
 #pragma unroll
-        for (int hs = 0; hs < NSH; ++hs) {
+        for (int hs2 = 0; hs2 < NSHH; ++hs2) {
+          const int hs = hh * NSHH + hs2;
+          if (HS > 1 && hs >= NSH) break;  // uniform
           const bf16x8 wf = *reinterpret_cast<const bf16x8*>(sWe + hs * 1024 + lane * 16);
           const f32x4 be4 = *reinterpret_cast<const f32x4*>(sBe + hs * 16 + kq * 4);
 #pragma unroll
@@ -213,6 +257,7 @@ __global__ __launch_bounds__(64 * NW) void fused_ir_band_kernel(BandArgs a) {
       // the input pixels of row t + U: in flight under the next U steps
       load_x(iy + U, xq[ph]);  // (past the band's last row: a harmless clamped reload)
       lds_barrier();
+      flush_pending();  // the second half's partial sums of last step's row are visible
       // ---- [depthwise] row iy into the open output rows it feeds
       // stride 1: output y0+t (ky 0, slot t%3), y0+t-1 (ky 1), y0+t-2 (ky 2, completes)
       // stride 2: t even -> y0+t/2 (ky 0), y0+t/2-1 (ky 2, completes); t odd -> ky 1
@@ -233,7 +278,9 @@ __global__ __launch_bounds__(64 * NW) void fused_ir_band_kernel(BandArgs a) {
       }
       if (rowin && xv) {
 #pragma unroll
-        for (int c = 0; c < NCH; ++c) {
+        for (int cc = 0; cc < NCHH; ++cc) {
+          const int c = hh * NCHH + cc;
+          if (HS > 1 && c >= NCH) break;  // uniform
           const int co = (c * 32 + kq * 8) * 2;
           f16x8 v[3];
 #pragma unroll
@@ -244,7 +291,7 @@ __global__ __launch_bounds__(64 * NW) void fused_ir_band_kernel(BandArgs a) {
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx) {
               const f16x8 w = *reinterpret_cast<const f16x8*>(sWd + ((ky[j] * 3 + kx) * HID) * 2 + co);
-              D[sl[j]][c] = v[kx] * w + D[sl[j]][c];
+              D[sl[j]][cc] = v[kx] * w + D[sl[j]][cc];
             }
           }
         }
@@ -257,51 +304,54 @@ __global__ __launch_bounds__(64 * NW) void fused_ir_band_kernel(BandArgs a) {
         if (o >= y0 && o < y1) {
           f32x4 acc[NS];
 #pragma unroll
-          for (int n = 0; n < NS; ++n) acc[n] = *reinterpret_cast<const f32x4*>(sBp + n * 16 + kq * 4);
+          for (int n = 0; n < NS; ++n)
+            acc[n] = hh == 0 ? *reinterpret_cast<const f32x4*>(sBp + n * 16 + kq * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int c = 0; c < NCH; ++c) {
+          for (int cc = 0; cc < NCHH; ++cc) {
+            const int c = hh * NCHH + cc;
+            if (HS > 1 && c >= NCH) break;  // uniform
             const f16x8 bd = *reinterpret_cast<const f16x8*>(sBd + (c * 32 + kq * 8) * 2);
-            f16x8 d = D[sc][c] + bd;
+            f16x8 d = D[sc][cc] + bd;
             d = __builtin_elementwise_min(__builtin_elementwise_max(d, h0), h1);
-            D[sc][c] = h0;
+            D[sc][cc] = h0;
 #pragma unroll
             for (int n = 0; n < NS; ++n) {
               const f16x8 wp = *reinterpret_cast<const f16x8*>(sWp + (n * NCH + c) * 1024 + lane * 16);
               acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wp, d, acc[n], 0, 0, 0);
             }
           }
-          if (xv) {
-            const size_t opix = ((size_t)b * a.OH + o) * a.OW + x0 + xl;
+          if (HS == 1) {
+            store_row(o, acc);
+          } else if (hh == 1) {  // partial sums -> exchange buffer (t & 1)
+            f32x4* xs = sX + ((size_t)((t & 1) * NW + wid) * NS) * 64 + lane;
 #pragma unroll
-            for (int n = 0; n < NS; ++n) {
-              const int ch = n * 16 + kq * 4;
-              if (ch >= a.Cout) continue;
-              f32x4 v = acc[n];
-              if (a.residual) {  // stride 1, Cin == Cout: same pixel of the input
-                const bf16x4 r = *reinterpret_cast<const bf16x4*>(a.in + opix * a.Cin + ch);
+            for (int n = 0; n < NS; ++n) xs[n * 64] = acc[n];
+          } else {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) v[q] += (float)r[q];
-              }
-              const bf16x4 ob = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-              *reinterpret_cast<bf16x4*>(a.out + opix * a.Cout + ch) = ob;
-            }
+            for (int n = 0; n < NS; ++n) pend[n] = acc[n];
+            pend_o = o;
+            pend_buf = t & 1;
           }
         }
       }
     }
   }
+  if (HS == 2) {
+    lds_barrier();
+    flush_pending();
+  }
 }
 
-template <int S, int NSH, int NS, int NSLOT, int NW>
+template <int S, int NSH, int NS, int NSLOT, int NW, int HS>
 void launch_band(const BandArgs& a, size_t lds, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_ir_band_kernel<S, NSH, NS, NSLOT, NW>),
+    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_ir_band_kernel<S, NSH, NS, NSLOT, NW, HS>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
           "fused_ir_band attr");
     attr = true;
   }
-  hipLaunchKernelGGL((fused_ir_band_kernel<S, NSH, NS, NSLOT, NW>), dim3(a.B * a.nby * a.nbx), dim3(64 * NW), lds,
+  hipLaunchKernelGGL((fused_ir_band_kernel<S, NSH, NS, NSLOT, NW, HS>), dim3(a.B * a.nby * a.nbx), dim3(64 * NW * HS), lds,
                      st, a);
   check_launch("fused_ir_band");
 }
@@ -329,9 +379,19 @@ BandGeom band_geom(int stride, int hidP, int OW) {
 
 }  // namespace
 
-size_t fused_ir_band_lds(int stride, int hidP, int OW, int blob_bytes, int nslot) {
-  const BandGeom g = band_geom(stride, hidP, OW);
-  return (size_t)((blob_bytes + 15) & ~15) + (size_t)nslot * g.EROW;
+// split = 2: the map width is cut into two column bands (129 -> 78 + 51: 5 column waves
+// instead of 9, so hs = 2 fits the 1024-thread workgroup); E rows then hold the band's input
+// columns only. A band of TW outputs reads (TW - 1) * S + 3 input columns, which the NW * S
+// pixel groups of its waves must cover: TW <= 16 * NW - 2.
+static int band_tw(int OW, int split) {
+  return split == 2 ? 16 * band_waves((OW + 1) / 2) - 2 : OW;
+}
+
+size_t fused_ir_band_lds(int stride, int hidP, int OW, int blob_bytes, int nslot, int hs, int Cout, int split) {
+  const int tw = band_tw(OW, split);
+  const BandGeom g = band_geom(stride, hidP, tw < OW ? tw : OW);
+  const size_t xch = hs == 2 ? (size_t)2 * band_waves(split == 2 ? (OW + 1) / 2 : OW) * ((Cout + 15) / 16) * 1024 : 0;
+  return (size_t)((blob_bytes + 15) & ~15) + (size_t)nslot * g.EROW + xch;
 }
 
 int fused_ir_band_cols(int stride) { (void)stride; return 0; }  // full map width
@@ -342,24 +402,34 @@ void fused_ir_band(const FusedBandParams& p, hipStream_t st) {
   if (p.residual && (p.stride != 1 || p.Cin != p.Cout)) throw std::invalid_argument("fused_ir_band: bad residual");
   if (p.OH != (p.IH - 1) / p.stride + 1 || p.OW != (p.IW - 1) / p.stride + 1)
     throw std::invalid_argument("fused_ir_band: output size must be the pad-1 3x3 conv's");
-  const BandGeom g = band_geom(p.stride, p.hidP, p.OW);
-  const size_t lds = fused_ir_band_lds(p.stride, p.hidP, p.OW, p.blob_bytes, p.nslot);
+  const int split = p.split == 2 ? 2 : 1;
+  const int tw = band_tw(p.OW, split) < p.OW ? band_tw(p.OW, split) : p.OW;  // band output columns
+  const BandGeom g = band_geom(p.stride, p.hidP, tw);
+  const int hs = p.hs == 2 ? 2 : 1;
+  const size_t lds = fused_ir_band_lds(p.stride, p.hidP, p.OW, p.blob_bytes, p.nslot, hs, p.Cout, split);
   if (lds > 160 * 1024) throw std::invalid_argument("fused_ir_band: LDS over 160 KiB");
   BandArgs a{p.in, reinterpret_cast<const char*>(p.blob), p.out, p.B, p.IH, p.IW, p.Cin, p.OH, p.OW, p.Cout,
-             p.residual, p.R, 1, cdiv(p.OH, p.R), g.HE, g.P, g.EROW, p.blob_bytes,
+             p.residual, p.R, cdiv(p.OW, tw), cdiv(p.OH, p.R), tw, g.HE, g.P, g.EROW, p.blob_bytes,
              p.o_be, p.o_wd, p.o_bd, p.o_wp, p.o_bp};
   const int NSH = p.hidP / 16, NS = (p.Cout + 15) / 16;
-  const int NW = band_waves(p.OW);
+  const int NW = band_waves(split == 2 ? (p.OW + 1) / 2 : p.OW);
+  if ((tw - 1) * p.stride + 3 > 16 * NW * p.stride) throw std::invalid_argument("fused_ir_band: band too wide");
 #define BAND(S_, NSH_, NS_, NW_)                                                 \
   if (p.stride == S_ && NSH == NSH_ && NS == NS_ && NW == NW_) {                 \
-    if (p.nslot == 2) launch_band<S_, NSH_, NS_, 2, NW_>(a, lds, st);            \
-    else launch_band<S_, NSH_, NS_, 1, NW_>(a, lds, st);                         \
+    if (hs == 2) {  /* 2 x NW waves must fit 1024 threads: NW <= 8 */            \
+      if (NW_ > 8) throw std::invalid_argument("fused_ir_band: hs 2 needs <= 8 column waves"); \
+      if (p.nslot == 2) launch_band<S_, NSH_, NS_, 2, NW_, (NW_ > 8 ? 1 : 2)>(a, lds, st); \
+      else launch_band<S_, NSH_, NS_, 1, NW_, (NW_ > 8 ? 1 : 2)>(a, lds, st);    \
+    } else if (p.nslot == 2) launch_band<S_, NSH_, NS_, 2, NW_, 1>(a, lds, st);  \
+    else launch_band<S_, NSH_, NS_, 1, NW_, 1>(a, lds, st);                      \
     return;                                                                      \
   }
   // block 1 (16 -> 96 -> 24, s2), 2 (24 -> 144 -> 24), 3 (24 -> 144 -> 32, s2),
   // 4-5 (32 -> 192 -> 32), 6 (32 -> 192 -> 64, s2); hidden 144 runs padded to 160
   // (map widths at 513^2: 129, 129, 65, 65, 33)
   BAND(2, 6, 2, 9) BAND(1, 10, 2, 9) BAND(2, 10, 2, 5) BAND(1, 12, 2, 5) BAND(2, 12, 4, 3)
+  // blocks 1-2 in two column bands (split = 2: 5 column waves)
+  BAND(2, 6, 2, 5) BAND(1, 10, 2, 5)
 #undef BAND
   throw std::invalid_argument("fused_ir_band: no instantiation for this (stride, hidden, Cout)");
 }

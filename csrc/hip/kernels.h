@@ -151,9 +151,12 @@ struct FusedBandParams {
   bf16* out = nullptr;        // [B, OH, OW, Cout]
   int B = 0, IH = 0, IW = 0, Cin = 0, OH = 0, OW = 0, Cout = 0, hidP = 0, stride = 1, residual = 0;
   int R = 8, nslot = 2, blob_bytes = 0, o_be = 0, o_wd = 0, o_bd = 0, o_wp = 0, o_bp = 0;
+  int hs = 1;                 // 2: two waves per column group, each half the hidden channels
+  int split = 1;              // 2: two column bands across the map width
 };
 void fused_ir_band(const FusedBandParams& p, hipStream_t s);
-size_t fused_ir_band_lds(int stride, int hidP, int OW, int blob_bytes, int nslot);
+size_t fused_ir_band_lds(int stride, int hidP, int OW, int blob_bytes, int nslot, int hs = 1, int Cout = 0,
+                         int split = 1);
 int fused_ir_band_cols(int stride);
 // Fused stem (3x3 s2, 3 -> 32, relu6, letterbox gather) + MobileNetV2 block 0
 // (dw 3x3 on 32 ch + relu6, project 32 -> 16); weights: ws [32][32] bf16 with

@@ -639,14 +639,22 @@ class HipDeepLab:
             if "band" not in blk:
                 blk["band"] = self._pack_band(blk, s)
             bp_ = blk["band"]
-            for nslot in (2, 1):
-                if FB.band_lds(bp_, s.stride, OW, nslot) > 160 * 1024:
+            # (split 2 -- blocks 1-2 as two column bands, 5+5 waves with hs 2 -- measured
+            # 86-92 us vs 65-69 us for the full-width band: profiles/r3_negative_results.txt)
+            for split in (1,):
+                if not FB.band_supported(s.cin, hid, s.cout, s.stride, s.dilation, OW, split):
                     continue
-                for R in self._band_rows(B, OH, OW, s.stride):
-                    variants.insert(0, (f"band{R}s{nslot}", [
-                        lambda *_, x=inp, out=out, h=h, w=w, R=R, nslot=nslot, bp_=bp_: FB.fused_ir_band(
-                            x, bp_, out, B=B, IH=h, IW=w, stride=s.stride, residual=s.residual, R=R,
-                            nslot=nslot)]))
+                for hs in ((1, 2) if FB.band_waves(OW, split) <= 8 else (1,)):
+                    for nslot in (2, 1):
+                        if FB.band_lds(bp_, s.stride, OW, nslot, hs, split) > 160 * 1024:
+                            continue
+                        for R in self._band_rows(B, OH, OW, s.stride):
+                            tag = f"band{R}s{nslot}" + ("h" if hs == 2 else "") + ("c" if split == 2 else "")
+                            variants.insert(0, (tag, [
+                                lambda *_, x=inp, out=out, h=h, w=w, R=R, nslot=nslot, bp_=bp_, hs=hs,
+                                split=split: FB.fused_ir_band(x, bp_, out, B=B, IH=h, IW=w, stride=s.stride,
+                                                              residual=s.residual, R=R, nslot=nslot, hs=hs,
+                                                              split=split)]))
         outer_ops.append(Choice(f"block{i}", variants))
         return out, OH, OW, s.cout
 

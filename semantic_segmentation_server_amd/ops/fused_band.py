@@ -31,14 +31,22 @@ import torch
 
 # (stride, hidP / 16, ceil(Cout / 16), waves = ceil(OW / 16)) instantiated in
 # fused_ir_band.hip: blocks 1-6 at 513^2 (output widths 129, 129, 65, 65, 65, 33)
-BAND_SHAPES = {(2, 6, 2, 9), (1, 10, 2, 9), (2, 10, 2, 5), (1, 12, 2, 5), (2, 12, 4, 3)}
+BAND_SHAPES = {(2, 6, 2, 9), (1, 10, 2, 9), (2, 10, 2, 5), (1, 12, 2, 5), (2, 12, 4, 3),
+               (2, 6, 2, 5), (1, 10, 2, 5)}  # the last two: blocks 1-2 as two column bands
 
 
-def band_supported(cin: int, hid: int, cout: int, stride: int, dil: int, OW: int) -> bool:
-    """A band spans the full output width OW (ceil(OW / 16) waves of 16 columns)."""
+def band_waves(OW: int, split: int = 1) -> int:
+    """Column waves of one band: ceil(OW / 16), or for split = 2 those of ceil(OW / 2)."""
+    return -(-(-(-OW // 2) if split == 2 else OW) // 16)
+
+
+def band_supported(cin: int, hid: int, cout: int, stride: int, dil: int, OW: int,
+                   split: int = 1) -> bool:
+    """A band spans the full output width OW (ceil(OW / 16) waves of 16 columns), or half
+    of it (split = 2)."""
     hidP = -(-hid // 32) * 32
     return (dil == 1 and cin <= 32 and cin % 8 == 0 and stride in (1, 2)
-            and (stride, hidP // 16, -(-cout // 16), -(-OW // 16)) in BAND_SHAPES)
+            and (stride, hidP // 16, -(-cout // 16), band_waves(OW, split)) in BAND_SHAPES)
 
 
 def _al(n: int) -> int:
@@ -86,32 +94,38 @@ def pack_fused_band(we: torch.Tensor, be: torch.Tensor, wd: torch.Tensor, bd: to
                 o_bd=offs[3], o_wp=offs[4], o_bp=offs[5], blob_bytes=o)
 
 
-def band_lds(packed: Dict, stride: int, OW: int, nslot: int) -> int:
+def band_lds(packed: Dict, stride: int, OW: int, nslot: int, hs: int = 1, split: int = 1) -> int:
     from .hip_ops import _hip_mod
-    return int(_hip_mod().fused_ir_band_lds(stride, packed["hidP"], OW, packed["blob_bytes"], nslot))
+    return int(_hip_mod().fused_ir_band_lds(stride, packed["hidP"], OW, packed["blob_bytes"], nslot,
+                                            hs, packed["Cout"], split))
 
 
 def fused_ir_band(x: torch.Tensor, packed: Dict, out: torch.Tensor, *, B: int, IH: int, IW: int,
-                  stride: int, residual: bool, R: int = 8, nslot: int = 2) -> torch.Tensor:
-    """Launch fused_ir_band_kernel. x [B, IH, IW, Cin] bf16 -> out [B, OH, OW, Cout] bf16."""
+                  stride: int, residual: bool, R: int = 8, nslot: int = 2, hs: int = 1,
+                  split: int = 1) -> torch.Tensor:
+    """Launch fused_ir_band_kernel. x [B, IH, IW, Cin] bf16 -> out [B, OH, OW, Cout] bf16.
+    ``hs = 2``: two waves per 16-column group, each owning half of the hidden channels
+    (twice the waves per CU at the same LDS, plus a small partial-sum exchange)."""
     from .hip_ops import _chk, _dbg, _hip_mod, _ptr, _stream
     Cin, Cout = packed["Cin"], packed["Cout"]
     OH, OW = (IH - 1) // stride + 1, (IW - 1) // stride + 1
     if residual and (stride != 1 or Cin != Cout):
         raise ValueError("fused_ir_band: residual needs stride 1 and Cin == Cout")
-    if nslot not in (1, 2) or R < 1:
-        raise ValueError("fused_ir_band: nslot 1 or 2, R >= 1")
-    if not band_supported(Cin, packed["hid"], Cout, stride, 1, OW):
+    if nslot not in (1, 2) or R < 1 or hs not in (1, 2) or split not in (1, 2):
+        raise ValueError("fused_ir_band: nslot 1 or 2, R >= 1, hs 1 or 2, split 1 or 2")
+    if hs == 2 and band_waves(OW, split) > 8:
+        raise ValueError("fused_ir_band: hs 2 needs <= 8 column waves (use split 2)")
+    if not band_supported(Cin, packed["hid"], Cout, stride, 1, OW, split):
         raise ValueError("fused_ir_band: no instantiation for this block")
     _chk(x, torch.bfloat16, "x", B * IH * IW * Cin)
     _chk(out, torch.bfloat16, "out", B * OH * OW * Cout)
     _chk(packed["blob"], torch.uint8, "blob", packed["blob_bytes"])
-    if band_lds(packed, stride, OW, nslot) > 160 * 1024:
+    if band_lds(packed, stride, OW, nslot, hs, split) > 160 * 1024:
         raise ValueError("fused_ir_band: LDS over 160 KiB")
     _hip_mod().fused_ir_band(_ptr(x), _ptr(packed["blob"]), _ptr(out), B, IH, IW, Cin, OH, OW, Cout,
                              packed["hidP"], stride, int(bool(residual)), R, nslot,
                              packed["blob_bytes"], packed["o_be"], packed["o_wd"], packed["o_bd"],
-                             packed["o_wp"], packed["o_bp"], _stream())
+                             packed["o_wp"], packed["o_bp"], _stream(), hs, split)
     _dbg("fused_ir_band")
     return out
 

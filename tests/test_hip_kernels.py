@@ -1282,16 +1282,24 @@ def test_fused_ir_band(cin, cout, stride, H, W, R, nslot):
         pytest.skip("LDS")
     assert FB.band_supported(cin, spec.hidden, cout, stride, 1, (W - 1) // stride + 1)
     OH, OW = (H - 1) // stride + 1, (W - 1) // stride + 1
-    out = torch.full((B, OH, OW, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
-    FB.fused_ir_band(_nhwc(x).to(DEV), packed, out, B=B, IH=H, IW=W, stride=stride,
-                     residual=spec.residual, R=R, nslot=nslot)
-    torch.cuda.synchronize()
-    assert torch.isfinite(out).all()
-    assert _rel(_nchw(out).cpu(), ref) < 2e-2
-    if H * W <= 129 * 129:
-        emu = FB.emulate_fused_band(_nhwc(x).float().numpy(), packed, stride=stride,
-                                    residual=spec.residual)
-        assert _rel(out.cpu().float(), torch.from_numpy(emu)) < 5e-3
+    emu = None
+    # hs 2: two waves per column group; split 2: two column bands (blocks 1-2)
+    cfgs = [(hs, sp) for sp in (1, 2) for hs in (1, 2)
+            if FB.band_supported(cin, spec.hidden, cout, stride, 1, OW, sp) and FB.band_waves(OW, sp) <= (8 if hs == 2 else 99)]
+    for hs, sp in cfgs:
+        if FB.band_lds(packed, stride, OW, nslot, hs, sp) > 160 * 1024:
+            continue
+        out = torch.full((B, OH, OW, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
+        FB.fused_ir_band(_nhwc(x).to(DEV), packed, out, B=B, IH=H, IW=W, stride=stride,
+                         residual=spec.residual, R=R, nslot=nslot, hs=hs, split=sp)
+        torch.cuda.synchronize()
+        assert torch.isfinite(out).all(), (hs, sp)
+        assert _rel(_nchw(out).cpu(), ref) < 2e-2, (hs, sp)
+        if H * W <= 129 * 129:
+            if emu is None:
+                emu = FB.emulate_fused_band(_nhwc(x).float().numpy(), packed, stride=stride,
+                                            residual=spec.residual)
+            assert _rel(out.cpu().float(), torch.from_numpy(emu)) < 5e-3, (hs, sp)
 
 
 def test_multistream_batched_step_tags_streams():
