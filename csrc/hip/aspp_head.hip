@@ -35,8 +35,6 @@ namespace ssa {
 
 namespace {
 
-constexpr int kHW = 8;           // waves per workgroup
-constexpr int kHT = kHW * 64;    // threads
 constexpr int kKC = 2;           // 32-deep k-steps per chunk (64 channels)
 constexpr int kTP = 264;         // projection tile pitch (bf16 elements, 528 B)
 constexpr int kNP = 256;         // projection channels
@@ -49,8 +47,12 @@ struct HeadArgs {
 
 __device__ __forceinline__ int frag_slot(int lane, int kk) { return lane ^ (((lane >> 4) * 2 + kk * 8) & 15); }
 
-template <int G, int KS>
-__global__ __launch_bounds__(kHT) void aspp_head_kernel(HeadArgs a) {
+// NWH = 16 (round 3): one projection subtile per wave, twice the waves per CU to cover the
+// staging / LDS latency (the grouped ASPP GEMM gained 20 % from the same change)
+template <int G, int KS, int NWH>
+__global__ __launch_bounds__(NWH * 64) void aspp_head_kernel(HeadArgs a) {
+  constexpr int kHW = NWH, kHT = NWH * 64;
+  constexpr int NSUB = 16 / NWH;                  // projection subtiles per wave
   constexpr int NCH = KS / kKC;
   constexpr int SLOT = G * kKC * 1024;
   constexpr int NPC = G * 16 * 8;                 // 16-byte staging pieces per chunk
@@ -91,19 +93,21 @@ __global__ __launch_bounds__(kHT) void aspp_head_kernel(HeadArgs a) {
       *reinterpret_cast<bf16x8*>(smem + off) = stg[s][q];
     }
   };
-  // ---- this wave's projection weights: subtiles n = 2*wid + {0, 1}, [n][k][lane][8]
-  bf16x8 afr[3][kKC][2];
-  const bf16* wpw = a.wp + ((size_t)(2 * wid) * KS * 64 + lane) * 8;
+  // ---- this wave's projection weights: subtiles n = NSUB*wid + {0 .. NSUB-1}, [n][k][lane][8]
+  bf16x8 afr[3][kKC][NSUB];
+  const bf16* wpw = a.wp + ((size_t)(NSUB * wid) * KS * 64 + lane) * 8;
   auto a_load = [&](int c, int s) {
 #pragma unroll
     for (int kk = 0; kk < kKC; ++kk)
 #pragma unroll
-      for (int n = 0; n < 2; ++n) afr[s][kk][n] = ld8(wpw + ((size_t)n * KS + c * kKC + kk) * 512);
+      for (int n = 0; n < NSUB; ++n) afr[s][kk][n] = ld8(wpw + ((size_t)n * KS + c * kKC + kk) * 512);
   };
 
-  f32x4 acc[G][2];
+  f32x4 acc[G][NSUB];
 #pragma unroll
-  for (int g = 0; g < G; ++g) acc[g][0] = acc[g][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int n = 0; n < NSUB; ++n) acc[g][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   stage_load(0, 0);
   a_load(0, 0);
@@ -130,10 +134,10 @@ __global__ __launch_bounds__(kHT) void aspp_head_kernel(HeadArgs a) {
 #pragma unroll
       for (int g = 0; g < G; ++g) b[g] = *reinterpret_cast<const bf16x8*>(sl + (g * kKC + kk) * 1024 + fs);
 #pragma unroll
-      for (int g = 0; g < G; ++g) {
-        acc[g][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[c % 3][kk][0], b[g], acc[g][0], 0, 0, 0);
-        acc[g][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[c % 3][kk][1], b[g], acc[g][1], 0, 0, 0);
-      }
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int n = 0; n < NSUB; ++n)
+          acc[g][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[c % 3][kk][n], b[g], acc[g][n], 0, 0, 0);
     }
     // slot (c+1)&1 was last read at step c-1 (behind that step's barrier)
     if (c + 1 < NCH) stage_store((c + 1) & 1, (c + 1) & 1);
@@ -143,8 +147,8 @@ __global__ __launch_bounds__(kHT) void aspp_head_kernel(HeadArgs a) {
   // ---- epilogue 1: projection bias + image bias + ReLU -> bf16 tile in LDS
   bf16* T = reinterpret_cast<bf16*>(smem);
 #pragma unroll
-  for (int n = 0; n < 2; ++n) {
-    const int ch = (2 * wid + n) * 16 + kq * 4;
+  for (int n = 0; n < NSUB; ++n) {
+    const int ch = (NSUB * wid + n) * 16 + kq * 4;
     const f32x4 b4 = *reinterpret_cast<const f32x4*>(a.bp + ch);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -182,18 +186,18 @@ __global__ __launch_bounds__(kHT) void aspp_head_kernel(HeadArgs a) {
   }
 }
 
-template <int G, int KS>
+template <int G, int KS, int NWH>
 void launch_head(const HeadArgs& a, hipStream_t s) {
   const size_t lds = aspp_head_lds(G, KS * 32);
   static bool attr = false;
   if (!attr) {
-    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&aspp_head_kernel<G, KS>),
+    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&aspp_head_kernel<G, KS, NWH>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
           "aspp_head attr");
     attr = true;
   }
   const int grid = cdiv(a.M, G * 16);
-  hipLaunchKernelGGL((aspp_head_kernel<G, KS>), dim3(grid), dim3(kHT), lds, s, a);
+  hipLaunchKernelGGL((aspp_head_kernel<G, KS, NWH>), dim3(grid), dim3(NWH * 64), lds, s, a);
   check_launch("aspp_head");
 }
 
@@ -212,10 +216,11 @@ void aspp_head(const AsppHeadParams& p, hipStream_t s) {
   if ((long long)p.M * p.K >= (1LL << 40)) throw std::invalid_argument("aspp_head: input too large");
   HeadArgs a{p.cat, p.wp, p.bp, p.img_bias, p.wl, p.bl, p.out, p.M, p.HW > 0 ? p.HW : 1, p.ldo};
   const int KS = p.K / 32;
-#define HEAD(G_, KS_)                  \
-  if (p.G == G_ && KS == KS_) {        \
-    launch_head<G_, KS_>(a, s);        \
-    return;                            \
+#define HEAD(G_, KS_)                                              \
+  if (p.G == G_ && KS == KS_) {                                    \
+    if (p.waves == 16) launch_head<G_, KS_, 16>(a, s);             \
+    else launch_head<G_, KS_, 8>(a, s);                            \
+    return;                                                        \
   }
   HEAD(1, 32) HEAD(2, 32) HEAD(3, 32) HEAD(5, 32) HEAD(9, 32)
 #undef HEAD

@@ -174,14 +174,18 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("aspp_head",
         [](uintptr_t cat, uintptr_t wp, uintptr_t bp, uintptr_t img_bias, uintptr_t wl, uintptr_t bl,
-           uintptr_t out, int M, int K, int HW, int ncls, int ldo, int G, uintptr_t stream) {
+           uintptr_t out, int M, int K, int HW, int ncls, int ldo, int G, uintptr_t stream, int waves) {
           AsppHeadParams p;
+          p.waves = waves;
           p.cat = P<const bf16>(cat); p.wp = P<const bf16>(wp); p.bp = P<const float>(bp);
           p.img_bias = P<const float>(img_bias); p.wl = P<const bf16>(wl); p.bl = P<const float>(bl);
           p.out = P<bf16>(out);
           p.M = M; p.K = K; p.HW = HW; p.ncls = ncls; p.ldo = ldo; p.G = G;
           aspp_head(p, S(stream));
-        });
+        },
+        py::arg("cat"), py::arg("wp"), py::arg("bp"), py::arg("img_bias"), py::arg("wl"), py::arg("bl"),
+        py::arg("out"), py::arg("M"), py::arg("K"), py::arg("HW"), py::arg("ncls"), py::arg("ldo"),
+        py::arg("G"), py::arg("stream"), py::arg("waves") = 8);
 
   m.def("dw_project",
         [](uintptr_t hid_in, uintptr_t wd, uintptr_t bd, uintptr_t wp, uintptr_t bp, uintptr_t res,

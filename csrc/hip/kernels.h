@@ -186,6 +186,7 @@ struct AsppHeadParams {
   bf16* out = nullptr;              // [M, ldo] logits (channels >= ncls written as 0 up to ldo)
   int M = 0, K = 0, N = 256, HW = 0, ncls = 0, ldo = 0;
   int G = 9;                        // 16-pixel groups per workgroup (1, 2, 3, 5, 9)
+  int waves = 8;                    // 8 (2 projection subtiles per wave) or 16 (1)
 };
 void aspp_head(const AsppHeadParams& p, hipStream_t s);
 size_t aspp_head_lds(int G, int K);

@@ -417,10 +417,10 @@ class HipDeepLab:
                 self.head = K.pack_aspp_head(self.proj_w, self.proj_b, self.logit_w, self.logit_b, dev)
             Mh = B * h * w
             g0 = K.aspp_head_groups(Mh)
-            head = [(f"head_g{g}", [lambda *_, g=g, h=h, w=w: K.aspp_head(
+            head = [(f"head_g{g}" + ("w" if nw == 16 else ""), [lambda *_, g=g, h=h, w=w, nw=nw: K.aspp_head(
                 cat.view(Mh, self.cat_c), self.head, logits.view(Mh, self.ldk), M=Mh, HW=h * w,
-                ldo=self.ldk, img_bias=img_bias, G=g)]) for g in K.ASPP_HEAD_G
-                if g == g0 or (g < g0 and -(-Mh // (16 * g)) <= 1024)]
+                ldo=self.ldk, img_bias=img_bias, G=g, waves=nw)]) for g in K.ASPP_HEAD_G
+                if g == g0 or (g < g0 and -(-Mh // (16 * g)) <= 1024) for nw in (8, 16)]
             ops.append(Choice("aspp.head", head + [("split", split)]))
         else:
             ops.extend(split)

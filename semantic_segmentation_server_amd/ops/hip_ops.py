@@ -842,12 +842,12 @@ def aspp_head_groups(M: int) -> int:
 
 
 def aspp_head(cat, packed: dict, out, *, M: int, HW: int, ldo: int, img_bias=None,
-              G: Optional[int] = None) -> torch.Tensor:
+              G: Optional[int] = None, waves: int = 8) -> torch.Tensor:
     """Fused ASPP projection (+bias, +per-image bias, ReLU) and logits conv (aspp_head.hip).
     cat: [M, K] bf16; out: [M, ldo] bf16 logits (channels ncls..ldo-1 written as zeros)."""
     K, ncls = packed["K"], packed["ncls"]
     G = aspp_head_groups(M) if G is None else G
-    if G not in ASPP_HEAD_G or K != 1024 or ldo % 4 or not ncls <= ldo <= 32:
+    if G not in ASPP_HEAD_G or K != 1024 or ldo % 4 or not ncls <= ldo <= 32 or waves not in (8, 16):
         raise ValueError(f"aspp_head: unsupported G={G} K={K} ldo={ldo}")
     _chk(cat, torch.bfloat16, "cat", M * K)
     _chk(out, torch.bfloat16, "out", M * ldo)
@@ -861,7 +861,7 @@ def aspp_head(cat, packed: dict, out, *, M: int, HW: int, ldo: int, img_bias=Non
         _chk(img_bias, torch.float32, "img_bias", (M // HW) * 256)
     _hip_mod().aspp_head(_ptr(cat), _ptr(packed["wp"]), _ptr(packed["bp"]), _ptr(img_bias),
                          _ptr(packed["wl"]), _ptr(packed["bl"]), _ptr(out), M, K, HW, ncls, ldo, G,
-                         _stream())
+                         _stream(), waves)
     _dbg('aspp_head')
     return out
 

@@ -1228,7 +1228,8 @@ def test_fused_ir_stream(cin, cout, dil, H, S):
     (3 * 121 + 0, 121, 32, 32, True),        # M tail inside a 16-pixel group, full 32 classes
 ])
 @pytest.mark.parametrize("G", [None, 1, 2, 3, 5, 9])
-def test_aspp_head(M, HW, ncls, ldo, img, G):
+@pytest.mark.parametrize("waves", [8, 16])
+def test_aspp_head(M, HW, ncls, ldo, img, G, waves):
     """Fused ASPP projection + logits vs fp32 torch: relu(cat Wp^T + bp + ib) rounded to
     bf16 (the kernel's on-chip projection tile), then Wl . proj + bl."""
     K = _hip()
@@ -1248,7 +1249,7 @@ def test_aspp_head(M, HW, ncls, ldo, img, G):
     packed = K.pack_aspp_head(wp, bp, wl, bl, device=DEV)
     out = torch.full((M, ldo), float("nan"), dtype=torch.bfloat16, device=DEV)
     K.aspp_head(cat.to(DEV), packed, out, M=M, HW=HW, ldo=ldo,
-                img_bias=None if ib is None else ib.to(DEV), G=G)
+                img_bias=None if ib is None else ib.to(DEV), G=G, waves=waves)
     torch.cuda.synchronize()
     got = out.float().cpu()
     assert torch.isfinite(got).all()
