@@ -553,28 +553,45 @@ __device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char
   const int total = ntap * cch;
 
   int is_tap = 0, is_c = 0;  // issue cursor
-  auto issue = [&](int stage) {
+  // per-tap state of the cursor, recomputed only when it moves to the next tap: the rows'
+  // source offsets (element index of channel 0 for this tap, -1 = padding -> zero page) and
+  // the tap's weight offset. Round 2 recomputed the bounds and offsets for every 64-channel
+  // stage: ~135 VALU + ~155 SALU per wave and stage against 32 MFMAs (PMC of the 16-wave
+  // grouped ASPP tile, profiles/r3_step_pmc.txt)
+  int asrc[GA];
+  int wtap = 0;
+  auto set_tap = [&]() {
     const int t = (int)((tl >> (4 * is_tap)) & 15);
     const int dy = (t / a.KW - a.KH / 2) * a.dil, dx = (t % a.KW - a.KW / 2) * a.dil;
-    const int c = is_c * BK + lc * 8;
-    const bool cok = c < a.Cin;
-    const int doff = (dy * a.IW + dx) * a.Cin + c;
-    char* sA = smem + stage * SB;
+    const int doff = (dy * a.IW + dx) * a.Cin;
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
       const int iy = ay[i] + dy, ix = ax[i] + dx;
-      const bool ok = av[i] && cok && iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW;
-      const void* src = ok ? (const void*)(a.in + aoff[i] + doff) : (const void*)g_zero_page;
+      const bool ok = av[i] && iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW;
+      asrc[i] = ok ? aoff[i] + doff : -1;
+    }
+    wtap = t * a.Cin;
+  };
+  if (ntap > 0) set_tap();
+  auto issue = [&](int stage) {
+    const int c = is_c * BK + lc * 8;
+    const bool cok = c < a.Cin;
+    char* sA = smem + stage * SB;
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      const void* src = (asrc[i] >= 0 && cok) ? (const void*)(a.in + asrc[i] + c) : (const void*)g_zero_page;
       __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(sA + (wid * (BM / NW) + i * RPG) * ROWB), 16, 0, 0);
     }
     char* sB = sA + BM * ROWB;
-    const int wofs = t * a.Cin + c;
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
-      const void* src = (bv[j] && cok) ? (const void*)(a.w + boff[j] + wofs) : (const void*)g_zero_page;
+      const void* src = (bv[j] && cok) ? (const void*)(a.w + boff[j] + wtap + c) : (const void*)g_zero_page;
       __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(sB + (wid * (BN / NW) + j * RPG) * ROWB), 16, 0, 0);
     }
-    if (++is_c == cch) { is_c = 0; ++is_tap; }
+    if (++is_c == cch) {
+      is_c = 0;
+      if (++is_tap < ntap) set_tap();
+    }
   };
 
   f32x4 acc[MT][NT];

@@ -15,5 +15,5 @@ for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_VMEM_RD S
   SSA_SLOT_PARALLEL=0 timeout -s KILL 180 rocprofv3 --pmc $set -d $REPO/$O/p$i -o run --output-format csv -- python3 $REPO/bench.py --steps 3 --warmup 1 --lag 1 --rpc 0 > $REPO/$O/p$i.log 2>&1 || { echo "set $i failed rc=$?"; tail -5 $REPO/$O/p$i.log; exit 1; }
 done
 cd $REPO
-python3 scripts/pmc_summary.py $O > $O/summary.txt 2>&1 || true
+python3 scripts/pmc_summary.py $O/p1 $O/p2 $O/p3 > $O/summary.txt 2>&1 || true
 head -60 $O/summary.txt
