@@ -8,22 +8,21 @@
 // tests check these kernels against it and against the exact host tracer.
 //
 // Pipeline (fixed launch sequence, no host round trip, hipGraph-capturable):
-//   k_ccl_local  per 32x8 tile: palette -> 3x3 box blur (REFLECT_101, rounded) ->
+//   k_ccl_local  per 32x32 tile: palette -> 3x3 box blur (REFLECT_101, rounded) ->
 //                BGR2GRAY on RGB (fixed point) -> > thr, then union-find in LDS:
-//                foreground 8-connected, background 4-connected
-//   k_ccl_boundary  global union-find (atomicMin, Playne-Hawick style) only
-//                across tile edges; image-border background joins the virtual
-//                "outside" node 0
-//   k_compress   label = root with path halving (root = raster index of the
-//                component's first pixel + 1, 0 = outside)
-//                (component roots: zero accumulators)
-//   k_quads      per 2x2 quad: polygon pieces (full square / triangle) as exact
-//                integer moments a00 = 2A, a10 = 6*int x, a01 = 6*int y
-//   k_tree       subtree sums: every component adds its own pieces to all its
-//                ancestors
-//   k_select     contours whose polygon area >= min_area get a record slot
-//   k_hist       class histogram of each selected contour's fill (component +
-//                everything it encloses; holes also get the parent's ring pixels)
+//                foreground 8-connected, background 4-connected; zeroes the counters
+//   k_ccl_edges  cross-tile unions as pairs of tile-local roots
+//   k_ccl_merge  one workgroup per frame: union-find over those pairs in LDS (or, for
+//                frames past its caps, a global union-find across the tile edges);
+//                image-border background joins the virtual "outside" node 0; final
+//                labels of the tile-local roots (component root = raster index of its
+//                first pixel + 1, 0 = outside); roots zero their accumulators
+//   k_accum      per pixel: its 2x2 quad's polygon pieces as exact integer moments
+//                (a00 = 2A, a10 = 6*int x, a01 = 6*int y) and its class into the fill
+//                histograms (component + everything it encloses; holes also get the
+//                parent's ring pixels), strip-privatised in LDS and added to every
+//                ancestor in the border tree at flush time (subtree sums)
+//   k_assign     contours whose polygon area >= min_area get a record slot
 //   k_finalize   majority label, score, centroid (OpenCV's double arithmetic),
 //                normalisation, records in findContours pre-order
 #include "common.h"
@@ -37,36 +36,37 @@ namespace {
 struct FrameWS {
   int32_t* L;          // [N + 1] union-find labels (index 0 = outside)
   uint8_t* mask;       // [N] 1 = foreground
-  int32_t* parent;     // [N] per root index: parent node id (0 = frame/outside)
   int32_t* slot;       // [N] per root index: record slot or -1
-  int32_t* a00;        // [N] own 2*area
-  int32_t* t00;        // [N] subtree 2*area
-  long long* a10;      // [N]
-  long long* a01;      // [N]
-  long long* t10;      // [N]
-  long long* t01;      // [N]
-  int32_t* hist;       // [K][bins]
-  int32_t* nslot;      // [0] selected, [1] contours dropped (> K passed), [2] cross-tile edges, [3] selected holes
+  int32_t* t00;        // [N] per root index: subtree 2*area
+  long long* t10;      // [N] subtree 6 * int x
+  long long* t01;      // [N] subtree 6 * int y
+  int32_t* th;         // [N][bins] per root index: class histogram of the contour's fill
+  int32_t* nslot;      // [0] selected, [1] contours dropped (> K passed), [2] cross-tile edges, [3] roots
   int32_t* slot_node;  // [K]
-  int32_t* cidx;       // [N] per tile-local root pixel: its index among the tile's roots
+  int32_t* cidx;       // [N] per tile-local root pixel: its index among the tile's roots,
+                       //     after k_ccl_merge its final label
   int32_t* rootpix;    // [ntiles][kTileRoots] raster index of each tile-local root
   int32_t* ntroot;     // [ntiles] tile-local roots per tile
-  int32_t* toff;       // [ntiles] compact-id offset of each tile (merge kernel)
-  int32_t* clabel;     // [kMergeCap] final label of each compact node
   int32_t* flag;       // [4]: [0] = 1 -> frame took the global union-find fallback
   int32_t* edges;      // [kEdgeCap][2] cross-tile unions (tile-local root pairs, -1 = outside)
-  int32_t* bcnt;       // [ceil(N / 256)] passing contours per k_select block (raster order)
+  int32_t* rlist;      // [N] raster indices of the component roots (nslot[3] of them, any order)
+  int fb;              // (kernels after k_ccl_merge) flag[0]: L holds final labels
 };
 
-constexpr int TW = 32, TH = 32;     // local CCL tile
+#ifndef SSA_CCL_TH
+#define SSA_CCL_TH 32
+#endif
+constexpr int TW = 32, TH = SSA_CCL_TH;  // local CCL tile
 constexpr int kTileRoots = TW * TH;  // worst case roots per tile
 constexpr int kMergeCap = 12288;     // compact nodes the per-frame LDS merge handles
 constexpr int kEdgeCap = 1 << 16;    // cross-tile union pairs per frame
 
-// Workspace layout: per frame, fixed stride; counters/hists first (memset region).
+// Workspace layout: per frame, fixed stride; counters first (zeroed by k_ccl_local).
+// The per-root arrays are indexed by the root's raster index (no cap on the number of
+// components); only roots' entries are ever written or read, and k_ccl_merge zeroes them.
 struct Layout {
   size_t N, K, bins, ntiles;
-  size_t small_bytes;  // nslot(16) + hist + slot_node, per frame (zeroed every call)
+  size_t small_bytes;  // nslot(16) + slot_node, per frame (zeroed every call)
   size_t big_bytes;    // per frame
   size_t total(int B) const { return (small_bytes + big_bytes) * (size_t)B; }
 };
@@ -79,10 +79,9 @@ Layout layout(int H, int W, int K, int bins) {
   l.K = K;
   l.bins = bins;
   l.ntiles = (size_t)((W + TW - 1) / TW) * ((H + TH - 1) / TH);
-  l.small_bytes = al(16 + (size_t)K * bins * 4 + (size_t)K * 4);
-  l.big_bytes = al((l.N + 1) * 4) + al(l.N) + 4 * al(l.N * 4) + 4 * al(l.N * 8) + al(l.N * 4) +
-                al(l.ntiles * kTileRoots * 4) + 2 * al(l.ntiles * 4) + al(kMergeCap * 4) + al(16) +
-                al((size_t)kEdgeCap * 8) + al((l.N + 255) / 256 * 4);
+  l.small_bytes = al(16 + (size_t)K * 4);
+  l.big_bytes = al((l.N + 1) * 4) + al(l.N) + 2 * al(l.N * 4) + 2 * al(l.N * 8) + al(l.N * bins * 4) +
+                al(l.N * 4) + al(l.ntiles * kTileRoots * 4) + al(l.ntiles * 4) + al(16) + al((size_t)kEdgeCap * 8) + al(l.N * 4);
   return l;
 }
 
@@ -90,27 +89,22 @@ __host__ __device__ inline FrameWS frame_ws(char* ws, const Layout& l, int B, in
   FrameWS f;
   char* s = ws + (size_t)b * l.small_bytes;
   f.nslot = reinterpret_cast<int32_t*>(s);
-  f.hist = reinterpret_cast<int32_t*>(s + 16);
-  f.slot_node = reinterpret_cast<int32_t*>(s + 16 + l.K * l.bins * 4);
+  f.slot_node = reinterpret_cast<int32_t*>(s + 16);
   char* p = ws + (size_t)B * l.small_bytes + (size_t)b * l.big_bytes;
   f.L = reinterpret_cast<int32_t*>(p); p += al((l.N + 1) * 4);
   f.mask = reinterpret_cast<uint8_t*>(p); p += al(l.N);
-  f.parent = reinterpret_cast<int32_t*>(p); p += al(l.N * 4);
   f.slot = reinterpret_cast<int32_t*>(p); p += al(l.N * 4);
-  f.a00 = reinterpret_cast<int32_t*>(p); p += al(l.N * 4);
   f.t00 = reinterpret_cast<int32_t*>(p); p += al(l.N * 4);
-  f.a10 = reinterpret_cast<long long*>(p); p += al(l.N * 8);
-  f.a01 = reinterpret_cast<long long*>(p); p += al(l.N * 8);
   f.t10 = reinterpret_cast<long long*>(p); p += al(l.N * 8);
   f.t01 = reinterpret_cast<long long*>(p); p += al(l.N * 8);
+  f.th = reinterpret_cast<int32_t*>(p); p += al(l.N * l.bins * 4);
   f.cidx = reinterpret_cast<int32_t*>(p); p += al(l.N * 4);
   f.rootpix = reinterpret_cast<int32_t*>(p); p += al(l.ntiles * kTileRoots * 4);
   f.ntroot = reinterpret_cast<int32_t*>(p); p += al(l.ntiles * 4);
-  f.toff = reinterpret_cast<int32_t*>(p); p += al(l.ntiles * 4);
-  f.clabel = reinterpret_cast<int32_t*>(p); p += al(kMergeCap * 4);
   f.flag = reinterpret_cast<int32_t*>(p); p += al(16);
   f.edges = reinterpret_cast<int32_t*>(p); p += al((size_t)kEdgeCap * 8);
-  f.bcnt = reinterpret_cast<int32_t*>(p); p += al((l.N + 255) / 256 * 4);
+  f.rlist = reinterpret_cast<int32_t*>(p); p += al(l.N * 4);
+  f.fb = 0;
   return f;
 }
 
@@ -245,6 +239,12 @@ __global__ __launch_bounds__(kCclThreads) void k_ccl_local(KArgs a, const int32_
   const int x = x0 + tx;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
   if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) f.L[0] = 0;
+  {  // the frame's tiles zero its counters (round 2 spent a k_zero launch on this)
+    uint4* z = reinterpret_cast<uint4*>(a.ws + (size_t)b * a.lay.small_bytes);
+    const int words = (int)(a.lay.small_bytes / 16), nt = gridDim.x * gridDim.y;
+    for (int i = (blockIdx.y * gridDim.x + blockIdx.x) * kCclThreads + tid; i < words; i += nt * kCclThreads)
+      z[i] = make_uint4(0, 0, 0, 0);
+  }
   const uint8_t* lab = a.labels + (size_t)b * a.H * a.W;
   for (int i = tid; i < HH2 * HW2; i += kCclThreads) {
     const int yy = clampi(reflect101(y0 - 1 + i / HW2, a.ch), 0, a.ch - 1);
@@ -346,11 +346,16 @@ __global__ __launch_bounds__(kCclThreads) void k_ccl_local(KArgs a, const int32_
 //   per wave.
 // k_ccl_merge: ONE workgroup per frame numbers the tile-local roots (a few per
 //   tile on real masks) compactly, runs union-find over the pair list on LDS
-//   atomics, and maps every compact node to its component's final label (min
-//   raster index + 1, outside-connected background -> 0).
-// The pre-existing global union-find (k_ccl_boundary: device-coherent pointer
-// chasing from every CU, serialised on the roots of big components) remains the
-// fallback for frames that overflow kMergeCap roots or kEdgeCap pairs.
+//   atomics, writes every tile-local root's final label (min raster index + 1,
+//   outside-connected background -> 0) over its cidx entry, zeroes the accumulators
+//   of every component root and lists the roots. Pixels are resolved on the fly
+//   afterwards (fin(): L -> tile-local root -> cidx): no full-frame relabelling pass
+//   (round 2's k_compress, 22 us per 32 frames).
+// Frames past kMergeCap roots or kEdgeCap pairs take the global union-find (device-
+// coherent pointer chasing) across the tile edges and a relabelling pass instead, both
+// run by the merge workgroup; fin() then reads the final label straight from L. (Round
+// 2 launched that fallback as its own full-grid kernel: 5-8 us per 32 frames that
+// almost never need it.)
 __device__ __forceinline__ void emit_pairs(FrameWS& f, int n, const int (&pa)[3], const int (&pb)[3]) {
   // wave-aggregated append of this lane's n pairs
   int incl = n;
@@ -459,17 +464,32 @@ __global__ __launch_bounds__(256) void k_ccl_edges(KArgs a) {
   emit_pairs(f, keep, pa, pb);
 }
 
+__device__ __forceinline__ void ccl_boundary_pixel(KArgs& a, FrameWS& f, int p);
+
+__device__ __forceinline__ void add_root(FrameWS& f, int bins, int p, int* s_nr) {
+  f.slot[p] = -1;
+  f.t00[p] = 0;
+  f.t10[p] = 0;
+  f.t01[p] = 0;
+  int* h = f.th + (size_t)p * bins;
+  for (int c = 0; c < bins; ++c) h[c] = 0;
+  f.rlist[atomicAdd(s_nr, 1)] = p;
+}
+
 __global__ __launch_bounds__(1024) void k_ccl_merge(KArgs a) {
   extern __shared__ int sm[];
   const int b = blockIdx.x;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
-  const int tx_n = (a.cw + TW - 1) / TW, ty_n = (a.ch + TH - 1) / TH;
+  const int cw = a.cw, ch = a.ch;
+  const int tx_n = (cw + TW - 1) / TW, ty_n = (ch + TH - 1) / TH;
   const int nt = tx_n * ty_n;
   const int tid = threadIdx.x;
   int* toff = sm;                   // [nt + 1]
   int* part = sm + nt + 1;          // [1024] scan partials
   int* par = part + 1024;           // [kMergeCap + 1] (last = outside)
   int* minr = par + kMergeCap + 1;  // [kMergeCap + 1]
+  int* s_nr = minr + kMergeCap + 1; // [1] roots listed
+  if (tid == 0) *s_nr = 0;
   // exclusive scan of the per-tile root counts
   const int per = (nt + 1023) / 1024;
   const int t0 = tid * per, t1 = min(nt, t0 + per);
@@ -492,17 +512,33 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(KArgs a) {
   __syncthreads();
   const int R = toff[nt];
   const int E = f.nslot[2];
+  const int N = ch * cw;
   if (tid == 0) f.flag[0] = (R > kMergeCap || E > kEdgeCap) ? 1 : 0;
-  if (R > kMergeCap || E > kEdgeCap) return;  // fallback: k_ccl_boundary + k_compress
+  if (R > kMergeCap || E > kEdgeCap) {
+    for (int p = tid; p < N; p += 1024) ccl_boundary_pixel(a, f, p);
+    __threadfence();
+    __syncthreads();
+    // Read-only traversal: a path-halving store here could overwrite another thread's
+    // final root store with a stale grandparent (observed: 1 pixel in ~1M left pointing
+    // at a non-root). Every concurrent store below writes a root, so plain traversal
+    // always terminates at the true root.
+    for (int p = tid; p < N; p += 1024) {
+      const int r = find_root(f.L, p + 1);
+      __hip_atomic_store(f.L + p + 1, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (r == p + 1) add_root(f, a.bins, p, s_nr);
+    }
+    __syncthreads();
+    if (tid == 0) f.nslot[3] = *s_nr;
+    return;
+  }
   const int OUT = R;
   for (int i = tid; i <= R; i += 1024) {
     par[i] = i;
     minr[i] = 0x7fffffff;
   }
-  for (int t = tid; t < nt; t += 1024) f.toff[t] = toff[t];
   __syncthreads();
   auto compact = [&](int r) {
-    const int ly = r / a.cw, lx = r - ly * a.cw;
+    const int ly = r / cw, lx = r - ly * cw;
     return toff[(ly / TH) * tx_n + lx / TW] + f.cidx[r];
   };
   for (int e = tid; e < E; e += 1024) {
@@ -517,28 +553,23 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(KArgs a) {
   }
   __syncthreads();
   const int outroot = lfind(par, OUT);
-  for (int i = tid; i < R; i += 1024) {
-    const int r = lfind(par, i);
-    f.clabel[i] = r == outroot ? 0 : minr[r] + 1;
+  // every set but the outside one is a component: its minimum pixel is the root
+  for (int i = tid; i < R; i += 1024)
+    if (i != outroot && lds_ld(par + i) == i) add_root(f, a.bins, minr[i], s_nr);
+  // final label of every tile-local root, over its cidx entry (compact() is done)
+  for (int t = tid; t < nt; t += 1024) {
+    const int n = f.ntroot[t];
+    for (int c = 0; c < n; ++c) {
+      const int r = lfind(par, toff[t] + c);
+      f.cidx[f.rootpix[(size_t)t * kTileRoots + c]] = r == outroot ? 0 : minr[r] + 1;
+    }
   }
+  __syncthreads();
+  if (tid == 0) f.nslot[3] = *s_nr;
 }
 
-// Cross-tile merges (and image-border background -> outside node 0). Only
-// pixels on a tile's left column / top row or on the image border do work.
-// Launched with a small grid per frame (grid-stride over the pixels): frames the LDS
-// merge handled (nearly all) leave after ONE flag load per workgroup instead of a
-// full-frame grid of early-exiting threads (18 us per 32 frames in round 1).
-__device__ __forceinline__ void ccl_boundary_pixel(KArgs& a, FrameWS& f, int p);
-
-__global__ __launch_bounds__(256) void k_ccl_boundary(KArgs a) {
-  const int b = blockIdx.y;
-  const int N = a.ch * a.cw;
-  FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
-  if (f.flag[0] == 0) return;  // merged in LDS
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < N; p += gridDim.x * blockDim.x)
-    ccl_boundary_pixel(a, f, p);
-}
-
+// Cross-tile merges (and image-border background -> outside node 0) of the fallback
+// path: only pixels on a tile's left column / top row or on the image border do work.
 __device__ __forceinline__ void ccl_boundary_pixel(KArgs& a, FrameWS& f, int p) {
   const int y = p / a.cw, x = p - y * a.cw;
   const bool left = x > 0 && (x % TW) == 0;
@@ -590,40 +621,16 @@ __device__ __forceinline__ void ccl_boundary_pixel(KArgs& a, FrameWS& f, int p) 
   }
 }
 
-__global__ __launch_bounds__(256) void k_compress(KArgs a) {
-  const int b = blockIdx.y;
-  const int N = a.ch * a.cw;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= N) return;
-  FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
-  int r;
-  if (f.flag[0] == 0) {  // compact merge: pixel -> its tile-local root -> final label
-    const int lr = f.L[p + 1] - 1;
-    const int ly = lr / a.cw, lx = lr - ly * a.cw;
-    const int tx_n = (a.cw + TW - 1) / TW;
-    const int t = (ly / TH) * tx_n + lx / TW;
-    r = f.clabel[f.toff[t] + f.cidx[lr]];
-    f.L[p + 1] = r;
-  } else {
-    // Read-only traversal: a path-halving store here could overwrite another
-    // thread's final root store with a stale grandparent (observed: 1 pixel in ~1M
-    // left pointing at a non-root). Every concurrent store below writes a root, so
-    // plain traversal always terminates at the true root.
-    r = find_root(f.L, p + 1);
-    __hip_atomic_store(f.L + p + 1, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // the component's first pixel (its label is its own raster index + 1): zero its
-  // accumulators here (round 1 spent a separate full-frame pass, k_roots, on this;
-  // the parent link needs every final label and is set by k_tree)
-  if (r == p + 1) {
-    f.slot[p] = -1;
-    f.a00[p] = 0;
-    f.t00[p] = 0;
-    f.a10[p] = 0;
-    f.a01[p] = 0;
-    f.t10[p] = 0;
-    f.t01[p] = 0;
-  }
+// Parent of component n in the border tree: the component of the pixel left of its
+// first pixel (0 = the frame at the image border). A pure function of the final labels.
+// Final component label of pixel q (root raster index + 1, 0 = outside).
+__device__ __forceinline__ int fin(const FrameWS& f, int q) {
+  const int l = f.L[q + 1];
+  return f.fb ? l : f.cidx[l - 1];
+}
+
+__device__ __forceinline__ int parent_of(const FrameWS& f, int cw, int n) {
+  return (n - 1) % cw > 0 ? fin(f, n - 2) : 0;
 }
 
 // Per-block privatisation of the component sums. A real scene's mask has a few
@@ -636,8 +643,7 @@ __global__ __launch_bounds__(256) void k_compress(KArgs a) {
 // component is reduced by shuffles first; a full table falls back to global
 // atomics, so correctness never depends on the table size.
 constexpr int kHash = 128;
-constexpr int kQuadBlocks = 256;  // blocks per frame for the strip-privatised quad pass
-constexpr int kHistBlocks = 512;  // blocks per frame for the histogram pass
+constexpr int kQuadBlocks = 256;  // blocks per frame for the strip-privatised accumulation pass
 
 struct QuadTable {
   int key[kHash];
@@ -646,29 +652,60 @@ struct QuadTable {
   unsigned long long s01[kHash];
 };
 
-__device__ __forceinline__ void table_add(QuadTable& T, FrameWS& f, int node, int d00,
+// Subtree sums without a tree pass: every (block, component) partial is added to the
+// component and all its ancestors at flush time (round 2 summed own pieces first and
+// walked the ancestors per root in a separate full-frame pass, k_tree).
+__device__ void moments_up(FrameWS& f, int cw, int node, int d00, long long d10, long long d01) {
+  for (int n = node, depth = 0; n != 0 && depth <= 65536; ++depth, n = parent_of(f, cw, n)) {
+    atomicAdd(f.t00 + n - 1, d00);
+    atomicAdd(reinterpret_cast<unsigned long long*>(f.t10 + n - 1), (unsigned long long)d10);
+    atomicAdd(reinterpret_cast<unsigned long long*>(f.t01 + n - 1), (unsigned long long)d01);
+  }
+}
+
+// Histogram keys: (node * bins + class) * 2 + ring (> 0 for node >= 1; 0 = empty slot).
+// An own-pixel count goes to the node and all its ancestors (a contour's fill is its
+// component plus everything it encloses); a ring count (parent pixels 4-adjacent to a
+// hole, part of the hole contour's fill only) goes to the hole alone.
+__device__ void hist_up(FrameWS& f, int cw, int bins, int key, int cnt) {
+  const int v = key >> 1, node = v / bins, c = v - node * bins;
+  if (key & 1) {
+    atomicAdd(f.th + (size_t)(node - 1) * bins + c, cnt);
+    return;
+  }
+  for (int n = node, depth = 0; n != 0 && depth <= 65536; ++depth, n = parent_of(f, cw, n))
+    atomicAdd(f.th + (size_t)(n - 1) * bins + c, cnt);
+}
+
+constexpr int kHistHash = 256;
+
+struct AccTable {
+  QuadTable q;
+  int hkey[kHistHash];
+  int hcnt[kHistHash];
+};
+
+__device__ __forceinline__ void table_add(AccTable& T, FrameWS& f, int cw, int node, int d00,
                                           long long d10, long long d01) {
   int h = (int)(((unsigned)node * 2654435761u) >> 25) & (kHash - 1);
 #pragma unroll 1
   for (int probe = 0; probe < 16; ++probe, h = (h + 1) & (kHash - 1)) {
-    int k = __hip_atomic_load(&T.key[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    int k = __hip_atomic_load(&T.q.key[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (k == 0) {
-      k = atomicCAS(&T.key[h], 0, node);
+      k = atomicCAS(&T.q.key[h], 0, node);
       if (k == 0) k = node;
     }
     if (k == node) {
-      atomicAdd(&T.s00[h], d00);
-      atomicAdd(&T.s10[h], (unsigned long long)d10);
-      atomicAdd(&T.s01[h], (unsigned long long)d01);
+      atomicAdd(&T.q.s00[h], d00);
+      atomicAdd(&T.q.s10[h], (unsigned long long)d10);
+      atomicAdd(&T.q.s01[h], (unsigned long long)d01);
       return;
     }
   }
-  atomicAdd(f.a00 + node - 1, d00);
-  atomicAdd(reinterpret_cast<unsigned long long*>(f.a10 + node - 1), (unsigned long long)d10);
-  atomicAdd(reinterpret_cast<unsigned long long*>(f.a01 + node - 1), (unsigned long long)d01);
+  moments_up(f, cw, node, d00, d10, d01);
 }
 
-__device__ __forceinline__ void agg_add(QuadTable& T, FrameWS& f, int node, int d00, long long d10,
+__device__ __forceinline__ void agg_add(AccTable& T, FrameWS& f, int cw, int node, int d00, long long d10,
                                         long long d01) {
   const bool active = node > 0;
   const unsigned long long act = __ballot(active);
@@ -676,7 +713,7 @@ __device__ __forceinline__ void agg_add(QuadTable& T, FrameWS& f, int node, int 
   const int leader = __ffsll((long long)act) - 1;
   const int lnode = __shfl(node, leader, 64);
   if (__all(!active || node == lnode)) {
-    // one quad's pieces are < 2^13 (6x + 3, x < 1024), so a 64-lane sum fits in
+    // one quad's pieces are < 2^19 (6x + 3, x < 65536), so a 64-lane sum fits in
     // 32 bits: reduce in int32 (half the cross-lane traffic of the 64-bit sums)
     int s00 = active ? d00 : 0;
     int s10 = active ? (int)d10 : 0, s01 = active ? (int)d01 : 0;
@@ -686,289 +723,262 @@ __device__ __forceinline__ void agg_add(QuadTable& T, FrameWS& f, int node, int 
       s10 += __shfl_xor(s10, o, 64);
       s01 += __shfl_xor(s01, o, 64);
     }
-    if ((int)(threadIdx.x & 63) == leader) table_add(T, f, lnode, s00, s10, s01);
+    if ((int)(threadIdx.x & 63) == leader) table_add(T, f, cw, lnode, s00, s10, s01);
   } else if (active) {
-    table_add(T, f, node, d00, d10, d01);
+    table_add(T, f, cw, node, d00, d10, d01);
   }
 }
 
-// ---------------------------------------------------------------- quads
-// Corner order TL, TR, BL, BR. Triangle of corner k = k + its two quad
-// neighbours; sums of its 3 vertices' coordinates = 3x + TX[k], 3y + TY[k].
-__global__ __launch_bounds__(256) void k_quads(KArgs a) {
-  __shared__ QuadTable T;
-  const int b = blockIdx.y;
-  const int QW = a.cw - 1, QH = a.ch - 1;
-  const int Q = QW > 0 && QH > 0 ? QW * QH : 0;
-  FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
-  for (int i = threadIdx.x; i < kHash; i += 256) {
-    T.key[i] = 0; T.s00[i] = 0; T.s10[i] = 0; T.s01[i] = 0;
-  }
-  __syncthreads();
-  const int per = (Q + gridDim.x - 1) / gridDim.x;
-  const int q0 = blockIdx.x * per, q1 = min(Q, q0 + per);
-  for (int qb = q0; qb < q1; qb += 256) {
-    const int q = qb + threadIdx.x;
-    int fnode = 0, f00 = 0;
-    long long f10 = 0, f01 = 0;
-    int bn[2] = {0, 0}, b00[2] = {0, 0};
-    long long b10[2] = {0, 0}, b01[2] = {0, 0};
-    if (q < q1) {
-      const int y = q / QW, x = q - y * QW;
-      const int p0 = y * a.cw + x;
-      const int idx[4] = {p0, p0 + 1, p0 + a.cw, p0 + a.cw + 1};
-      const int TX[4] = {1, 2, 1, 2}, TY[4] = {1, 1, 2, 2};
-      int node[4];
-      bool fg[4];
-      int nf = 0, missing = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        fg[k] = f.mask[idx[k]] != 0;
-        node[k] = f.L[idx[k] + 1];
-        if (fg[k]) { ++nf; fnode = node[k]; } else { missing = k; }
-      }
-      const long long X = x, Y = y;
-      if (nf == 4) {
-        f00 = 2; f10 = 6 * X + 3; f01 = 6 * Y + 3;
-      } else if (nf == 3) {
-        const int o = 3 - missing;  // triangle of the opposite corner
-        f00 = 1; f10 = 3 * X + TX[o]; f01 = 3 * Y + TY[o];
-      } else {
-        fnode = 0;
-      }
-      int nb = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (fg[k] || node[k] == 0) continue;
-        bool first = true;
-        int cnt = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (!fg[j] && node[j] == node[k]) {
-            ++cnt;
-            if (j < k) first = false;
-          }
-        }
-        if (!first) continue;
-        if (nb < 2) {
-          bn[nb] = node[k];
-          if (cnt >= 2) { b00[nb] = 2; b10[nb] = 6 * X + 3; b01[nb] = 6 * Y + 3; }
-          else { b00[nb] = 1; b10[nb] = 3 * X + TX[k]; b01[nb] = 3 * Y + TY[k]; }
-          ++nb;
-        }
-      }
+__device__ __forceinline__ void htable_add(AccTable& T, FrameWS& f, int cw, int bins, int key, int cnt) {
+  int h = (int)(((unsigned)key * 2654435761u) >> 24) & (kHistHash - 1);
+#pragma unroll 1
+  for (int probe = 0; probe < 16; ++probe, h = (h + 1) & (kHistHash - 1)) {
+    int k = __hip_atomic_load(&T.hkey[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (k == 0) {
+      k = atomicCAS(&T.hkey[h], 0, key);
+      if (k == 0) k = key;
     }
-    agg_add(T, f, fnode, f00, f10, f01);
-    agg_add(T, f, bn[0], b00[0], b10[0], b01[0]);
-    agg_add(T, f, bn[1], b00[1], b10[1], b01[1]);
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < kHash; i += 256) {
-    const int node = T.key[i];
-    if (node == 0) continue;
-    atomicAdd(f.a00 + node - 1, T.s00[i]);
-    atomicAdd(reinterpret_cast<unsigned long long*>(f.a10 + node - 1), T.s10[i]);
-    atomicAdd(reinterpret_cast<unsigned long long*>(f.a01 + node - 1), T.s01[i]);
-  }
-}
-
-// ---------------------------------------------------------------- tree sums
-__global__ __launch_bounds__(256) void k_tree(KArgs a) {
-  const int b = blockIdx.y;
-  const int N = a.ch * a.cw;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= N) return;
-  FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
-  if (f.L[p + 1] != p + 1) return;
-  // parent in the border tree = component of the left neighbour of the first pixel
-  // (0 at the image border); a pure function of the final labels, so the ancestor walk
-  // below evaluates it directly instead of reading links other threads are writing
-  auto parent_of = [&](int n) { return (n - 1) % a.cw > 0 ? f.L[n - 1] : 0; };
-  f.parent[p] = parent_of(p + 1);
-  const int o00 = f.a00[p];
-  const long long o10 = f.a10[p], o01 = f.a01[p];
-  if (o00 == 0 && o10 == 0 && o01 == 0) return;
-  int n = p + 1;
-  for (int depth = 0; n != 0 && depth < 65536; ++depth) {
-    atomicAdd(f.t00 + n - 1, o00);
-    atomicAdd(reinterpret_cast<unsigned long long*>(f.t10 + n - 1), (unsigned long long)o10);
-    atomicAdd(reinterpret_cast<unsigned long long*>(f.t01 + n - 1), (unsigned long long)o01);
-    n = parent_of(n);
-  }
-}
-
-// ---------------------------------------------------------------- select
-// k_select counts, per 256-pixel block, the roots whose contour passes min_area;
-// k_assign (one workgroup per frame) scans those counts and hands the record slots
-// to the first K passing contours in raster order of their discovery pixel. The
-// choice is deterministic (round 1 took them in atomicAdd order, so with more than K
-// passing contours the kept subset changed from run to run) and keeps the
-// smallest discovery keys: among siblings those come LAST in findContours order, so
-// they are the records the reference's LIFO buffer serves first
-// (/root/reference/sem_seg_server.py:186-192, 52-60). Contours past K are counted in
-// nslot[1]; k_finalize flags the frame by a negative record count.
-__device__ __forceinline__ bool passes(const FrameWS& f, const KArgs& a, int p) {
-  if (f.L[p + 1] != p + 1) return false;
-  const int t = f.t00[p];
-  return t != 0 && (double)t * 0.5 >= a.min_area;
-}
-
-__global__ __launch_bounds__(256) void k_select(KArgs a) {
-  const int b = blockIdx.y;
-  const int N = a.ch * a.cw;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
-  const int n = __syncthreads_count(p < N && passes(f, a, p));
-  if (threadIdx.x == 0) f.bcnt[blockIdx.x] = n;
-}
-
-__global__ __launch_bounds__(1024) void k_assign(KArgs a) {
-  __shared__ int s_pre[1024];
-  __shared__ int s_tot;
-  const int b = blockIdx.x, t = threadIdx.x;
-  const int N = a.ch * a.cw;
-  const int nb = (N + 255) / 256;
-  FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
-  // per-thread chunk of consecutive blocks, then an exclusive scan over the threads
-  const int per = (nb + 1023) / 1024;
-  const int b0 = min(nb, t * per), b1 = min(nb, b0 + per);
-  int own = 0;
-  for (int i = b0; i < b1; ++i) own += f.bcnt[i];
-  s_pre[t] = own;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
-    const int v = t >= o ? s_pre[t - o] : 0;
-    __syncthreads();
-    s_pre[t] += v;
-    __syncthreads();
-  }
-  if (t == 1023) s_tot = s_pre[1023];
-  int base = s_pre[t] - own;  // passing contours before this thread's blocks
-  __syncthreads();
-  const int total = s_tot;
-  const int kept = min(total, a.K);
-  // walk this thread's blocks with a non-zero count below the cut; each such block's
-  // 256 pixels are ranked by one 64-lane sweep per 64 pixels (ballot prefix counts).
-  // Blocks are handed to waves: gather (block, base) pairs in LDS first.
-  __shared__ int s_blk[256], s_base[256], s_n;
-  if (t == 0) s_n = 0;
-  __syncthreads();
-  for (int i = b0; i < b1 && base < kept; ++i) {
-    const int c = f.bcnt[i];
-    if (c) {
-      const int k = atomicAdd(&s_n, 1);  // at most K (<= 256) blocks hold kept contours
-      if (k < 256) { s_blk[k] = i; s_base[k] = base; }
-      base += c;
+    if (k == key) {
+      atomicAdd(&T.hcnt[h], cnt);
+      return;
     }
   }
-  __syncthreads();
-  const int nblk = min(s_n, 256);
-  const int wid = t >> 6, lane = t & 63;
-  int holes = 0;
-  for (int k = wid; k < nblk; k += 16) {
-    int r = s_base[k];
-    for (int q = 0; q < 4; ++q) {
-      const int p = s_blk[k] * 256 + q * 64 + lane;
-      const bool ok = p < N && passes(f, a, p);
-      const unsigned long long m = __ballot(ok);
-      const int rank = r + __popcll(m & ((1ull << lane) - 1));
-      if (ok && rank < kept) {
-        f.slot[p] = rank;
-        f.slot_node[rank] = p + 1;
-        holes += f.mask[p] == 0;
-      }
-      r += __popcll(m);
-    }
-  }
-  if (holes) atomicAdd(f.nslot + 3, holes);
-  if (t == 0) {
-    f.nslot[0] = kept;
-    f.nslot[1] = total - kept;
-  }
+  hist_up(f, cw, bins, key, cnt);
 }
 
-// ---------------------------------------------------------------- histograms
-// Same privatisation: the (slot, class) histogram of a frame is tiny (nslot x bins
-// counters, typically 1-3 slots) and every pixel of a selected contour's fill adds
-// to it, so each block of a frame's strip accumulates in LDS (wave-aggregated
-// first) and flushes its non-zero counters once.
-constexpr int kMaxHist = 256 * 32;
-
-// Wave-aggregated histogram add: the wave's lanes are grouped by key (one ballot
-// per distinct key; class maps are blobby, so 64 consecutive pixels carry 1-4
-// distinct (slot, class) keys) and ONE lane per group adds the group's count --
-// instead of up to 64 same-address LDS atomics serialising on a bank.
-__device__ __forceinline__ void hist_add(int* sh, int bins, int slot, int label) {
-  const int key = slot >= 0 ? slot * bins + label : -1;
-  unsigned long long act = __ballot(key >= 0);
+// Wave-aggregated histogram add: the wave's lanes are grouped by key (one ballot per
+// distinct key; class maps are blobby, so 64 consecutive pixels carry 1-4 distinct
+// keys) and ONE lane per group adds the group's count.
+__device__ __forceinline__ void hagg(AccTable& T, FrameWS& f, int cw, int bins, int key) {
+  unsigned long long act = __ballot(key > 0);
   const int me = (int)(threadIdx.x & 63);
   while (act) {  // wave-uniform loop, at most 64 iterations
     const int leader = __ffsll((long long)act) - 1;
     const int lkey = __shfl(key, leader, 64);
     const unsigned long long grp = __ballot(key == lkey) & act;
-    if (me == leader) atomicAdd(sh + lkey, __popcll(grp));
+    if (me == leader) htable_add(T, f, cw, bins, lkey, __popcll(grp));
     act &= ~grp;
   }
 }
 
-__global__ __launch_bounds__(256) void k_hist(KArgs a) {
-  extern __shared__ int sh[];  // [ns * bins]
+// ---------------------------------------------------------------- accumulate
+// One pass over the frame's pixels, strip-privatised per block, producing everything
+// k_select / k_finalize need for every component:
+//  * the 2x2 quad whose top-left corner is the pixel: polygon pieces (full square /
+//    triangle) as exact integer moments a00 = 2A, a10 = 6*int x, a01 = 6*int y
+//    (corner order TL, TR, BL, BR; triangle of corner k = k + its two quad neighbours,
+//    sums of its 3 vertices' coordinates = 3x + TX[k], 3y + TY[k]);
+//  * the pixel's class into its component's fill histogram, and into the ring
+//    histogram of each distinct hole it is 4-adjacent to (holes of its own component).
+// Round 2 ran this as three passes (k_quads, k_tree, k_hist: 92 us per 32 frames).
+__global__ __launch_bounds__(256) void k_accum(KArgs a) {
+  __shared__ AccTable T;
   const int b = blockIdx.y;
-  const int N = a.ch * a.cw;
+  const int cw = a.cw, ch = a.ch, bins = a.bins;
+  const int N = cw * ch;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
-  const int ns = min(*f.nslot, a.K);
-  if (ns == 0) return;  // block-uniform early exit: no contour selected
-  const int nh = ns * a.bins;
-  // ring pixels only exist around selected holes; frames without one (the usual
-  // case: selected contours are blobs) skip the 4-neighbour checks entirely
-  const bool sel_holes = f.nslot[3] > 0 && !(a.dbg & 2);
-  for (int i = threadIdx.x; i < nh; i += 256) sh[i] = 0;
+  f.fb = f.flag[0];
+  for (int i = threadIdx.x; i < kHash; i += 256) {
+    T.q.key[i] = 0; T.q.s00[i] = 0; T.q.s10[i] = 0; T.q.s01[i] = 0;
+  }
+  for (int i = threadIdx.x; i < kHistHash; i += 256) {
+    T.hkey[i] = 0; T.hcnt[i] = 0;
+  }
   __syncthreads();
+  const uint8_t* lab = a.labels + (size_t)b * a.H * a.W;
   const int per = (N + gridDim.x - 1) / gridDim.x;
   const int p0 = blockIdx.x * per, p1 = min(N, p0 + per);
   for (int pb = p0; pb < p1; pb += 256) {
     const int p = pb + threadIdx.x;
-    int label = 0, n = 0, y = 0, x = 0;
-    bool fgp = false;
+    int fnode = 0, f00 = 0;
+    long long f10 = 0, f01 = 0;
+    int bn[2] = {0, 0}, b00[2] = {0, 0};
+    long long b10[2] = {0, 0}, b01[2] = {0, 0};
+    int hkey = 0, rkey[4] = {0, 0, 0, 0};
     if (p < p1) {
-      y = p / a.cw;
-      x = p - y * a.cw;
-      label = a.labels[(size_t)b * a.H * a.W + y * a.W + x];
-      if (label >= a.bins) label = a.bins - 1;
-      n = f.L[p + 1];
-      fgp = f.mask[p] != 0;
-    }
-    // ancestors (inclusive): the fill of every enclosing contour contains p
-    for (int depth = 0; depth <= 65536; ++depth) {
-      if ((a.dbg & 1) || !__any(n != 0)) break;
-      const int s = (n != 0) ? f.slot[n - 1] : -1;
-      hist_add(sh, a.bins, s, label);
-      if (n != 0) n = f.parent[n - 1];
-    }
-    // ring: a foreground pixel 4-adjacent to a selected hole of its own component
-    int hs[4] = {-1, -1, -1, -1};
-    if (p < p1 && fgp && sel_holes) {
-      const int me = f.L[p + 1];
-      const int nb[4] = {x > 0 ? p - 1 : -1, x + 1 < a.cw ? p + 1 : -1, y > 0 ? p - a.cw : -1,
-                         y + 1 < a.ch ? p + a.cw : -1};
-      int seen[4] = {0, 0, 0, 0};
+      const int y = p / cw, x = p - y * cw;
+      const bool fgp = f.mask[p] != 0;
+      const int np = fin(f, p);
+      int c = lab[y * a.W + x];
+      if (c >= bins) c = bins - 1;
+      if (np != 0 && !(a.dbg & 1)) hkey = (np * bins + c) * 2;
+      if (x + 1 < cw && y + 1 < ch) {
+        const int idx[4] = {p, p + 1, p + cw, p + cw + 1};
+        const int TX[4] = {1, 2, 1, 2}, TY[4] = {1, 1, 2, 2};
+        int node[4];
+        bool fg[4];
+        int nf = 0, missing = 0;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (nb[k] < 0 || f.mask[nb[k]]) continue;
-        const int h = f.L[nb[k] + 1];
-        if (h == 0 || f.parent[h - 1] != me) continue;
-        bool dup = false;
-        for (int j = 0; j < k; ++j) dup |= (seen[j] == h);
-        seen[k] = h;
-        if (!dup) hs[k] = f.slot[h - 1];
+        for (int k = 0; k < 4; ++k) {
+          fg[k] = k == 0 ? fgp : f.mask[idx[k]] != 0;
+          node[k] = k == 0 ? np : fin(f, idx[k]);
+          if (fg[k]) { ++nf; fnode = node[k]; } else { missing = k; }
+        }
+        const long long X = x, Y = y;
+        if (nf == 4) {
+          f00 = 2; f10 = 6 * X + 3; f01 = 6 * Y + 3;
+        } else if (nf == 3) {
+          const int o = 3 - missing;  // triangle of the opposite corner
+          f00 = 1; f10 = 3 * X + TX[o]; f01 = 3 * Y + TY[o];
+        } else {
+          fnode = 0;
+        }
+        int nb = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (fg[k] || node[k] == 0) continue;
+          bool first = true;
+          int cnt = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (!fg[j] && node[j] == node[k]) {
+              ++cnt;
+              if (j < k) first = false;
+            }
+          }
+          if (!first) continue;
+          if (nb < 2) {
+            bn[nb] = node[k];
+            if (cnt >= 2) { b00[nb] = 2; b10[nb] = 6 * X + 3; b01[nb] = 6 * Y + 3; }
+            else { b00[nb] = 1; b10[nb] = 3 * X + TX[k]; b01[nb] = 3 * Y + TY[k]; }
+            ++nb;
+          }
+        }
+      }
+      // ring: the foreground pixels 4-adjacent to a hole that belong to the hole's parent
+      // component are part of the hole contour's fill. Counted from the hole side (hole
+      // pixels are rare; round-2's check from every foreground pixel cost ~20 us per 32
+      // frames): a hole pixel credits each such neighbour r whose first 4-neighbour
+      // (order left, right, up, down) inside the hole is this pixel, so r counts once.
+      if (!fgp && np != 0 && !(a.dbg & 2)) {
+        const int par = parent_of(f, cw, np);
+        const int nbr[4] = {x > 0 ? p - 1 : -1, x + 1 < cw ? p + 1 : -1, y > 0 ? p - cw : -1,
+                            y + 1 < ch ? p + cw : -1};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int r = nbr[k];
+          if (r < 0 || !f.mask[r] || fin(f, r) != par) continue;
+          const int ry = r / cw, rx = r - ry * cw;
+          const int rn[4] = {rx > 0 ? r - 1 : -1, rx + 1 < cw ? r + 1 : -1, ry > 0 ? r - cw : -1,
+                             ry + 1 < ch ? r + cw : -1};
+          bool first = true;
+          for (int j = 0; j < 4 && rn[j] != p; ++j)
+            if (rn[j] >= 0 && !f.mask[rn[j]] && fin(f, rn[j]) == np) { first = false; break; }
+          if (!first) continue;
+          int rc = lab[ry * a.W + rx];
+          if (rc >= bins) rc = bins - 1;
+          rkey[k] = (np * bins + rc) * 2 + 1;
+        }
       }
     }
+    agg_add(T, f, cw, fnode, f00, f10, f01);
+    agg_add(T, f, cw, bn[0], b00[0], b10[0], b01[0]);
+    agg_add(T, f, cw, bn[1], b00[1], b10[1], b01[1]);
+    hagg(T, f, cw, bins, hkey);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) hist_add(sh, a.bins, hs[k], label);
+    for (int k = 0; k < 4; ++k)
+      if (__any(rkey[k] > 0)) hagg(T, f, cw, bins, rkey[k]);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < nh; i += 256)
-    if (sh[i]) atomicAdd(f.hist + i, sh[i]);
+  for (int i = threadIdx.x; i < kHash; i += 256) {
+    const int node = T.q.key[i];
+    if (node != 0) moments_up(f, cw, node, T.q.s00[i], (long long)T.q.s10[i], (long long)T.q.s01[i]);
+  }
+  for (int i = threadIdx.x; i < kHistHash; i += 256) {
+    const int key = T.hkey[i];
+    if (key != 0) hist_up(f, cw, bins, key, T.hcnt[i]);
+  }
+}
+
+// ---------------------------------------------------------------- select
+// k_assign (one workgroup per frame) hands the record slots to the first K passing
+// contours in raster order of their discovery pixel: the passing roots of the root
+// list are gathered in LDS and bitonic-sorted. The choice is deterministic (round 1
+// took them in atomicAdd order, so with more than K passing contours the kept subset
+// changed from run to run) and keeps the smallest discovery keys: among
+// siblings those come LAST in findContours order, so they are the records the
+// reference's LIFO buffer serves first (/root/reference/sem_seg_server.py:186-192,
+// 52-60). Contours past K are counted in nslot[1]; k_finalize flags the frame by a
+// negative record count. Frames with more than kSortCap passing contours take a
+// raster-order scan of every pixel instead. (Round 2 ran a full-frame k_select pass
+// before this kernel: 20 us per 32 frames.)
+__device__ __forceinline__ bool passes(const FrameWS& f, const KArgs& a, int p) {
+  if (fin(f, p) != p + 1) return false;
+  const int t = f.t00[p];
+  return t != 0 && (double)t * 0.5 >= a.min_area;
+}
+
+constexpr int kSortCap = 8192;
+
+__global__ __launch_bounds__(1024) void k_assign(KArgs a) {
+  __shared__ int s_key[kSortCap];
+  __shared__ int s_cnt, s_w[16];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int N = a.ch * a.cw;
+  FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
+  f.fb = f.flag[0];
+  if (t == 0) s_cnt = 0;
+  __syncthreads();
+  const int nroot = f.nslot[3];
+  for (int i = t; i < nroot; i += 1024) {
+    const int p = f.rlist[i];
+    if (passes(f, a, p)) {
+      const int k = atomicAdd(&s_cnt, 1);
+      if (k < kSortCap) s_key[k] = p;
+    }
+  }
+  __syncthreads();
+  const int total = s_cnt;
+  const int kept = min(total, a.K);
+  if (total <= kSortCap) {
+    int n2 = 1;
+    while (n2 < total) n2 <<= 1;
+    for (int i = total + t; i < n2; i += 1024) s_key[i] = 0x7fffffff;
+    __syncthreads();
+    for (int k = 2; k <= n2; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = t; i < n2; i += 1024) {
+          const int ij = i ^ j;
+          if (ij > i) {
+            const int u = s_key[i], v = s_key[ij];
+            if ((u > v) == ((i & k) == 0)) { s_key[i] = v; s_key[ij] = u; }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    for (int i = t; i < kept; i += 1024) {
+      const int p = s_key[i];
+      f.slot[p] = i;
+      f.slot_node[i] = p + 1;
+    }
+  } else {
+    const int wid = t >> 6, lane = t & 63;
+    int base = 0;
+    for (int c0 = 0; c0 < N && base < kept; c0 += 1024) {
+      const int p = c0 + t;
+      const bool ok = p < N && passes(f, a, p);
+      const unsigned long long m = __ballot(ok);
+      if (lane == 0) s_w[wid] = __popcll(m);
+      __syncthreads();
+      int wb = 0, tot = 0;
+      for (int w = 0; w < 16; ++w) {
+        wb += w < wid ? s_w[w] : 0;
+        tot += s_w[w];
+      }
+      const int rank = base + wb + __popcll(m & ((1ull << lane) - 1));
+      if (ok && rank < kept) {
+        f.slot[p] = rank;
+        f.slot_node[rank] = p + 1;
+      }
+      base += tot;
+      __syncthreads();
+    }
+  }
+  if (t == 0) {
+    f.nslot[0] = kept;
+    f.nslot[1] = total - kept;
+  }
 }
 
 // ---------------------------------------------------------------- finalize
@@ -979,23 +989,23 @@ __device__ __forceinline__ int disc_key(const FrameWS& f, int n) {
   return f.mask[r] ? r : r - 1;
 }
 
-__device__ __forceinline__ int node_depth(const FrameWS& f, int n) {
+__device__ __forceinline__ int node_depth(const FrameWS& f, int cw, int n) {
   int d = 0;
-  for (; n != 0; n = f.parent[n - 1]) ++d;
+  for (; n != 0; n = parent_of(f, cw, n)) ++d;
   return d;
 }
 
 // Does node a (depth da) come before node b (depth db) in findContours pre-order?
 // (a is an ancestor of b, or at the first divergence a's branch has the larger key.)
-__device__ bool precedes(const FrameWS& f, int a, int da, int b, int db) {
+__device__ bool precedes(const FrameWS& f, int cw, int a, int da, int b, int db) {
   int u = a, v = b;
-  for (; db > da; --db) v = f.parent[v - 1];
+  for (; db > da; --db) v = parent_of(f, cw, v);
   if (u == v) return true;   // a is an ancestor of b
-  for (; da > db; --da) u = f.parent[u - 1];
+  for (; da > db; --da) u = parent_of(f, cw, u);
   if (u == v) return false;  // b is an ancestor of a
-  while (f.parent[u - 1] != f.parent[v - 1]) {
-    u = f.parent[u - 1];
-    v = f.parent[v - 1];
+  while (parent_of(f, cw, u) != parent_of(f, cw, v)) {
+    u = parent_of(f, cw, u);
+    v = parent_of(f, cw, v);
   }
   return disc_key(f, u) > disc_key(f, v);
 }
@@ -1003,6 +1013,7 @@ __device__ bool precedes(const FrameWS& f, int a, int da, int b, int db) {
 __global__ __launch_bounds__(64) void k_finalize(KArgs a) {
   const int b = blockIdx.x;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
+  f.fb = f.flag[0];
   float* rec = a.records + (size_t)b * (1 + 5 * a.K);
   __shared__ int s_node[256];
   __shared__ int s_path[256][kMaxDepth];
@@ -1021,7 +1032,7 @@ __global__ __launch_bounds__(64) void k_finalize(KArgs a) {
     // ancestor chain (top first) of discovery keys
     int chain[kMaxDepth];
     int len = 0;
-    for (int n = node; n != 0 && len < kMaxDepth; n = f.parent[n - 1]) {
+    for (int n = node; n != 0 && len < kMaxDepth; n = parent_of(f, a.cw, n)) {
       const int r = n - 1;
       const bool isfg = f.mask[r] != 0;
       chain[len++] = isfg ? r : r - 1;
@@ -1031,12 +1042,12 @@ __global__ __launch_bounds__(64) void k_finalize(KArgs a) {
     if (len == kMaxDepth) {
       // chain truncated (nesting deeper than kMaxDepth): order by parent walks instead
       int n = node, d = 0;
-      for (; n != 0 && d <= kMaxDepth; n = f.parent[n - 1]) ++d;
+      for (; n != 0 && d <= kMaxDepth; n = parent_of(f, a.cw, n)) ++d;
       if (n != 0) s_deep = 1;
     }
     // statistics
     const int r = node - 1;
-    const int* h = f.hist + (size_t)i * a.bins;
+    const int* h = f.th + (size_t)r * a.bins;
     int best = 0, tot = 0;
     for (int c = 0; c < a.bins; ++c) {
       tot += h[c];
@@ -1064,9 +1075,9 @@ __global__ __launch_bounds__(64) void k_finalize(KArgs a) {
   if (s_deep) {  // exact order at any depth: lift to equal depth, then walk to the LCA
     for (int i = t; i < ns; i += 64) {
       int rank = 0;
-      const int di = node_depth(f, s_node[i]);
+      const int di = node_depth(f, a.cw, s_node[i]);
       for (int j = 0; j < ns; ++j)
-        if (j != i) rank += precedes(f, s_node[j], node_depth(f, s_node[j]), s_node[i], di);
+        if (j != i) rank += precedes(f, a.cw, s_node[j], node_depth(f, a.cw, s_node[j]), s_node[i], di);
       s_order[rank] = i;
     }
     __syncthreads();
@@ -1100,12 +1111,6 @@ __global__ __launch_bounds__(64) void k_finalize(KArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_zero(uint4* __restrict__ p, size_t n16) {
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16;
-       i += (size_t)gridDim.x * blockDim.x)
-    p[i] = make_uint4(0, 0, 0, 0);
-}
-
 }  // namespace
 
 size_t post_workspace_bytes(int B, int H, int W, int K, int num_bins) {
@@ -1114,9 +1119,10 @@ size_t post_workspace_bytes(int B, int H, int W, int K, int num_bins) {
 
 void postprocess(const PostParams& p, hipStream_t s) {
   if (p.K > 256) throw std::invalid_argument("postprocess: K > 256");
-  if ((size_t)p.K * p.num_bins > (size_t)kMaxHist) throw std::invalid_argument("postprocess: K * bins too large");
-  if (p.H > 65535 || p.W > 65535)  // k_quads' 32-bit wave sums of 6x + 3 pieces
+  if (p.H > 65535 || p.W > 65535)  // k_accum's 32-bit wave sums of 6x + 3 pieces
     throw std::invalid_argument("postprocess: maps larger than 65535 pixels per side");
+  if (((long long)p.crop_h * p.crop_w + 1) * p.num_bins * 2 >= (1ll << 31))  // k_accum's histogram keys
+    throw std::invalid_argument("postprocess: crop * classes too large for 32-bit histogram keys");
   if (p.crop_h > p.H || p.crop_w > p.W || p.crop_h <= 0 || p.crop_w <= 0)
     throw std::invalid_argument("postprocess: bad crop");
   KArgs a;
@@ -1130,12 +1136,8 @@ void postprocess(const PostParams& p, hipStream_t s) {
     const char* e = getenv("SSA_POST_DBG");
     a.dbg = e ? atoi(e) : 0;
   }
-  // zero the per-frame counters and histograms (one contiguous, 256-B aligned region).
-  // A kernel, not hipMemsetAsync: a memset node captured by torch.cuda.graph faulted
-  // (illegal address) on its second replay on ROCm 7.x; kernel nodes replay cleanly.
-  const size_t n16 = a.lay.small_bytes * p.B / 16;
-  hipLaunchKernelGGL(k_zero, dim3((unsigned)std::min<size_t>((n16 + 255) / 256, 1024)), dim3(256), 0,
-                     s, reinterpret_cast<uint4*>(a.ws), n16);
+  // the per-frame counters are zeroed inside k_ccl_local (a kernel, not hipMemsetAsync:
+  // a memset node captured by torch.cuda.graph faulted on its second replay on ROCm 7.x)
   const int N = p.crop_h * p.crop_w;
   const dim3 blk(256);
   const dim3 gp(cdiv(N, 256), p.B);
@@ -1150,10 +1152,10 @@ void postprocess(const PostParams& p, hipStream_t s) {
   {
     const int tx_n = cdiv(p.crop_w, TW), ty_n = cdiv(p.crop_h, TH);
     const int nt = tx_n * ty_n;
-    const size_t lds = (size_t)(nt + 1 + 1024 + 2 * (kMergeCap + 1)) * 4;
     const int lines = (ty_n - 1) + 2 + 2 * (tx_n - 1) + 2;
     if (st++ < stages)
       hipLaunchKernelGGL(k_ccl_edges, dim3(cdiv(std::max(p.crop_w, p.crop_h), 256), lines, p.B), blk, 0, s, a);
+    const size_t lds = (size_t)(nt + 1 + 1024 + 2 * (kMergeCap + 1) + 1) * 4;
     if (lds > 160 * 1024) throw std::invalid_argument("postprocess: crop too large for the LDS merge");
     static bool attr = false;
     if (!attr) {
@@ -1164,24 +1166,11 @@ void postprocess(const PostParams& p, hipStream_t s) {
     }
     if (st++ < stages) hipLaunchKernelGGL(k_ccl_merge, dim3(p.B), dim3(1024), lds, s, a);
   }
-  if (st++ < stages) hipLaunchKernelGGL(k_ccl_boundary, dim3(std::min(cdiv(N, 256), 64), p.B), blk, 0, s, a);
-  if (st++ < stages) hipLaunchKernelGGL(k_compress, gp, blk, 0, s, a);
-  // strip-privatised passes: kQuadBlocks strips per frame (SSA_QUAD_BLOCKS overrides, tuning)
+  // strip-privatised pass: kQuadBlocks strips per frame (SSA_QUAD_BLOCKS overrides, tuning)
   const char* qb_env = getenv("SSA_QUAD_BLOCKS");
   const int qblocks = qb_env ? std::max(1, atoi(qb_env)) : kQuadBlocks;
-  const dim3 gs(qblocks, p.B);
-  // k_hist only runs on frames with a selected contour (usually a few of the batch):
-  // many more, shorter strips per frame so those frames' dependent per-pixel
-  // L -> slot -> parent chains are spread over the whole chip instead of 64 blocks
-  const char* hb_env = getenv("SSA_HIST_BLOCKS");
-  const int hblocks = hb_env ? std::max(1, atoi(hb_env)) : kHistBlocks;
-  const dim3 gh(hblocks, p.B);
-  if (st++ < stages) hipLaunchKernelGGL(k_quads, gs, blk, 0, s, a);
-  if (st++ < stages) hipLaunchKernelGGL(k_tree, gp, blk, 0, s, a);
-  if (st++ < stages) hipLaunchKernelGGL(k_select, gp, blk, 0, s, a);
+  if (st++ < stages) hipLaunchKernelGGL(k_accum, dim3(qblocks, p.B), blk, 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_assign, dim3(p.B), dim3(1024), 0, s, a);
-  if (st++ < stages)
-    hipLaunchKernelGGL(k_hist, gh, blk, (size_t)std::min(p.K, 256) * p.num_bins * 4, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_finalize, dim3(p.B), dim3(64), 0, s, a);
   check_launch("postprocess");
 }
