@@ -49,6 +49,7 @@ struct FrameWS {
   int32_t* ntroot;     // [ntiles] tile-local roots per tile
   int32_t* flag;       // [4]: [0] = 1 -> frame took the global union-find fallback
   int32_t* edges;      // [kEdgeCap][2] cross-tile unions (tile-local root pairs, -1 = outside)
+  int32_t* rpar;       // [N] per root index: border-tree parent (component label, 0 = frame)
   int32_t* rlist;      // [N] raster indices of the component roots (nslot[3] of them, any order)
   int fb;              // (kernels after k_ccl_merge) flag[0]: L holds final labels
 };
@@ -81,7 +82,7 @@ Layout layout(int H, int W, int K, int bins) {
   l.ntiles = (size_t)((W + TW - 1) / TW) * ((H + TH - 1) / TH);
   l.small_bytes = al(16 + (size_t)K * 4);
   l.big_bytes = al((l.N + 1) * 4) + al(l.N) + 2 * al(l.N * 4) + 2 * al(l.N * 8) + al(l.N * bins * 4) +
-                al(l.N * 4) + al(l.ntiles * kTileRoots * 4) + al(l.ntiles * 4) + al(16) + al((size_t)kEdgeCap * 8) + al(l.N * 4);
+                al(l.N * 4) + al(l.ntiles * kTileRoots * 4) + al(l.ntiles * 4) + al(16) + al((size_t)kEdgeCap * 8) + 2 * al(l.N * 4);
   return l;
 }
 
@@ -103,6 +104,7 @@ __host__ __device__ inline FrameWS frame_ws(char* ws, const Layout& l, int B, in
   f.ntroot = reinterpret_cast<int32_t*>(p); p += al(l.ntiles * 4);
   f.flag = reinterpret_cast<int32_t*>(p); p += al(16);
   f.edges = reinterpret_cast<int32_t*>(p); p += al((size_t)kEdgeCap * 8);
+  f.rpar = reinterpret_cast<int32_t*>(p); p += al(l.N * 4);
   f.rlist = reinterpret_cast<int32_t*>(p); p += al(l.N * 4);
   f.fb = 0;
   return f;
@@ -224,14 +226,15 @@ static_assert(RPT * kCclThreads == TW * TH && TW == 32, "k_ccl_local: 32-wide ti
 
 __global__ __launch_bounds__(kCclThreads) void k_ccl_local(KArgs a, const int32_t* __restrict__ pal) {
   constexpr int HW2 = TW + 2, HH2 = TH + 2, RS = kCclThreads / TW;  // RS: row stride of a thread's pixels
-  __shared__ int spal[256 * 3];
+  __shared__ int spal[256];  // packed r | g << 10 | b << 20 (3-sums of a field stay < 1024)
   __shared__ uint8_t slab[HH2 * HW2];
-  __shared__ int hs[3][HH2 * TW];
+  __shared__ int hs[HH2 * TW];  // packed horizontal 3-sums
   __shared__ int lbl[TW * TH];
   __shared__ unsigned fgrow[TH], bgrow[TH];
   __shared__ int s_nroot;
   const int tid = threadIdx.x;
-  for (int i = tid; i < 256 * 3; i += kCclThreads) spal[i] = pal[i];
+  for (int i = tid; i < 256; i += kCclThreads)
+    spal[i] = (pal[3 * i] & 255) | (pal[3 * i + 1] & 255) << 10 | (pal[3 * i + 2] & 255) << 20;
   if (tid == 0) s_nroot = 0;
   const int b = blockIdx.z;
   const int x0 = blockIdx.x * TW, y0 = blockIdx.y * TH;
@@ -256,8 +259,7 @@ __global__ __launch_bounds__(kCclThreads) void k_ccl_local(KArgs a, const int32_
     const int r = i / TW, c = i % TW;
     const uint8_t* sr = slab + r * HW2 + c;
     const int l0 = sr[0], l1 = sr[1], l2 = sr[2];
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) hs[ch][i] = spal[l0 * 3 + ch] + spal[l1 * 3 + ch] + spal[l2 * 3 + ch];
+    hs[i] = spal[l0] + spal[l1] + spal[l2];
   }
   __syncthreads();
   bool m[RPT], in[RPT];
@@ -271,9 +273,10 @@ __global__ __launch_bounds__(kCclThreads) void k_ccl_local(KArgs a, const int32_
     m[k] = false;
     if (in[k]) {
       int c[3];
+      const int h0 = hs[ty * TW + tx], h1 = hs[(ty + 1) * TW + tx], h2 = hs[(ty + 2) * TW + tx];
 #pragma unroll
       for (int ch = 0; ch < 3; ++ch) {
-        const int sum = hs[ch][ty * TW + tx] + hs[ch][(ty + 1) * TW + tx] + hs[ch][(ty + 2) * TW + tx];
+        const int sum = ((h0 >> (10 * ch)) & 1023) + ((h1 >> (10 * ch)) & 1023) + ((h2 >> (10 * ch)) & 1023);
         c[ch] = (sum * 2 + 9) / 18;
       }
       const int g = (c[0] * 1868 + c[1] * 9617 + c[2] * 4899 + (1 << 13)) >> 14;
@@ -528,7 +531,12 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(KArgs a) {
       if (r == p + 1) add_root(f, a.bins, p, s_nr);
     }
     __syncthreads();
-    if (tid == 0) f.nslot[3] = *s_nr;
+    const int nr = *s_nr;
+    for (int i = tid; i < nr; i += 1024) {
+      const int p = f.rlist[i];
+      f.rpar[p] = p % cw > 0 ? ld_relaxed(f.L + p) : 0;
+    }
+    if (tid == 0) f.nslot[3] = nr;
     return;
   }
   const int OUT = R;
@@ -565,7 +573,13 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(KArgs a) {
     }
   }
   __syncthreads();
-  if (tid == 0) f.nslot[3] = *s_nr;
+  // border-tree parent of every root: the final label of the pixel left of it
+  const int nr = *s_nr;
+  for (int i = tid; i < nr; i += 1024) {
+    const int p = f.rlist[i];
+    f.rpar[p] = p % cw > 0 ? f.cidx[f.L[p] - 1] : 0;
+  }
+  if (tid == 0) f.nslot[3] = nr;
 }
 
 // Cross-tile merges (and image-border background -> outside node 0) of the fallback
@@ -622,7 +636,8 @@ __device__ __forceinline__ void ccl_boundary_pixel(KArgs& a, FrameWS& f, int p) 
 }
 
 // Parent of component n in the border tree: the component of the pixel left of its
-// first pixel (0 = the frame at the image border). A pure function of the final labels.
+// first pixel (0 = the frame at the image border), a pure function of the final labels,
+// tabulated per root by k_ccl_merge (one load instead of the L -> cidx chain).
 // Final component label of pixel q (root raster index + 1, 0 = outside).
 __device__ __forceinline__ int fin(const FrameWS& f, int q) {
   const int l = f.L[q + 1];
@@ -630,7 +645,7 @@ __device__ __forceinline__ int fin(const FrameWS& f, int q) {
 }
 
 __device__ __forceinline__ int parent_of(const FrameWS& f, int cw, int n) {
-  return (n - 1) % cw > 0 ? fin(f, n - 2) : 0;
+  return f.rpar[n - 1];
 }
 
 // Per-block privatisation of the component sums. A real scene's mask has a few
@@ -655,8 +670,8 @@ struct QuadTable {
 // Subtree sums without a tree pass: every (block, component) partial is added to the
 // component and all its ancestors at flush time (round 2 summed own pieces first and
 // walked the ancestors per root in a separate full-frame pass, k_tree).
-__device__ void moments_up(FrameWS& f, int cw, int node, int d00, long long d10, long long d01) {
-  for (int n = node, depth = 0; n != 0 && depth <= 65536; ++depth, n = parent_of(f, cw, n)) {
+__device__ void moments_up(FrameWS& f, int cw, int node, int d00, long long d10, long long d01, int maxd) {
+  for (int n = node, depth = 0; n != 0 && depth <= maxd; ++depth, n = parent_of(f, cw, n)) {
     atomicAdd(f.t00 + n - 1, d00);
     atomicAdd(reinterpret_cast<unsigned long long*>(f.t10 + n - 1), (unsigned long long)d10);
     atomicAdd(reinterpret_cast<unsigned long long*>(f.t01 + n - 1), (unsigned long long)d01);
@@ -667,19 +682,20 @@ __device__ void moments_up(FrameWS& f, int cw, int node, int d00, long long d10,
 // An own-pixel count goes to the node and all its ancestors (a contour's fill is its
 // component plus everything it encloses); a ring count (parent pixels 4-adjacent to a
 // hole, part of the hole contour's fill only) goes to the hole alone.
-__device__ void hist_up(FrameWS& f, int cw, int bins, int key, int cnt) {
+__device__ void hist_up(FrameWS& f, int cw, int bins, int key, int cnt, int maxd) {
   const int v = key >> 1, node = v / bins, c = v - node * bins;
   if (key & 1) {
     atomicAdd(f.th + (size_t)(node - 1) * bins + c, cnt);
     return;
   }
-  for (int n = node, depth = 0; n != 0 && depth <= 65536; ++depth, n = parent_of(f, cw, n))
+  for (int n = node, depth = 0; n != 0 && depth <= maxd; ++depth, n = parent_of(f, cw, n))
     atomicAdd(f.th + (size_t)(n - 1) * bins + c, cnt);
 }
 
 constexpr int kHistHash = 256;
 
 struct AccTable {
+  int maxd;  // ancestor levels a flush adds to (65536; 0 = SSA_POST_DBG bit 4 timing ablation)
   QuadTable q;
   int hkey[kHistHash];
   int hcnt[kHistHash];
@@ -702,7 +718,7 @@ __device__ __forceinline__ void table_add(AccTable& T, FrameWS& f, int cw, int n
       return;
     }
   }
-  moments_up(f, cw, node, d00, d10, d01);
+  moments_up(f, cw, node, d00, d10, d01, T.maxd);
 }
 
 __device__ __forceinline__ void agg_add(AccTable& T, FrameWS& f, int cw, int node, int d00, long long d10,
@@ -743,7 +759,7 @@ __device__ __forceinline__ void htable_add(AccTable& T, FrameWS& f, int cw, int 
       return;
     }
   }
-  hist_up(f, cw, bins, key, cnt);
+  hist_up(f, cw, bins, key, cnt, T.maxd);
 }
 
 // Wave-aggregated histogram add: the wave's lanes are grouped by key (one ballot per
@@ -784,6 +800,7 @@ __global__ __launch_bounds__(256) void k_accum(KArgs a) {
   for (int i = threadIdx.x; i < kHistHash; i += 256) {
     T.hkey[i] = 0; T.hcnt[i] = 0;
   }
+  if (threadIdx.x == 0) T.maxd = (a.dbg & 4) ? 0 : 65536;
   __syncthreads();
   const uint8_t* lab = a.labels + (size_t)b * a.H * a.W;
   const int per = (N + gridDim.x - 1) / gridDim.x;
@@ -795,23 +812,45 @@ __global__ __launch_bounds__(256) void k_accum(KArgs a) {
     int bn[2] = {0, 0}, b00[2] = {0, 0};
     long long b10[2] = {0, 0}, b01[2] = {0, 0};
     int hkey = 0, rkey[4] = {0, 0, 0, 0};
+    // each lane loads its pixel and the one below; the quad's right column comes from
+    // the next lane (consecutive pixels), so every label is resolved twice instead of
+    // four times (the dependent L -> cidx loads are this pass's latency chain)
+    const int lane = threadIdx.x & 63;
+    int y = 0, x = 0, n0 = 0, n2 = 0;
+    bool m0 = false, m2 = false;
+    if (p < N) {
+      y = p / cw;
+      x = p - y * cw;
+      m0 = f.mask[p] != 0;
+      n0 = fin(f, p);
+      if (y + 1 < ch) {
+        m2 = f.mask[p + cw] != 0;
+        n2 = fin(f, p + cw);
+      }
+    }
+    bool m1 = __shfl_down((int)m0, 1, 64) != 0, m3 = __shfl_down((int)m2, 1, 64) != 0;
+    int n1 = __shfl_down(n0, 1, 64), n3 = __shfl_down(n2, 1, 64);
+    if (lane == 63 && p < N && x + 1 < cw) {
+      m1 = f.mask[p + 1] != 0;
+      n1 = fin(f, p + 1);
+      if (y + 1 < ch) {
+        m3 = f.mask[p + cw + 1] != 0;
+        n3 = fin(f, p + cw + 1);
+      }
+    }
     if (p < p1) {
-      const int y = p / cw, x = p - y * cw;
-      const bool fgp = f.mask[p] != 0;
-      const int np = fin(f, p);
+      const bool fgp = m0;
+      const int np = n0;
       int c = lab[y * a.W + x];
       if (c >= bins) c = bins - 1;
       if (np != 0 && !(a.dbg & 1)) hkey = (np * bins + c) * 2;
       if (x + 1 < cw && y + 1 < ch) {
-        const int idx[4] = {p, p + 1, p + cw, p + cw + 1};
         const int TX[4] = {1, 2, 1, 2}, TY[4] = {1, 1, 2, 2};
-        int node[4];
-        bool fg[4];
+        const int node[4] = {n0, n1, n2, n3};
+        const bool fg[4] = {m0, m1, m2, m3};
         int nf = 0, missing = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          fg[k] = k == 0 ? fgp : f.mask[idx[k]] != 0;
-          node[k] = k == 0 ? np : fin(f, idx[k]);
           if (fg[k]) { ++nf; fnode = node[k]; } else { missing = k; }
         }
         const long long X = x, Y = y;
@@ -882,11 +921,11 @@ __global__ __launch_bounds__(256) void k_accum(KArgs a) {
   __syncthreads();
   for (int i = threadIdx.x; i < kHash; i += 256) {
     const int node = T.q.key[i];
-    if (node != 0) moments_up(f, cw, node, T.q.s00[i], (long long)T.q.s10[i], (long long)T.q.s01[i]);
+    if (node != 0) moments_up(f, cw, node, T.q.s00[i], (long long)T.q.s10[i], (long long)T.q.s01[i], T.maxd);
   }
   for (int i = threadIdx.x; i < kHistHash; i += 256) {
     const int key = T.hkey[i];
-    if (key != 0) hist_up(f, cw, bins, key, T.hcnt[i]);
+    if (key != 0) hist_up(f, cw, bins, key, T.hcnt[i], T.maxd);
   }
 }
 

@@ -3,7 +3,9 @@
 // with rocprofv3) on identical label maps without the Python stack:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I csrc/hip csrc/tools/post_bench.hip \
 //         csrc/hip/postprocess.hip -o post_bench
-//   ./post_bench [reps]
+//   ./post_bench [reps] [maps.bin [only]]
+// (maps.bin: raw [32, 513, 513] uint8 label maps, e.g. the bench model's output dumped by
+// scripts/label_stats.py, timed as a fourth kind "file")
 // Maps: B = 32 frames of 513 x 513 cropped to 513 x 385 (the headline's 640x480
 // letterbox). "flat": background and a non-masked class; "planted": 3-10 ellipses of
 // person / car per frame, some with holes and islands; "noisy": planted + 1 % salt.
@@ -89,11 +91,22 @@ int main(int argc, char** argv) {
   chk(hipEventCreate(&e0), "ev");
   chk(hipEventCreate(&e1), "ev");
   printf("workspace %.1f MB/frame\n", wsb / (double)B / 1e6);
-  const char* names[3] = {"flat", "planted", "noisy"};
+  const char* names[4] = {"flat", "planted", "noisy", "file"};
+  const int kinds = argc > 2 ? 4 : 3, k0 = argc > 3 ? 3 : 0;  // argv[3]: the file kind only
   std::vector<float> rec((size_t)B * (1 + 5 * K));
-  for (int kind = 0; kind < 3; ++kind) {
+  for (int kind = k0; kind < kinds; ++kind) {
     std::vector<uint8_t> maps;
-    make_maps(maps, B, H, W, ch, cw, kind, 1234 + kind);
+    if (kind < 3) {
+      make_maps(maps, B, H, W, ch, cw, kind, 1234 + kind);
+    } else {
+      maps.resize((size_t)B * H * W);
+      FILE* fp = fopen(argv[2], "rb");
+      if (!fp || fread(maps.data(), 1, maps.size(), fp) != maps.size()) {
+        fprintf(stderr, "cannot read %s\n", argv[2]);
+        return 1;
+      }
+      fclose(fp);
+    }
     chk(hipMemcpy(dlab, maps.data(), maps.size(), hipMemcpyHostToDevice), "lab");
     PostParams p;
     p.labels = dlab; p.B = B; p.H = H; p.W = W; p.crop_h = ch; p.crop_w = cw;

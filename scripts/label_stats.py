@@ -22,7 +22,11 @@ def main():
     src = SyntheticSource(640, 480, seed=1, pool=8)
     frames = torch.from_numpy(src.read_batch(B)[0]).cuda()
     labels, post = eng._step_device(frames)
-    lab = labels.cpu().numpy()[:, :eng.crop_h, :eng.crop_w]
+    full = labels.cpu().numpy()
+    if len(sys.argv) > 1:  # raw [B, H, W] uint8 dump for csrc/tools/post_bench.hip
+        full.astype(np.uint8).tofile(sys.argv[1])
+        print("dumped", full.shape, "to", sys.argv[1])
+    lab = full[:, :eng.crop_h, :eng.crop_w]
     rec = post.cpu().numpy()
     print("crop", eng.crop_w, eng.crop_h, "records/frame", rec[:, 0].mean())
     cls, cnt = np.unique(lab, return_counts=True)
