@@ -909,7 +909,11 @@ void conv_gemm_grouped(const ConvParams* ps, int n, const int* order, int nblock
     // and LDS latency of the 1-workgroup-per-CU 256 x 256 tiles (MFMA busy ~23 % in v6)
     case 15: launch_conv_glds_group<4, 4, 2, 4, 4>(ga, nblocks, s); break;      // 256 x 256
     case 16: launch_conv_glds_group<4, 4, 4, 4, 4, 32>(ga, nblocks, s); break;  // 256 x 256, 32-deep
-    default: throw std::invalid_argument("conv_gemm_grouped: variant must be 5, 6, 8, 10-16");
+    // 16 waves on half-size tiles (32 x 64 / 64 x 32 per wave): twice the tiles, so the LPT
+    // grid's last round (548 tiles of up to 9 taps on 256 CUs at 256 x 256) is finer
+    case 17: launch_conv_glds_group<2, 4, 2, 4, 4>(ga, nblocks, s); break;      // 128 x 256
+    case 18: launch_conv_glds_group<4, 2, 2, 4, 4>(ga, nblocks, s); break;      // 256 x 128
+    default: throw std::invalid_argument("conv_gemm_grouped: variant must be 5, 6, 8, 10-18");
   }
 }
 

@@ -363,7 +363,7 @@ class HipDeepLab:
             # that fits two workgroups per CU -- gave label maps that differed in 26 of 450
             # runs with plan copies on three streams, every other variant 0 / 450:
             # profiles/r2_concurrency_race.txt; kept out until that is understood)
-            for gv in (5, 6, 8, 12, 13, 14, 15, 16):
+            for gv in (5, 6, 8, 12, 13, 14, 15, 16, 17, 18):
                 BM = K.GROUP_TILE[gv][0]
                 convs = [dict(x=x, w=b0w, bias=b0b, out=cat, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w,
                               Cout=A, k=1, dil=1, ldo=self.cat_c, co_off=0, act="relu")]

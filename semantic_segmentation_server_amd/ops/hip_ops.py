@@ -130,7 +130,8 @@ def tap_group_perm(B: int, H: int, W: int, k: int, dil: int, BM: int, device=Non
 
 
 GROUP_TILE = {5: (128, 256), 6: (256, 256), 8: (128, 256), 10: (128, 128), 11: (128, 128),
-              12: (256, 256), 13: (128, 256), 14: (256, 256), 15: (256, 256), 16: (256, 256)}
+              12: (256, 256), 13: (128, 256), 14: (256, 256), 15: (256, 256), 16: (256, 256),
+              17: (128, 256), 18: (256, 128)}
 
 
 def _tile_taps(B: int, H: int, W: int, k: int, dil: int, BM: int,

@@ -110,7 +110,8 @@ def test_conv_gemm_tap_grouped(B, H, W, rate, variant, bm):
 @pytest.mark.parametrize("B,H,W,Cin,Cout,variant", [
     (3, 33, 33, 320, 256, 5), (2, 33, 33, 320, 256, 6), (2, 17, 19, 64, 200, 8),
     (2, 21, 20, 96, 136, 11), (3, 33, 33, 320, 256, 12), (2, 17, 19, 96, 200, 13),
-    (2, 21, 20, 320, 136, 14), (3, 33, 33, 320, 256, 15), (2, 21, 20, 96, 136, 16)])
+    (2, 21, 20, 320, 136, 14), (3, 33, 33, 320, 256, 15), (2, 21, 20, 96, 136, 16),
+    (3, 33, 33, 320, 256, 17), (2, 21, 20, 96, 136, 18)])
 def test_conv_gemm_grouped_aspp(B, H, W, Cin, Cout, variant):
     """ASPP branches (1x1 + atrous 6/12/18, tap-grouped rows) in one LPT-ordered grid:
     each branch's channel slice matches F.conv2d, the other channels stay untouched."""
