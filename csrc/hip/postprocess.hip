@@ -382,7 +382,9 @@ __device__ __forceinline__ void emit_pairs(FrameWS& f, int n, const int (&pa)[3]
   }
 }
 
-__global__ __launch_bounds__(256) void k_ccl_edges(KArgs a) {
+constexpr int kEdgeThreads = 256;
+
+__global__ __launch_bounds__(kEdgeThreads) void k_ccl_edges(KArgs a) {
   const int b = blockIdx.z;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
   const int tx_n = (a.cw + TW - 1) / TW, ty_n = (a.ch + TH - 1) / TH;
@@ -406,65 +408,69 @@ __global__ __launch_bounds__(256) void k_ccl_edges(KArgs a) {
     else { fixed = l == 2 * (tx_n - 1) ? 0 : a.cw - 1; kind = 4; }
     len = a.ch;
   }
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool valid = i < len && fixed >= 0 && (horiz ? fixed < a.ch : fixed < a.cw) &&
-                     !(kind == 3 && fixed + 1 >= a.cw);
-  const int x = horiz ? i : fixed, y = horiz ? fixed : i;
-  const int p = y * a.cw + x;
-  int pa[3] = {0, 0, 0}, pb[3] = {0, 0, 0};
-  int n = 0;
-  if (valid) {
-    const bool m = f.mask[p] != 0;
-    const int me = f.L[p + 1] - 1;
-    auto add = [&](int other) {  // distinct partners only
-      for (int k = 0; k < n; ++k)
-        if (pb[k] == other) return;
-      pa[n] = me;
-      pb[n] = other;
-      ++n;
-    };
-    auto lr = [&](int q) { return f.L[q + 1] - 1; };
-    if (kind == 0) {  // top row of a tile: unions with the row above
-      const int up = p - a.cw;
-      if (m) {
-        if (x > 0 && f.mask[up - 1]) add(lr(up - 1));
-        if (f.mask[up]) add(lr(up));
-        if (x + 1 < a.cw && f.mask[up + 1]) add(lr(up + 1));
-      } else if (!f.mask[up]) {
-        add(lr(up));
+  // (one 192-thread block per line, looping over the line, measured 2 us slower than a
+  // block per 256 pixels: profiles/r3_post_ab.txt)
+  for (int i0 = blockIdx.x * blockDim.x; i0 < len; i0 += gridDim.x * blockDim.x) {
+    const int i = i0 + (int)threadIdx.x;
+    const bool valid = i < len && fixed >= 0 && (horiz ? fixed < a.ch : fixed < a.cw) &&
+                       !(kind == 3 && fixed + 1 >= a.cw);
+    const int x = horiz ? i : fixed, y = horiz ? fixed : i;
+    const int p = y * a.cw + x;
+    int pa[3] = {0, 0, 0}, pb[3] = {0, 0, 0};
+    int n = 0;
+    if (valid) {
+      const bool m = f.mask[p] != 0;
+      const int me = f.L[p + 1] - 1;
+      auto add = [&](int other) {  // distinct partners only
+        for (int k = 0; k < n; ++k)
+          if (pb[k] == other) return;
+        pa[n] = me;
+        pb[n] = other;
+        ++n;
+      };
+      auto lr = [&](int q) { return f.L[q + 1] - 1; };
+      if (kind == 0) {  // top row of a tile: unions with the row above
+        const int up = p - a.cw;
+        if (m) {
+          if (x > 0 && f.mask[up - 1]) add(lr(up - 1));
+          if (f.mask[up]) add(lr(up));
+          if (x + 1 < a.cw && f.mask[up + 1]) add(lr(up + 1));
+        } else if (!f.mask[up]) {
+          add(lr(up));
+        }
+      } else if (kind == 2) {  // left column of a tile: unions with the column to the left
+        if (m) {
+          if (f.mask[p - 1]) add(lr(p - 1));
+          if (y > 0 && (y % TH) != 0 && f.mask[p - a.cw - 1]) add(lr(p - a.cw - 1));
+        } else if (!f.mask[p - 1]) {
+          add(lr(p - 1));
+        }
+      } else if (kind == 3) {  // right column: up-right diagonal into the next tile
+        if (m && y > 0 && (y % TH) != 0 && f.mask[p - a.cw + 1]) add(lr(p - a.cw + 1));
       }
-    } else if (kind == 2) {  // left column of a tile: unions with the column to the left
-      if (m) {
-        if (f.mask[p - 1]) add(lr(p - 1));
-        if (y > 0 && (y % TH) != 0 && f.mask[p - a.cw - 1]) add(lr(p - a.cw - 1));
-      } else if (!f.mask[p - 1]) {
-        add(lr(p - 1));
-      }
-    } else if (kind == 3) {  // right column: up-right diagonal into the next tile
-      if (m && y > 0 && (y % TH) != 0 && f.mask[p - a.cw + 1]) add(lr(p - a.cw + 1));
+      if ((kind == 1 || kind == 4) && !m) add(-1);  // image-border background -> outside
     }
-    if ((kind == 1 || kind == 4) && !m) add(-1);  // image-border background -> outside
-  }
-  // drop pairs the previous lane (previous pixel along this line) also emitted
-  const int lane = threadIdx.x & 63;
-  const int qa0 = __shfl_up(pa[0], 1, 64), qb0 = __shfl_up(pb[0], 1, 64);
-  const int qa1 = __shfl_up(pa[1], 1, 64), qb1 = __shfl_up(pb[1], 1, 64);
-  const int qa2 = __shfl_up(pa[2], 1, 64), qb2 = __shfl_up(pb[2], 1, 64);
-  const int qn = __shfl_up(n, 1, 64);
-  int keep = 0;
+    // drop pairs the previous lane (previous pixel along this line) also emitted
+    const int lane = threadIdx.x & 63;
+    const int qa0 = __shfl_up(pa[0], 1, 64), qb0 = __shfl_up(pb[0], 1, 64);
+    const int qa1 = __shfl_up(pa[1], 1, 64), qb1 = __shfl_up(pb[1], 1, 64);
+    const int qa2 = __shfl_up(pa[2], 1, 64), qb2 = __shfl_up(pb[2], 1, 64);
+    const int qn = __shfl_up(n, 1, 64);
+    int keep = 0;
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    if (k < n) {
-      bool dup = false;
-      if (lane > 0) {
-        dup |= qn > 0 && qa0 == pa[k] && qb0 == pb[k];
-        dup |= qn > 1 && qa1 == pa[k] && qb1 == pb[k];
-        dup |= qn > 2 && qa2 == pa[k] && qb2 == pb[k];
+    for (int k = 0; k < 3; ++k) {
+      if (k < n) {
+        bool dup = false;
+        if (lane > 0) {
+          dup |= qn > 0 && qa0 == pa[k] && qb0 == pb[k];
+          dup |= qn > 1 && qa1 == pa[k] && qb1 == pb[k];
+          dup |= qn > 2 && qa2 == pa[k] && qb2 == pb[k];
+        }
+        if (!dup) { pa[keep] = pa[k]; pb[keep] = pb[k]; ++keep; }
       }
-      if (!dup) { pa[keep] = pa[k]; pb[keep] = pb[k]; ++keep; }
     }
+    emit_pairs(f, keep, pa, pb);
   }
-  emit_pairs(f, keep, pa, pb);
 }
 
 __device__ __forceinline__ void ccl_boundary_pixel(KArgs& a, FrameWS& f, int p);
@@ -1193,7 +1199,8 @@ void postprocess(const PostParams& p, hipStream_t s) {
     const int nt = tx_n * ty_n;
     const int lines = (ty_n - 1) + 2 + 2 * (tx_n - 1) + 2;
     if (st++ < stages)
-      hipLaunchKernelGGL(k_ccl_edges, dim3(cdiv(std::max(p.crop_w, p.crop_h), 256), lines, p.B), blk, 0, s, a);
+      hipLaunchKernelGGL(k_ccl_edges, dim3(cdiv(std::max(p.crop_w, p.crop_h), kEdgeThreads), lines, p.B),
+                         dim3(kEdgeThreads), 0, s, a);
     const size_t lds = (size_t)(nt + 1 + 1024 + 2 * (kMergeCap + 1) + 1) * 4;
     if (lds > 160 * 1024) throw std::invalid_argument("postprocess: crop too large for the LDS merge");
     static bool attr = false;
@@ -1206,8 +1213,11 @@ void postprocess(const PostParams& p, hipStream_t s) {
     if (st++ < stages) hipLaunchKernelGGL(k_ccl_merge, dim3(p.B), dim3(1024), lds, s, a);
   }
   // strip-privatised pass: kQuadBlocks strips per frame (SSA_QUAD_BLOCKS overrides, tuning)
+  // rounds of 256 pixels per block chosen first, so no block ends with a near-empty round
+  // (771-pixel strips at 256 blocks per frame ran a 4th round for 3 pixels)
   const char* qb_env = getenv("SSA_QUAD_BLOCKS");
-  const int qblocks = qb_env ? std::max(1, atoi(qb_env)) : kQuadBlocks;
+  const int rounds = std::max(1, N / (256 * (qb_env ? std::max(1, atoi(qb_env)) : kQuadBlocks)));
+  const int qblocks = cdiv(N, 256 * rounds);
   if (st++ < stages) hipLaunchKernelGGL(k_accum, dim3(qblocks, p.B), blk, 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_assign, dim3(p.B), dim3(1024), 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_finalize, dim3(p.B), dim3(64), 0, s, a);
