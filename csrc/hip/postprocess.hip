@@ -169,8 +169,8 @@ __device__ void unite(int32_t* L, int a, int b) {
 }
 
 // ---------------------------------------------------------------- mask + local CCL
-// One 512-thread block = one TW x TH = 32 x 32 pixel tile, two pixels per thread
-// (rows ty and ty + 16), half a wave per tile row.
+// One 256-thread block = one TW x TH = 32 x 32 pixel tile, four pixels per thread
+// (rows ty + 8k), half a wave per tile row.
 //  1. mask: the tile's labels + 1-pixel REFLECT_101 halo are staged in LDS, the
 //     palette colours are box-summed separably (horizontal 3-sums in LDS, then
 //     vertical), rounded per channel like cv2.blur, converted with the fixed-point
@@ -216,13 +216,17 @@ __device__ void lunite(int* l, int a, int b) {
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
-// 512 threads per TW x TH tile: each thread owns RPT = TH / 16 pixels of one column
-// (rows ty + 16 k), so a block's global-load and barrier latency is paid once per
-// RPT pixels, and the bigger tile halves the cross-tile edges / tile-local roots
-// the merge handles.
-constexpr int kCclThreads = 512;
+// 256 threads per TW x TH tile: each thread owns RPT = TW * TH / 256 pixels of one
+// column (rows ty + 8 k), so a block's global-load and barrier latency is paid once per
+// RPT pixels (256 threads: 51 us per 32 bench frames vs 61 us at 512 and 94 us at 1024,
+// profiles/r3_post_ab.txt), and the 32 x 32 tile keeps the cross-tile edges / tile-local
+// roots the merge handles low.
+#ifndef SSA_CCL_THREADS
+#define SSA_CCL_THREADS 256
+#endif
+constexpr int kCclThreads = SSA_CCL_THREADS;
 constexpr int RPT = TH * TW / kCclThreads;
-static_assert(RPT * kCclThreads == TW * TH && TW == 32, "k_ccl_local: 32-wide tiles, 512 threads");
+static_assert(RPT * kCclThreads == TW * TH && TW == 32 && kCclThreads % 64 == 0, "k_ccl_local: 32-wide tiles");
 
 __global__ __launch_bounds__(kCclThreads) void k_ccl_local(KArgs a, const int32_t* __restrict__ pal) {
   constexpr int HW2 = TW + 2, HH2 = TH + 2, RS = kCclThreads / TW;  // RS: row stride of a thread's pixels
@@ -664,7 +668,7 @@ __device__ __forceinline__ int parent_of(const FrameWS& f, int cw, int n) {
 // component is reduced by shuffles first; a full table falls back to global
 // atomics, so correctness never depends on the table size.
 constexpr int kHash = 128;
-constexpr int kQuadBlocks = 256;  // blocks per frame for the strip-privatised accumulation pass
+constexpr int kQuadBlocks = 192;  // target blocks per frame of the accumulation pass (4 rounds of 256 px at 513 x 385: 229 vs 244 us at 3 rounds, 329 at 1; profiles/r3_post_ab.txt)
 
 struct QuadTable {
   int key[kHash];
@@ -793,17 +797,22 @@ __device__ __forceinline__ void hagg(AccTable& T, FrameWS& f, int cw, int bins, 
 //  * the pixel's class into its component's fill histogram, and into the ring
 //    histogram of each distinct hole it is 4-adjacent to (holes of its own component).
 // Round 2 ran this as three passes (k_quads, k_tree, k_hist: 92 us per 32 frames).
-__global__ __launch_bounds__(256) void k_accum(KArgs a) {
+#ifndef SSA_ACC_THREADS
+#define SSA_ACC_THREADS 256
+#endif
+constexpr int kAccThreads = SSA_ACC_THREADS;
+
+__global__ __launch_bounds__(kAccThreads) void k_accum(KArgs a) {
   __shared__ AccTable T;
   const int b = blockIdx.y;
   const int cw = a.cw, ch = a.ch, bins = a.bins;
   const int N = cw * ch;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
   f.fb = f.flag[0];
-  for (int i = threadIdx.x; i < kHash; i += 256) {
+  for (int i = threadIdx.x; i < kHash; i += kAccThreads) {
     T.q.key[i] = 0; T.q.s00[i] = 0; T.q.s10[i] = 0; T.q.s01[i] = 0;
   }
-  for (int i = threadIdx.x; i < kHistHash; i += 256) {
+  for (int i = threadIdx.x; i < kHistHash; i += kAccThreads) {
     T.hkey[i] = 0; T.hcnt[i] = 0;
   }
   if (threadIdx.x == 0) T.maxd = (a.dbg & 4) ? 0 : 65536;
@@ -811,7 +820,7 @@ __global__ __launch_bounds__(256) void k_accum(KArgs a) {
   const uint8_t* lab = a.labels + (size_t)b * a.H * a.W;
   const int per = (N + gridDim.x - 1) / gridDim.x;
   const int p0 = blockIdx.x * per, p1 = min(N, p0 + per);
-  for (int pb = p0; pb < p1; pb += 256) {
+  for (int pb = p0; pb < p1; pb += kAccThreads) {
     const int p = pb + threadIdx.x;
     int fnode = 0, f00 = 0;
     long long f10 = 0, f01 = 0;
@@ -925,11 +934,11 @@ __global__ __launch_bounds__(256) void k_accum(KArgs a) {
       if (__any(rkey[k] > 0)) hagg(T, f, cw, bins, rkey[k]);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < kHash; i += 256) {
+  for (int i = threadIdx.x; i < kHash; i += kAccThreads) {
     const int node = T.q.key[i];
     if (node != 0) moments_up(f, cw, node, T.q.s00[i], (long long)T.q.s10[i], (long long)T.q.s01[i], T.maxd);
   }
-  for (int i = threadIdx.x; i < kHistHash; i += 256) {
+  for (int i = threadIdx.x; i < kHistHash; i += kAccThreads) {
     const int key = T.hkey[i];
     if (key != 0) hist_up(f, cw, bins, key, T.hcnt[i], T.maxd);
   }
@@ -1217,8 +1226,8 @@ void postprocess(const PostParams& p, hipStream_t s) {
   // (771-pixel strips at 256 blocks per frame ran a 4th round for 3 pixels)
   const char* qb_env = getenv("SSA_QUAD_BLOCKS");
   const int rounds = std::max(1, N / (256 * (qb_env ? std::max(1, atoi(qb_env)) : kQuadBlocks)));
-  const int qblocks = cdiv(N, 256 * rounds);
-  if (st++ < stages) hipLaunchKernelGGL(k_accum, dim3(qblocks, p.B), blk, 0, s, a);
+  const int qblocks = cdiv(N, 256 * rounds) * (256 / kAccThreads);
+  if (st++ < stages) hipLaunchKernelGGL(k_accum, dim3(qblocks, p.B), dim3(kAccThreads), 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_assign, dim3(p.B), dim3(1024), 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_finalize, dim3(p.B), dim3(64), 0, s, a);
   check_launch("postprocess");

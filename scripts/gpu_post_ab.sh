@@ -15,6 +15,7 @@ for v in ${VERS:-old new}; do
   timeout -k 10 60 tools/bin/post_bench_$v 50 $O/bench_labels.bin || exit 1
 done
 for d in ${DBGS:-}; do echo "== s5 SSA_POST_DBG=$d"; SSA_POST_DBG=$d timeout -k 10 60 tools/bin/post_bench_s5 50 $O/bench_labels.bin || exit 1; done
+for q in ${QBS:-}; do echo "== new SSA_QUAD_BLOCKS=$q"; SSA_QUAD_BLOCKS=$q timeout -k 10 60 tools/bin/post_bench_new 50 $O/bench_labels.bin || exit 1; done
 cd /tmp && export TMPDIR=/tmp
 for v in ${VERS:-old new}; do
   timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $REPO/$O/$v -o run --output-format csv -- $REPO/tools/bin/post_bench_$v 20 $REPO/$O/bench_labels.bin only > $REPO/$O/$v.log 2>&1 || exit 2
