@@ -564,10 +564,19 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(KArgs a) {
     lunite(par, compact(ra), rb < 0 ? OUT : compact(rb));
   }
   __syncthreads();
-  for (int t = tid; t < nt; t += 1024) {
-    const int n = f.ntroot[t];
-    for (int c = 0; c < n; ++c)
-      atomicMin(&minr[lfind(par, toff[t] + c)], f.rootpix[(size_t)t * kTileRoots + c]);
+  // per compact node (not per tile: a tile's roots were one thread's serial chain of
+  // global loads): its tile by binary search over the tile offsets
+  auto tile_of = [&](int i) {  // last tile t with toff[t] <= i (empty tiles share offsets)
+    int lo = 0, hi = nt - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (toff[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+  };
+  for (int i = tid; i < R; i += 1024) {
+    const int t = tile_of(i);
+    atomicMin(&minr[lfind(par, i)], f.rootpix[(size_t)t * kTileRoots + (i - toff[t])]);
   }
   __syncthreads();
   const int outroot = lfind(par, OUT);
@@ -575,12 +584,10 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(KArgs a) {
   for (int i = tid; i < R; i += 1024)
     if (i != outroot && lds_ld(par + i) == i) add_root(f, a.bins, minr[i], s_nr);
   // final label of every tile-local root, over its cidx entry (compact() is done)
-  for (int t = tid; t < nt; t += 1024) {
-    const int n = f.ntroot[t];
-    for (int c = 0; c < n; ++c) {
-      const int r = lfind(par, toff[t] + c);
-      f.cidx[f.rootpix[(size_t)t * kTileRoots + c]] = r == outroot ? 0 : minr[r] + 1;
-    }
+  for (int i = tid; i < R; i += 1024) {
+    const int t = tile_of(i);
+    const int r = lfind(par, i);
+    f.cidx[f.rootpix[(size_t)t * kTileRoots + (i - toff[t])]] = r == outroot ? 0 : minr[r] + 1;
   }
   __syncthreads();
   // border-tree parent of every root: the final label of the pixel left of it
