@@ -674,7 +674,10 @@ __device__ __forceinline__ int parent_of(const FrameWS& f, int cw, int n) {
 // one global atomic per (block, component). A wave whose 64 lanes hit the same
 // component is reduced by shuffles first; a full table falls back to global
 // atomics, so correctness never depends on the table size.
-constexpr int kHash = 128;
+#ifndef SSA_KHASH
+#define SSA_KHASH 128  // 64 / 256 (with a 512 histogram table) measured equal / 5 us slower
+#endif
+constexpr int kHash = SSA_KHASH;  // per-block moments table (power of 2)
 constexpr int kQuadBlocks = 192;  // target blocks per frame of the accumulation pass (4 rounds of 256 px at 513 x 385: 229 vs 244 us at 3 rounds, 329 at 1; profiles/r3_post_ab.txt)
 
 struct QuadTable {
@@ -709,7 +712,10 @@ __device__ void hist_up(FrameWS& f, int cw, int bins, int key, int cnt, int maxd
     atomicAdd(f.th + (size_t)(n - 1) * bins + c, cnt);
 }
 
-constexpr int kHistHash = 256;
+#ifndef SSA_KHHASH
+#define SSA_KHHASH 256
+#endif
+constexpr int kHistHash = SSA_KHHASH;  // per-block histogram table (power of 2)
 
 struct AccTable {
   int maxd;  // ancestor levels a flush adds to (65536; 0 = SSA_POST_DBG bit 4 timing ablation)
