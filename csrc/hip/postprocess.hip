@@ -1238,7 +1238,10 @@ void postprocess(const PostParams& p, hipStream_t s) {
   // rounds of 256 pixels per block chosen first, so no block ends with a near-empty round
   // (771-pixel strips at 256 blocks per frame ran a 4th round for 3 pixels)
   const char* qb_env = getenv("SSA_QUAD_BLOCKS");
-  const int rounds = std::max(1, N / (256 * (qb_env ? std::max(1, atoi(qb_env)) : kQuadBlocks)));
+  // small batches get more, shorter strips so the grid still covers the 256 CUs (batch 1:
+  // 772 one-round blocks instead of 193 four-round blocks)
+  const int qtarget = qb_env ? std::max(1, atoi(qb_env)) : std::max(kQuadBlocks, 2048 / p.B);
+  const int rounds = std::max(1, N / (256 * qtarget));
   const int qblocks = cdiv(N, 256 * rounds) * (256 / kAccThreads);
   if (st++ < stages) hipLaunchKernelGGL(k_accum, dim3(qblocks, p.B), dim3(kAccThreads), 0, s, a);
   if (st++ < stages) hipLaunchKernelGGL(k_assign, dim3(p.B), dim3(1024), 0, s, a);
