@@ -157,8 +157,11 @@ class Engine:
     def _device_post(self, labels: torch.Tensor, out: Optional[torch.Tensor] = None):
         if self._hip_post is None:
             from ..postprocess.device import DevicePostprocess
+            # one histogram bin per model class (argmax labels are < num_classes): the
+            # per-root fill histograms are the largest part of the workspace
             self._hip_post = DevicePostprocess(self.device, self.H, self.W, self.palette,
-                                               self.cfg.max_segments)
+                                               self.cfg.max_segments,
+                                               bins=max(1, min(256, self.cfg.num_classes)))
         return self._hip_post.run(labels, self.crop_w, self.crop_h, self.min_area, out=out)
 
     def _use_device_post(self) -> bool:
