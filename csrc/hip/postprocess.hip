@@ -22,9 +22,10 @@
 //                histograms (component + everything it encloses; holes also get the
 //                parent's ring pixels), strip-privatised in LDS and added to every
 //                ancestor in the border tree at flush time (subtree sums)
-//   k_assign     contours whose polygon area >= min_area get a record slot
-//   k_finalize   majority label, score, centroid (OpenCV's double arithmetic),
-//                normalisation, records in findContours pre-order
+//   k_records    one workgroup per frame: contours whose polygon area >= min_area get
+//                a record slot (bitonic sort of the passing roots), then majority
+//                label, score, centroid (OpenCV's double arithmetic), normalisation,
+//                records in findContours pre-order
 #include "common.h"
 #include "kernels.h"
 
@@ -802,7 +803,7 @@ __device__ __forceinline__ void hagg(AccTable& T, FrameWS& f, int cw, int bins, 
 
 // ---------------------------------------------------------------- accumulate
 // One pass over the frame's pixels, strip-privatised per block, producing everything
-// k_select / k_finalize need for every component:
+// k_records needs for every component:
 //  * the 2x2 quad whose top-left corner is the pixel: polygon pieces (full square /
 //    triangle) as exact integer moments a00 = 2A, a10 = 6*int x, a01 = 6*int y
 //    (corner order TL, TR, BL, BR; triangle of corner k = k + its two quad neighbours,
@@ -958,14 +959,14 @@ __global__ __launch_bounds__(kAccThreads) void k_accum(KArgs a) {
 }
 
 // ---------------------------------------------------------------- select
-// k_assign (one workgroup per frame) hands the record slots to the first K passing
+// assign_frame (k_records, one workgroup per frame) hands the record slots to the first K passing
 // contours in raster order of their discovery pixel: the passing roots of the root
 // list are gathered in LDS and bitonic-sorted. The choice is deterministic (round 1
 // took them in atomicAdd order, so with more than K passing contours the kept subset
 // changed from run to run) and keeps the smallest discovery keys: among
 // siblings those come LAST in findContours order, so they are the records the
 // reference's LIFO buffer serves first (/root/reference/sem_seg_server.py:186-192,
-// 52-60). Contours past K are counted in nslot[1]; k_finalize flags the frame by a
+// 52-60). Contours past K are counted in nslot[1]; the finalize phase flags the frame by a
 // negative record count. Frames with more than kSortCap passing contours take a
 // raster-order scan of every pixel instead. (Round 2 ran a full-frame k_select pass
 // before this kernel: 20 us per 32 frames.)
@@ -977,13 +978,13 @@ __device__ __forceinline__ bool passes(const FrameWS& f, const KArgs& a, int p) 
 
 constexpr int kSortCap = 8192;
 
-__global__ __launch_bounds__(1024) void k_assign(KArgs a) {
+// (record slots handed out here are also kept in LDS, s_sn / s_res, for the finalize
+// phase of the same workgroup)
+__device__ __forceinline__ void assign_frame(const KArgs& a, FrameWS& f, int* s_sn, int* s_res) {
   __shared__ int s_key[kSortCap];
   __shared__ int s_cnt, s_w[16];
-  const int b = blockIdx.x, t = threadIdx.x;
+  const int t = threadIdx.x;
   const int N = a.ch * a.cw;
-  FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
-  f.fb = f.flag[0];
   if (t == 0) s_cnt = 0;
   __syncthreads();
   const int nroot = f.nslot[3];
@@ -1018,6 +1019,7 @@ __global__ __launch_bounds__(1024) void k_assign(KArgs a) {
       const int p = s_key[i];
       f.slot[p] = i;
       f.slot_node[i] = p + 1;
+      s_sn[i] = p + 1;
     }
   } else {
     const int wid = t >> 6, lane = t & 63;
@@ -1037,6 +1039,7 @@ __global__ __launch_bounds__(1024) void k_assign(KArgs a) {
       if (ok && rank < kept) {
         f.slot[p] = rank;
         f.slot_node[rank] = p + 1;
+        s_sn[rank] = p + 1;
       }
       base += tot;
       __syncthreads();
@@ -1045,7 +1048,10 @@ __global__ __launch_bounds__(1024) void k_assign(KArgs a) {
   if (t == 0) {
     f.nslot[0] = kept;
     f.nslot[1] = total - kept;
+    s_res[0] = kept;
+    s_res[1] = total - kept;
   }
+  __syncthreads();
 }
 
 // ---------------------------------------------------------------- finalize
@@ -1077,10 +1083,8 @@ __device__ bool precedes(const FrameWS& f, int cw, int a, int da, int b, int db)
   return disc_key(f, u) > disc_key(f, v);
 }
 
-__global__ __launch_bounds__(64) void k_finalize(KArgs a) {
-  const int b = blockIdx.x;
-  FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
-  f.fb = f.flag[0];
+__device__ __forceinline__ void finalize_frame(const KArgs& a, FrameWS& f, const int* s_sn, const int* s_res) {
+  const int b = blockIdx.x, NT = blockDim.x;
   float* rec = a.records + (size_t)b * (1 + 5 * a.K);
   __shared__ int s_node[256];
   __shared__ int s_path[256][kMaxDepth];
@@ -1089,12 +1093,12 @@ __global__ __launch_bounds__(64) void k_finalize(KArgs a) {
   __shared__ int s_emit[256];
   __shared__ float s_val[256][5];
   __shared__ int s_deep;
-  const int ns = min(*f.nslot, min(a.K, 256));
+  const int ns = min(s_res[0], min(a.K, 256));
   const int t = threadIdx.x;
   if (t == 0) s_deep = 0;
   __syncthreads();
-  for (int i = t; i < ns; i += 64) {
-    const int node = f.slot_node[i];
+  for (int i = t; i < ns; i += NT) {
+    const int node = s_sn[i];
     s_node[i] = node;
     // ancestor chain (top first) of discovery keys
     int chain[kMaxDepth];
@@ -1140,7 +1144,7 @@ __global__ __launch_bounds__(64) void k_finalize(KArgs a) {
   __syncthreads();
   // rank in pre-order: ancestor first; siblings by descending discovery key
   if (s_deep) {  // exact order at any depth: lift to equal depth, then walk to the LCA
-    for (int i = t; i < ns; i += 64) {
+    for (int i = t; i < ns; i += NT) {
       int rank = 0;
       const int di = node_depth(f, a.cw, s_node[i]);
       for (int j = 0; j < ns; ++j)
@@ -1149,7 +1153,7 @@ __global__ __launch_bounds__(64) void k_finalize(KArgs a) {
     }
     __syncthreads();
   }
-  for (int i = t; i < ns && !s_deep; i += 64) {
+  for (int i = t; i < ns && !s_deep; i += NT) {
     int rank = 0;
     for (int j = 0; j < ns; ++j) {
       if (j == i) continue;
@@ -1174,8 +1178,18 @@ __global__ __launch_bounds__(64) void k_finalize(KArgs a) {
       for (int c = 0; c < 5; ++c) rec[1 + 5 * n + c] = s_val[i][c];
       ++n;
     }
-    rec[0] = f.nslot[1] > 0 ? -(float)n : (float)n;  // negative: contours dropped past K
+    rec[0] = s_res[1] > 0 ? -(float)n : (float)n;  // negative: contours dropped past K
   }
+}
+
+// Record slots and records in ONE workgroup per frame (round 2: k_select + k_assign +
+// k_finalize, three launches): the slot assignment above, then the finalize phase.
+__global__ __launch_bounds__(1024) void k_records(KArgs a) {
+  __shared__ int s_sn[256], s_res[2];
+  FrameWS f = frame_ws(a.ws, a.lay, a.B, blockIdx.x);
+  f.fb = f.flag[0];
+  assign_frame(a, f, s_sn, s_res);
+  finalize_frame(a, f, s_sn, s_res);
 }
 
 }  // namespace
@@ -1244,8 +1258,7 @@ void postprocess(const PostParams& p, hipStream_t s) {
   const int rounds = std::max(1, N / (256 * qtarget));
   const int qblocks = cdiv(N, 256 * rounds) * (256 / kAccThreads);
   if (st++ < stages) hipLaunchKernelGGL(k_accum, dim3(qblocks, p.B), dim3(kAccThreads), 0, s, a);
-  if (st++ < stages) hipLaunchKernelGGL(k_assign, dim3(p.B), dim3(1024), 0, s, a);
-  if (st++ < stages) hipLaunchKernelGGL(k_finalize, dim3(p.B), dim3(64), 0, s, a);
+  if (st++ < stages) hipLaunchKernelGGL(k_records, dim3(p.B), dim3(1024), 0, s, a);
   check_launch("postprocess");
 }
 
