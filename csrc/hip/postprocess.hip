@@ -919,23 +919,47 @@ __global__ __launch_bounds__(kAccThreads) void k_accum(KArgs a) {
       // frames): a hole pixel credits each such neighbour r whose first 4-neighbour
       // (order left, right, up, down) inside the hole is this pixel, so r counts once.
       if (!fgp && np != 0 && !(a.dbg & 2)) {
-        const int par = parent_of(f, cw, np);
         const int nbr[4] = {x > 0 ? p - 1 : -1, x + 1 < cw ? p + 1 : -1, y > 0 ? p - cw : -1,
                             y + 1 < ch ? p + cw : -1};
+        bool fgn[4], any = false;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const int r = nbr[k];
-          if (r < 0 || !f.mask[r] || fin(f, r) != par) continue;
-          const int ry = r / cw, rx = r - ry * cw;
-          const int rn[4] = {rx > 0 ? r - 1 : -1, rx + 1 < cw ? r + 1 : -1, ry > 0 ? r - cw : -1,
-                             ry + 1 < ch ? r + cw : -1};
-          bool first = true;
-          for (int j = 0; j < 4 && rn[j] != p; ++j)
-            if (rn[j] >= 0 && !f.mask[rn[j]] && fin(f, rn[j]) == np) { first = false; break; }
-          if (!first) continue;
-          int rc = lab[ry * a.W + rx];
-          if (rc >= bins) rc = bins - 1;
-          rkey[k] = (np * bins + rc) * 2 + 1;
+          fgn[k] = nbr[k] >= 0 && f.mask[nbr[k]];
+          any |= fgn[k];
+        }
+        if (any) {  // interior hole pixels stop at the mask loads
+          const int par = parent_of(f, cw, np);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            if (!fgn[k]) continue;
+            const int r = nbr[k];
+            const int ry = r / cw, rx = r - ry * cw;
+            // r's 4-neighbours that precede this pixel in r's (left, right, up, down) order:
+            // this pixel is r's right (k = 0), left (k = 1), down (k = 2) or up (k = 3)
+            // neighbour; their labels are loaded together, not in a chain
+            int pre[3] = {-1, -1, -1};
+            if (k == 0) {
+              pre[0] = rx > 0 ? r - 1 : -1;
+            } else if (k == 2) {
+              pre[0] = rx > 0 ? r - 1 : -1;
+              pre[1] = rx + 1 < cw ? r + 1 : -1;
+              pre[2] = ry > 0 ? r - cw : -1;
+            } else if (k == 3) {
+              pre[0] = rx > 0 ? r - 1 : -1;
+              pre[1] = rx + 1 < cw ? r + 1 : -1;
+            }
+            const int fr = fin(f, r);
+            bool first = true;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+              const int q = pre[j];
+              if (q >= 0 && !f.mask[q] && fin(f, q) == np) first = false;
+            }
+            if (fr != par || !first) continue;
+            int rc = lab[ry * a.W + rx];
+            if (rc >= bins) rc = bins - 1;
+            rkey[k] = (np * bins + rc) * 2 + 1;
+          }
         }
       }
     }
