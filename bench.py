@@ -47,8 +47,10 @@ def main() -> int:
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
     p.add_argument("--backend", choices=["hip", "torch"], default="hip")
-    p.add_argument("--lag", type=int, default=2, choices=[1, 2],
-                   help="pipeline lag (2 = three steps in flight, the serving default)")
+    p.add_argument("--lag", type=int, default=2, choices=[0, 1, 2],
+                   help="pipeline lag (2 = three steps in flight, the throughput default; "
+                        "0 = one step in flight, records collected synchronously: the "
+                        "latency configuration)")
     p.add_argument("--arch", default="mnv2")
     p.add_argument("--aspp", default="full")
     p.add_argument("--input_size", type=int, default=513)
@@ -78,6 +80,10 @@ def main() -> int:
     a = p.parse_args()
     if a.serve:
         return _serve_bench(a)
+    # each rank's host threads and pinned staging on its GPU's NUMA node, before the first
+    # GPU call of the process (VERDICT r3 #3b; serving does the same in serve_distributed)
+    from semantic_segmentation_server_amd.parallel.affinity import pin_to_gpu_numa
+    pin_to_gpu_numa()
 
     import numpy as np
     import torch
@@ -154,6 +160,7 @@ def main() -> int:
     D.barrier(ctx)
     sync()
     rec0, fr0 = pipe.records_out, pipe.frames_done
+    pipe.reset_observations()
     t0 = time.perf_counter()
     run_steps(a.steps, a.warmup)
     sync()
@@ -166,6 +173,15 @@ def main() -> int:
     fps = frames_total / dt
     # records that reached the hub from the timed steps (rank 0 collects every rank's)
     timed_records, timed_frames = pipe.records_out - rec0, pipe.frames_done - fr0
+    # capture -> record-in-hub latency of the timed frames (rank 0 sees every rank's):
+    # capture = the host batch handed to the pipeline (its H2D starts); with lag L, L + 1
+    # steps are in flight, so this is ~(L + 1) step intervals plus the step's own time
+    lat = pipe.frame_latency.values()
+    frame_lat = {"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99))} \
+        if len(lat) else {"p50": None, "p99": None}
+    streams_seen = sorted(int(k) for k in pipe.stream_frames)
+    frames_collected = int(sum(pipe.stream_frames.values()))
+    order_errors = int(pipe.frame_order_errors)
 
     rpc = None
     if a.rpc > 0:
@@ -209,6 +225,11 @@ def main() -> int:
             },
             "p50_get_segmented_objects_ms": rpc.get("p50_ms") if rpc else None,
             "p99_get_segmented_objects_ms": rpc.get("p99_ms") if rpc else None,
+            "p50_frame_latency_ms": None if frame_lat["p50"] is None else round(frame_lat["p50"], 4),
+            "p99_frame_latency_ms": None if frame_lat["p99"] is None else round(frame_lat["p99"], 4),
+            "frames_collected": frames_collected,
+            "streams_collected": streams_seen,
+            "frame_order_errors": order_errors,
             "records_per_frame": round(timed_records / max(1, timed_frames), 4),
             "records_per_frame_under_rpc_load": (round(rpc["records"] / max(1, rpc["frames"]), 4)
                                                  if rpc and "records" in rpc else None),

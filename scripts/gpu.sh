@@ -1,0 +1,81 @@
+#!/bin/bash
+# One parameterised GPU runner (replaces the round-1..3 one-off gpu_*.sh scripts).
+#
+#   bash scripts/gpu.sh <outdir-name> <step> [<step> ...]
+#
+# steps (each runs under its own time limit; the first failure ends the call):
+#   tests        pytest -m gpu (whole suite, one process)
+#   tests:EXPR   pytest -m gpu -k EXPR
+#   smoke        __graft_entry__.smoke()
+#   bench        driver window x2 (python bench.py --steps 20 --warmup 5)
+#   bench100     100 timed steps, RPC under load
+#   b1           batch-1 bench (400 steps)
+#   cfg4         DeepLabv3-ResNet50 1025^2 int8 B=8 (60 steps) and bf16
+#   cfg5         4 camera streams x 8 frames (batched step)
+#   prof         sequential kernel trace of the B=32 step -> layer_times.txt
+#   profb1       sequential kernel trace of the B=1 step -> b1_layer_times.txt
+#   pmc          3 SQ counter passes over the sequential B=32 step -> pmc_summary.txt
+#   race         concurrent-plan determinism check (scripts/debug_race.py)
+#   py:SCRIPT    python SCRIPT (args in PY_ARGS)
+# Extra env: BENCH_ARGS is appended to every bench.py call.
+set -o pipefail
+cd "$(dirname "$0")/.."
+REPO=$PWD
+export SSA_NO_AUTOBUILD=1
+O=gpurun_out/${1:?outdir}
+shift
+mkdir -p $O
+PMC_SETS=(
+  "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_SMEM"
+  "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE"
+  "SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_MISC SQ_LDS_IDX_ACTIVE SQ_INSTS_BRANCH"
+)
+
+trace() {  # trace <name> <bench args...>: sequential-model kernel trace + layer table
+  local name=$1; shift
+  (cd /tmp && export TMPDIR=/tmp && SSA_SLOT_PARALLEL=0 timeout -k 10 400 rocprofv3 --kernel-trace --stats \
+    -d $REPO/$O/$name -o run --output-format csv -- python3 $REPO/bench.py "$@" --lag 1 --rpc 0 $BENCH_ARGS \
+    > $REPO/$O/$name.log 2>&1) || { echo "trace $name failed"; tail -5 $O/$name.log; return 1; }
+  python3 scripts/layer_times.py $(ls $O/$name/*/run_kernel_trace.csv 2>/dev/null || ls $O/$name/run_kernel_trace.csv) \
+    > $O/${name}_layer_times.txt && tail -45 $O/${name}_layer_times.txt
+}
+
+bench() {  # bench <tag> <seconds> <args...>
+  local tag=$1 t=$2; shift 2
+  timeout -k 10 $t python bench.py "$@" $BENCH_ARGS > $O/bench_$tag.json 2> $O/bench_$tag.err \
+    || { echo "bench $tag failed rc=$?"; grep -v "^frame" $O/bench_$tag.err | tail -8; return 1; }
+  cut -c1-400 $O/bench_$tag.json
+}
+
+for step in "$@"; do
+  echo "== $step"
+  case $step in
+    tests)   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+               > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }; tail -2 $O/pytest.txt ;;
+    tests:*) timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread \
+               -k "${step#tests:}" > $O/pytest_k.txt 2>&1 || { tail -30 $O/pytest_k.txt; exit 1; }; tail -5 $O/pytest_k.txt ;;
+    smoke)   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 \
+               || { tail -20 $O/smoke.txt; exit 1; }; tail -3 $O/smoke.txt ;;
+    bench)   bench d1 300 --steps 20 --warmup 5 && bench d2 300 --steps 20 --warmup 5 || exit 2 ;;
+    bench100) bench s100 300 --steps 100 --warmup 10 || exit 2 ;;
+    b1)      bench b1 300 --batch 1 --steps 400 --warmup 50 --rpc 0 || exit 2 ;;
+    cfg4)    bench c4i8 400 --arch resnet50 --input_size 1025 --camera 2048x1024 --batch 8 --dtype int8 --steps 60 --warmup 5 --rpc 0 \
+               && bench c4bf 400 --arch resnet50 --input_size 1025 --camera 2048x1024 --batch 8 --steps 60 --warmup 5 --rpc 0 || exit 2 ;;
+    cfg5)    bench c5 300 --streams 4 --batch 32 --steps 100 --warmup 10 --rpc 0 || exit 2 ;;
+    prof)    trace seq --steps 5 --warmup 2 || exit 3 ;;
+    profb1)  trace b1seq --batch 1 --steps 20 --warmup 5 || exit 3 ;;
+    pmc)     i=0
+             for set in "${PMC_SETS[@]}"; do
+               i=$((i+1))
+               (cd /tmp && export TMPDIR=/tmp && SSA_SLOT_PARALLEL=0 timeout -s KILL 180 rocprofv3 --pmc $set \
+                 -d $REPO/$O/pmc$i -o run --output-format csv -- python3 $REPO/bench.py --steps 3 --warmup 1 --lag 1 --rpc 0 $BENCH_ARGS \
+                 > $REPO/$O/pmc$i.log 2>&1) || { echo "pmc set $i failed"; tail -5 $O/pmc$i.log; exit 4; }
+             done
+             python3 scripts/pmc_summary.py $O/pmc1 $O/pmc2 $O/pmc3 > $O/pmc_summary.txt 2>&1; head -60 $O/pmc_summary.txt ;;
+    race)    timeout -k 10 600 python scripts/debug_race.py $RACE_ARGS > $O/race.txt 2>&1 || { tail -20 $O/race.txt; exit 5; }; tail -5 $O/race.txt ;;
+    py:*)    timeout -k 10 ${PY_TIMEOUT:-600} python -u ${step#py:} $PY_ARGS > $O/$(basename ${step#py:} .py).txt 2>&1 \
+               || { tail -30 $O/$(basename ${step#py:} .py).txt; exit 6; }; tail -${PY_TAIL:-40} $O/$(basename ${step#py:} .py).txt ;;
+    *)       echo "unknown step $step"; exit 9 ;;
+  esac
+done
+echo "== all steps ok"

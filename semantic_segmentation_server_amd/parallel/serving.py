@@ -59,7 +59,16 @@ class DistributedServer:
         # beside it for the heartbeat / control traffic; gloo alone on CPU ranks or when
         # the host gather is asked for
         gpu = torch.cuda.is_available() and cfg.device != "cpu"
-        pg = "nccl" if gpu and (cfg.ingest == "scatter" or cfg.gather in ("auto", "rccl")) else "gloo"
+        # record gather: with P-1 degradation on (the serving default) the gather stays on
+        # the host (pinned memory over gloo). An RCCL gather kernel whose peer died never
+        # completes, and the survivors' result streams would stay blocked behind it after
+        # the group is re-formed; --no_degrade (or --gather rccl) keeps the
+        # RCCL data path, which bench.py measures. The pipeline's completion wait polls
+        # for a peer's abort key on that path, so a lost peer still surfaces as PeerLost.
+        self.gather = cfg.gather
+        if self.gather == "auto" and cfg.degrade:
+            self.gather = "host"
+        pg = "nccl" if gpu and (cfg.ingest == "scatter" or self.gather in ("auto", "rccl")) else "gloo"
         self.ctx = ctx or D.init(pg, timeout_s=cfg.rank_timeout,
                                  device="cuda" if torch.cuda.is_available() and cfg.device != "cpu"
                                  else "auto")
@@ -105,8 +114,10 @@ class DistributedServer:
             self.feeder.start()
         pipe = DataParallelPipeline(ctx, self.engine, self.camera_res[0], self.camera_res[1],
                                     self.cfg.batch, self._ingest, self.hub, self.S, lag=1,
-                                    gather=self.cfg.gather)
+                                    gather=self.gather)
         pipe.tracer = self.tracer
+        pipe.metrics = self.metrics
+        pipe.rank_timeout_s = float(self.cfg.rank_timeout)
         self.driver = PipelineDriver(pipe, self.feeder, self.tracer, self.metrics)
         self._started = False
 

@@ -92,6 +92,7 @@ class Producer(threading.Thread):
                                         len(self.sources), lag=1)
             if tr is not None:
                 pipe.tracer = tr
+            pipe.metrics = self.metrics  # capture -> record frame latency (frame_latency_ms)
             drv = PipelineDriver(pipe, feeder, tr, self.metrics)
             first = drv.next_batch()
             if first is None:

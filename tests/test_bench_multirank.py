@@ -1,0 +1,53 @@
+"""The driver's multi-GPU command, rehearsed on the CPU (VERDICT r3 #3c).
+
+The driver launches ``python -m torch.distributed.run --nnodes=1 --nproc-per-node N
+--master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W`` on an
+8-GPU node. The same command runs here over gloo with the torch backend at a small input:
+the JSON line must come from rank 0 alone, count every rank, and the frames collected on
+rank 0 must carry every rank's stream id with per-stream frame ids in order (one lost,
+duplicated or overwritten metadata slot breaks that)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world,ingest", [(2, "local"), (3, "local"), (2, "scatter")])
+def test_bench_torchrun_cpu(world, ingest):
+    steps, warmup, batch = 3, 1, 2
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1", SSA_NUMA_PIN="0",
+               CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", str(steps),
+           "--warmup", str(warmup), "--backend", "torch", "--input_size", "129",
+           "--batch", str(batch), "--rpc", "0", "--ingest", ingest]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 prints the one JSON line
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == world
+    assert out["steps"] == steps and out["warmup"] == warmup
+    assert out["config"]["global_batch"] == batch * world
+    assert out["config"]["parallelism"] == f"dp{world}"
+    assert out["value"] > 0 and out["ms_per_step"] > 0
+    # every rank's frames reached rank 0, tagged with their own stream, ids in order
+    assert out["frames_collected"] == steps * batch * world
+    assert out["streams_collected"] == list(range(world))
+    assert out["frame_order_errors"] == 0
+    assert out["p50_frame_latency_ms"] is not None and out["p50_frame_latency_ms"] > 0
