@@ -16,6 +16,7 @@
 #   profb1       sequential kernel trace of the B=1 step -> b1_layer_times.txt
 #   pmc          3 SQ counter passes over the sequential B=32 step -> pmc_summary.txt
 #   race         concurrent-plan determinism check (scripts/debug_race.py)
+#   repro        packed-f32 co-residence reproducer, both builds (csrc/tools/packed_f32_repro.hip)
 #   py:SCRIPT    python SCRIPT (args in PY_ARGS)
 # Extra env: BENCH_ARGS is appended to every bench.py call.
 set -o pipefail
@@ -73,6 +74,8 @@ for step in "$@"; do
              done
              python3 scripts/pmc_summary.py $O/pmc1 $O/pmc2 $O/pmc3 > $O/pmc_summary.txt 2>&1; head -60 $O/pmc_summary.txt ;;
     race)    timeout -k 10 600 python scripts/debug_race.py $RACE_ARGS > $O/race.txt 2>&1 || { tail -20 $O/race.txt; exit 5; }; tail -5 $O/race.txt ;;
+    repro)   for b in repro_pk repro_nopk; do timeout -k 10 300 tools/bin/$b ${REPRO_REPS:-400} > $O/$b.txt 2>&1 \
+               || { tail -5 $O/$b.txt; exit 7; }; cat $O/$b.txt; done ;;
     py:*)    timeout -k 10 ${PY_TIMEOUT:-600} python -u ${step#py:} $PY_ARGS > $O/$(basename ${step#py:} .py).txt 2>&1 \
                || { tail -30 $O/$(basename ${step#py:} .py).txt; exit 6; }; tail -${PY_TAIL:-40} $O/$(basename ${step#py:} .py).txt ;;
     *)       echo "unknown step $step"; exit 9 ;;

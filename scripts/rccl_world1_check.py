@@ -2,9 +2,11 @@
 a real RCCL process group (SSA_FORCE_PG=1, backend nccl) with the gloo control group,
 the DP pipeline in its default gather mode (auto -> RCCL record + metadata gather to
 rank 0, then the pinned-host write kernel), lag 2 on slot-parallel plan copies; the
-records must equal an eager synchronous engine's on the same frames. Prints
-'OK gather=<mode> pg=<backend> records=<n>' (tests/test_hip_kernels.py runs it in a
-child process so the process group does not outlive it)."""
+records must equal an eager synchronous engine's on the same frames. ``scatter`` as the
+first argument: rank 0 uploads the node batch and RCCL-scatters it on the slot streams
+(X1, VERDICT r3 #3d). Prints 'OK gather=<mode> pg=<backend> records=<n>'
+(tests/test_hip_kernels.py runs it in a child process so the process group does not
+outlive it)."""
 import os
 import sys
 
@@ -36,7 +38,9 @@ for k in range(6):
     want.extend(zip(r["frame"].tolist(), r["label"].tolist(), r["area"].round(6).tolist()))
 torch.cuda.synchronize()
 hub = ResultHub(1)
-pipe = DataParallelPipeline(ctx, eng, 160, 120, 2, "local", hub, lag=1)  # auto: lag 2, RCCL gather
+ingest = sys.argv[1] if len(sys.argv) > 1 else "local"
+pipe = DataParallelPipeline(ctx, eng, 160, 120, 2, ingest, hub, lag=1)  # auto: lag 2, RCCL gather
+assert pipe.lag == 2 and eng.slot_parallel, (pipe.lag, eng.slot_parallel)
 got = []
 pipe.prefetch(batches[0].pin_memory())
 for k in range(6):
@@ -49,5 +53,7 @@ assert len(want) > 0
 assert sorted(got) == sorted(want), (len(got), len(want))
 assert hub.depth == len(want)
 D.barrier(ctx)
-print(f"OK gather={pipe.gather_mode} pg={ctx.backend} lag={pipe.lag} records={len(got)}", flush=True)
+assert pipe.frame_order_errors == 0 and sum(pipe.stream_frames.values()) == 12
+print(f"OK ingest={ingest} gather={pipe.gather_mode} pg={ctx.backend} lag={pipe.lag} records={len(got)}",
+      flush=True)
 D.destroy(ctx)

@@ -629,11 +629,13 @@ def test_engine_bound_input_graphs(split):
     assert len(eng._bound_graphs) == 2
 
 
-def test_rccl_world1_pipeline_records_match_eager():
+@pytest.mark.parametrize("ingest", ["local", "scatter"])
+def test_rccl_world1_pipeline_records_match_eager(ingest):
     """The multi-GPU default data path (RCCL process group + gloo control group, RCCL
-    record gather, lag 2 slot-parallel) rehearsed at world size 1 on this GPU
-    (SSA_FORCE_PG=1): records equal the eager engine's (scripts/rccl_world1_check.py,
-    in a child process so its process group does not leak into other tests)."""
+    record gather, lag 2 slot-parallel; with ``scatter`` also the RCCL frame scatter on
+    the slot streams) rehearsed at world size 1 on this GPU (SSA_FORCE_PG=1): records
+    equal the eager engine's (scripts/rccl_world1_check.py, in a child process so its
+    process group does not leak into other tests)."""
     import os
     import socket
     import subprocess
@@ -645,10 +647,10 @@ def test_rccl_world1_pipeline_records_match_eager():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, SSA_FORCE_PG="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
-    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "rccl_world1_check.py")],
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "rccl_world1_check.py"), ingest],
                        env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-    assert "OK gather=rccl pg=nccl lag=2" in r.stdout, r.stdout
+    assert f"OK ingest={ingest} gather=rccl pg=nccl lag=2" in r.stdout, r.stdout
 
 
 @pytest.mark.parametrize("lag", [0, 1, 2])
