@@ -158,6 +158,11 @@ void fused_ir_band(const FusedBandParams& p, hipStream_t s);
 size_t fused_ir_band_lds(int stride, int hidP, int OW, int blob_bytes, int nslot, int hs = 1, int Cout = 0,
                          int split = 1);
 int fused_ir_band_cols(int stride);
+// Hidden-sliced variant (fused_ir_slice.hip): waves = nw column groups x hidP/32 hidden
+// chunks, each wave's chunk weights in VGPRs; same blob as fused_ir_band (hs / split /
+// nslot / blob_bytes unused).
+void fused_ir_slice(const FusedBandParams& p, int nw, hipStream_t s);
+size_t fused_ir_slice_lds(int stride, int hidP, int OW, int Cout, int nw);
 // Fused stem (3x3 s2, 3 -> 32, relu6, letterbox gather) + MobileNetV2 block 0
 // (dw 3x3 on 32 ch + relu6, project 32 -> 16); weights: ws [32][32] bf16 with
 // K = (ky*3+kx)*3 + c (RGB), bs [32] f32, wd [9][32] f16, bd [32] f16, wp [16][32] f16, bp [16].

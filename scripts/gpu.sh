@@ -17,6 +17,8 @@
 #   pmc          3 SQ counter passes over the sequential B=32 step -> pmc_summary.txt
 #   race         concurrent-plan determinism check (scripts/debug_race.py)
 #   repro        packed-f32 co-residence reproducer, both builds (csrc/tools/packed_f32_repro.hip)
+#   retune:LIST  re-time the named choices (comma list) at B = ${TUNE_B:-32} on top of the committed
+#                picks -> $O/tune.json (copy into assets/tune_mi355x.json to commit)
 #   py:SCRIPT    python SCRIPT (args in PY_ARGS)
 # Extra env: BENCH_ARGS is appended to every bench.py call.
 set -o pipefail
@@ -76,6 +78,11 @@ for step in "$@"; do
     race)    timeout -k 10 600 python scripts/debug_race.py $RACE_ARGS > $O/race.txt 2>&1 || { tail -20 $O/race.txt; exit 5; }; tail -5 $O/race.txt ;;
     repro)   for b in repro_pk repro_nopk; do timeout -k 10 300 tools/bin/$b ${REPRO_REPS:-400} > $O/$b.txt 2>&1 \
                || { tail -5 $O/$b.txt; exit 7; }; cat $O/$b.txt; done ;;
+    retune:*) [ -f $O/tune.json ] || cp assets/tune_mi355x.json $O/tune.json
+             SSA_TUNE_FILE=$O/tune.json SSA_RETUNE_ONLY=${step#retune:} SSA_LOG_AUTOTUNE=1 \
+               timeout -k 10 600 python bench.py --batch ${TUNE_B:-32} --steps 5 --warmup 2 --rpc 0 \
+               > $O/retune_b${TUNE_B:-32}.json 2> $O/retune_b${TUNE_B:-32}.err || { tail -20 $O/retune_b${TUNE_B:-32}.err; exit 8; }
+             grep "autotune" $O/retune_b${TUNE_B:-32}.err | grep -v "picks from" | cut -c1-1500 ;;
     py:*)    timeout -k 10 ${PY_TIMEOUT:-600} python -u ${step#py:} $PY_ARGS > $O/$(basename ${step#py:} .py).txt 2>&1 \
                || { tail -30 $O/$(basename ${step#py:} .py).txt; exit 6; }; tail -${PY_TAIL:-40} $O/$(basename ${step#py:} .py).txt ;;
     *)       echo "unknown step $step"; exit 9 ;;

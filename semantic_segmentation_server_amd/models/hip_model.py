@@ -655,8 +655,36 @@ class HipDeepLab:
                                 split=split: FB.fused_ir_band(x, bp_, out, B=B, IH=h, IW=w, stride=s.stride,
                                                               residual=s.residual, R=R, nslot=nslot, hs=hs,
                                                               split=split)]))
+        if blk["expand"] is not None:
+            # hidden-sliced row streaming: wave = column group x 32 hidden channels, the
+            # chunk's weights in VGPRs (fused_ir_slice.hip: the band kernel's LDS weight
+            # re-reads were its bottleneck)
+            for nw in FB.slice_widths(s.cin, hid, s.cout, s.stride, s.dilation):
+                if "band" not in blk:
+                    blk["band"] = self._pack_band(blk, s)
+                bp_ = blk["band"]
+                if FB.slice_lds(bp_, s.stride, OW, nw) > 160 * 1024:
+                    continue
+                twmax = 16 * nw - (2 if s.stride == 1 else 1)
+                nbx = -(-OW // twmax)
+                for R in self._slice_rows(B, OH, nbx):
+                    variants.insert(0, (f"slice{R}w{nw}", [
+                        lambda *_, x=inp, out=out, h=h, w=w, R=R, nw=nw, bp_=bp_: FB.fused_ir_slice(
+                            x, bp_, out, B=B, IH=h, IW=w, stride=s.stride, residual=s.residual,
+                            R=R, nw=nw)]))
         outer_ops.append(Choice(f"block{i}", variants))
         return out, OH, OW, s.cout
+
+    @staticmethod
+    def _slice_rows(B: int, OH: int, nbx: int) -> List[int]:
+        """Rows per band for fused_ir_slice (one 12-15-wave workgroup per CU): grids of
+        ~1, 2, 3 and 4 workgroups per CU (256 CUs)."""
+        out = []
+        for target in (256, 512, 768, 1024):
+            R = min(max(2, -(-B * nbx * OH // target)), OH)
+            if R not in out:
+                out.append(R)
+        return out
 
     def _pack_band(self, blk: dict, s) -> dict:
         m = blk["module"]

@@ -130,6 +130,55 @@ def fused_ir_band(x: torch.Tensor, packed: Dict, out: torch.Tensor, *, B: int, I
     return out
 
 
+# ------------------------------------------------------------------ hidden-sliced variant
+# (stride, hidP / 32, ceil(Cout / 16), column groups) instantiated in fused_ir_slice.hip;
+# waves per workgroup = column groups x hidden chunks <= 16
+SLICE_SHAPES = {(2, 3, 2, 5), (2, 3, 2, 4), (1, 5, 2, 3), (1, 5, 2, 2), (2, 5, 2, 3), (2, 5, 2, 2),
+                (1, 6, 2, 2), (2, 6, 4, 2), (1, 6, 2, 1), (2, 6, 4, 1)}
+
+
+def slice_supported(cin: int, hid: int, cout: int, stride: int, dil: int, nw: int) -> bool:
+    hidP = -(-hid // 32) * 32
+    return (dil == 1 and cin <= 32 and cin % 8 == 0 and stride in (1, 2)
+            and (stride, hidP // 32, -(-cout // 16), nw) in SLICE_SHAPES)
+
+
+def slice_widths(cin: int, hid: int, cout: int, stride: int, dil: int) -> list:
+    """Column-group counts instantiated for this block, widest first."""
+    return sorted((nw for nw in range(1, 9) if slice_supported(cin, hid, cout, stride, dil, nw)),
+                  reverse=True)
+
+
+def slice_lds(packed: Dict, stride: int, OW: int, nw: int) -> int:
+    from .hip_ops import _hip_mod
+    return int(_hip_mod().fused_ir_slice_lds(stride, packed["hidP"], OW, packed["Cout"], nw))
+
+
+def fused_ir_slice(x: torch.Tensor, packed: Dict, out: torch.Tensor, *, B: int, IH: int, IW: int,
+                   stride: int, residual: bool, R: int = 8, nw: int = 2) -> torch.Tensor:
+    """Launch fused_ir_slice_kernel (csrc/hip/fused_ir_slice.hip): the band kernel's row
+    streaming with waves = nw column groups x hidden chunks of 32, each wave's chunk
+    weights held in VGPRs. Same blob as fused_ir_band; bit-identical results."""
+    from .hip_ops import _chk, _dbg, _hip_mod, _ptr, _stream
+    Cin, Cout = packed["Cin"], packed["Cout"]
+    OH, OW = (IH - 1) // stride + 1, (IW - 1) // stride + 1
+    if residual and (stride != 1 or Cin != Cout):
+        raise ValueError("fused_ir_slice: residual needs stride 1 and Cin == Cout")
+    if R < 1 or not slice_supported(Cin, packed["hid"], Cout, stride, 1, nw):
+        raise ValueError("fused_ir_slice: no instantiation for this block / width")
+    _chk(x, torch.bfloat16, "x", B * IH * IW * Cin)
+    _chk(out, torch.bfloat16, "out", B * OH * OW * Cout)
+    _chk(packed["blob"], torch.uint8, "blob", packed["blob_bytes"])
+    if slice_lds(packed, stride, OW, nw) > 160 * 1024:
+        raise ValueError("fused_ir_slice: LDS over 160 KiB")
+    _hip_mod().fused_ir_slice(_ptr(x), _ptr(packed["blob"]), _ptr(out), B, IH, IW, Cin, OH, OW, Cout,
+                              packed["hidP"], stride, int(bool(residual)), R, packed["o_be"],
+                              packed["o_wd"], packed["o_bd"], packed["o_wp"], packed["o_bp"], nw,
+                              _stream())
+    _dbg("fused_ir_slice")
+    return out
+
+
 # ----------------------------------------------------------------------------- emulation
 def emulate_fused_band(x: np.ndarray, packed: Dict, *, stride: int, residual: bool) -> np.ndarray:
     """Numpy re-execution of the kernel's math from the packed blob. x: [B, H, W, Cin]

@@ -1306,6 +1306,49 @@ def test_fused_ir_band(cin, cout, stride, H, W, R, nslot):
             assert _rel(out.cpu().float(), torch.from_numpy(emu)) < 5e-3, (hs, sp)
 
 
+@pytest.mark.parametrize("cin,cout,stride,H,W", [
+    (16, 24, 2, 257, 257),   # block 1
+    (24, 24, 1, 129, 129),   # block 2 (residual)
+    (24, 32, 2, 129, 129),   # block 3
+    (32, 32, 1, 65, 65),     # blocks 4-5 (residual)
+    (32, 64, 2, 65, 65),     # block 6
+    (24, 24, 1, 100, 129),   # rows not a multiple of R
+    (32, 32, 1, 7, 65),      # fewer rows than R
+])
+@pytest.mark.parametrize("R", [8, 5, 17])
+def test_fused_ir_slice(cin, cout, stride, H, W, R):
+    """Hidden-sliced row-streaming block (one wave per column group x hidden chunk, the
+    chunk's weights in VGPRs): vs the fp32 torch block, and bit-identical to the band
+    kernel (same blob, same accumulation order) at every instantiated width."""
+    from semantic_segmentation_server_amd.ops import fused_band as FB
+    from test_fused_band_cpu import band_block, pack_band  # tests/ is on sys.path
+    blk, spec = band_block(cin, cout, stride, seed=cin * 5 + cout + stride)
+    g = torch.Generator().manual_seed(37)
+    B = 2
+    x = torch.randn(B, cin, H, W, generator=g).to(torch.bfloat16)
+    with torch.no_grad():
+        ref = blk(x.float())
+    packed = pack_band(blk, spec, device=DEV)
+    OH, OW = (H - 1) // stride + 1, (W - 1) // stride + 1
+    widths = FB.slice_widths(cin, spec.hidden, cout, stride, 1)
+    assert widths
+    xd = _nhwc(x).to(DEV)
+    band = None
+    if FB.band_supported(cin, spec.hidden, cout, stride, 1, OW):
+        band = torch.full((B, OH, OW, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
+        FB.fused_ir_band(xd, packed, band, B=B, IH=H, IW=W, stride=stride, residual=spec.residual,
+                         R=R, nslot=2)
+    for nw in widths:
+        out = torch.full((B, OH, OW, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
+        FB.fused_ir_slice(xd, packed, out, B=B, IH=H, IW=W, stride=stride, residual=spec.residual,
+                          R=R, nw=nw)
+        torch.cuda.synchronize()
+        assert torch.isfinite(out).all(), nw
+        assert _rel(_nchw(out).cpu(), ref) < 2e-2, nw
+        if band is not None:
+            assert torch.equal(out, band), (nw, (out.float() - band.float()).abs().max().item())
+
+
 def test_multistream_batched_step_tags_streams():
     """Config 5 as one batched step: 4 camera streams x 2 frames fill one 8-frame graph
     replay; every record lands in its own stream's hub buffer (v2 per-stream reads) with a
