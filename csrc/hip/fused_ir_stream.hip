@@ -490,6 +490,11 @@ void fused_ir_stream(const FusedSpanParams& p, hipStream_t st) {
   // dilation 1 (halo <= 16 groups: 4 rounds per expansion wave) and 2 (<= 20: 5 rounds)
   if (p.W != 33 || p.dil > 2 || p.nh_max > (p.dil == 1 ? 4 : 5) * 64)
     throw std::invalid_argument("fused_ir_stream: W 33, dilation 1/2, halo <= 256/320 px");
+  // an unknown variant, or the 12-wave variant where it is not instantiated, must not
+  // silently launch another kernel under the requested name
+  if (p.npi < 0 || p.npi > 2) throw std::invalid_argument("fused_ir_stream: variant must be 0, 1 or 2");
+  if (p.npi == 2 && (p.dil != 1 || NS > 6))
+    throw std::invalid_argument("fused_ir_stream: the 12-wave variant needs dilation 1 and Cout <= 96");
   // 12-wave variant: blocks 7-12 (Cout <= 96; at Cout 160 the accumulators spill at 168 VGPRs)
 #define STREAM12(K_, N_) ((N_) <= 6 ? 2 : 0)
 #define STREAM(K_, N_)                                   \

@@ -815,6 +815,8 @@ __device__ __forceinline__ void hagg(AccTable& T, FrameWS& f, int cw, int bins, 
 #define SSA_ACC_THREADS 256
 #endif
 constexpr int kAccThreads = SSA_ACC_THREADS;
+static_assert(kAccThreads >= 64 && kAccThreads <= 256 && 256 % kAccThreads == 0,
+              "k_accum: 64, 128 or 256 threads (the strip grid is counted in 256-pixel rounds)");
 
 __global__ __launch_bounds__(kAccThreads) void k_accum(KArgs a) {
   __shared__ AccTable T;
@@ -1237,20 +1239,29 @@ void postprocess(const PostParams& p, hipStream_t s) {
   a.ws = static_cast<char*>(p.ws);
   a.lay = layout(p.H, p.W, p.K, p.num_bins);
   a.records = p.records;
+  a.dbg = 0;
+#ifdef SSA_POST_DEBUG
+  // ablation / staging knobs: debug builds only (-DSSA_POST_DEBUG), never in the
+  // production launch path
   {
     const char* e = getenv("SSA_POST_DBG");
     a.dbg = e ? atoi(e) : 0;
   }
+#endif
   // the per-frame counters are zeroed inside k_ccl_local (a kernel, not hipMemsetAsync:
   // a memset node captured by torch.cuda.graph faulted on its second replay on ROCm 7.x)
   const int N = p.crop_h * p.crop_w;
   const dim3 blk(256);
   const dim3 gp(cdiv(N, 256), p.B);
   // SSA_POST_STAGES=n (debug) launches only the first n stages
+#ifdef SSA_POST_DEBUG
   const int stages = [] {  // read per call (host only; graph capture records one value)
     const char* e = getenv("SSA_POST_STAGES");
     return e ? atoi(e) : 99;
   }();
+#else
+  constexpr int stages = 99;
+#endif
   int st = 0;
   const dim3 gt(cdiv(p.crop_w, TW), cdiv(p.crop_h, TH), p.B);
   if (st++ < stages) hipLaunchKernelGGL(k_ccl_local, gt, dim3(kCclThreads), 0, s, a, p.palette);
@@ -1275,7 +1286,11 @@ void postprocess(const PostParams& p, hipStream_t s) {
   // strip-privatised pass: kQuadBlocks strips per frame (SSA_QUAD_BLOCKS overrides, tuning)
   // rounds of 256 pixels per block chosen first, so no block ends with a near-empty round
   // (771-pixel strips at 256 blocks per frame ran a 4th round for 3 pixels)
+#ifdef SSA_POST_DEBUG
   const char* qb_env = getenv("SSA_QUAD_BLOCKS");
+#else
+  const char* qb_env = nullptr;
+#endif
   // small batches get more, shorter strips so the grid still covers the 256 CUs (batch 1:
   // 772 one-round blocks instead of 193 four-round blocks)
   const int qtarget = qb_env ? std::max(1, atoi(qb_env)) : std::max(kQuadBlocks, 2048 / p.B);

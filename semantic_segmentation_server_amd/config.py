@@ -72,6 +72,7 @@ class Config:
     debug_dump: Optional[str] = None       # directory for annotated PNG frames (reference :196-205)
     debug_every: int = 0                   # dump every N-th frame (0 = off)
     debug_sync: bool = False               # HIP_LAUNCH_BLOCKING=1, eager launches
+    supervise: bool = True                 # single-GPU CLI: GPU work in a supervised child process
 
     @property
     def min_area(self) -> float:
@@ -145,6 +146,9 @@ def add_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--debug_sync", action="store_true",
                    help="synchronous kernel launches (HIP_LAUNCH_BLOCKING=1, no hipGraph) so a "
                         "faulting kernel is reported at its own launch")
+    p.add_argument("--no_supervise", dest="supervise", action="store_false",
+                   help="run the GPU pipeline in the serving process itself (no restart of a "
+                        "faulted worker)")
     return p
 
 

@@ -275,7 +275,8 @@ class HipDeepLab:
         def buf(name, *shape, dtype=torch.bfloat16):
             # zeroed for tidiness only: no picked kernel reads plan bytes it did not write
             # (scripts/debug_poison.py run B: NaN-filled buffers give bit-identical labels;
-            # tests/test_hip_kernels.py::test_plan_independent_of_buffer_contents)
+            # tests/test_hip_kernels.py::test_plan_is_a_function_of_the_frame, at 257^2 and
+            # at the headline 513^2 / 640x480 shape with the B = 32 plan's kernels)
             if guard:  # debug (scripts/debug_guard.py): 0x5A bands before and after
                 n = 1
                 for d_ in shape:

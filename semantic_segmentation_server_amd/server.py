@@ -96,6 +96,19 @@ def main(argv=None) -> int:
         from .parallel.serving import serve_distributed
         return serve_distributed(cfg)
     print("Loading {} with {} labels.".format(cfg.model or f"random-init {cfg.arch}", cfg.labels))
+    if cfg.supervise and not cfg.debug_dump:
+        # the GPU pipeline in a supervised child: a faulted worker is replaced by a fresh
+        # process while the parent keeps the gRPC services and the buffered results up
+        from .runtime.supervisor import SupervisedServer
+        sup = SupervisedServer(cfg).start()
+        stop = threading.Event()
+        signal.signal(signal.SIGTERM, lambda *a: stop.set())
+        try:
+            sup.wait(stop)
+        except KeyboardInterrupt:
+            pass
+        sup.stop(None)
+        return 0 if not sup.failed else 1
     srv = Server(cfg).start()
     stop = threading.Event()
     signal.signal(signal.SIGTERM, lambda *a: stop.set())

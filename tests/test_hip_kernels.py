@@ -691,12 +691,12 @@ def test_dp_pipeline_records_match_eager(lag):
     assert sorted(got_all) == sorted(x for w in want for x in w)
 
 
-def _race_setup(B=2, S=257):
+def _race_setup(B=2, S=257, cam=(160, 120)):
     from semantic_segmentation_server_amd.runtime.engine import Engine
     from semantic_segmentation_server_amd.runtime.sources import SyntheticSource
     eng = Engine(_small_cfg(graph=True, batch=B, input_size=S, min_area_ratio=0.002), torch.device(DEV))
-    src = SyntheticSource(160, 120, seed=7, pool=4)
-    eng.set_camera(160, 120)
+    src = SyntheticSource(cam[0], cam[1], seed=7, pool=4)
+    eng.set_camera(*cam)
     frames = [torch.from_numpy(np.ascontiguousarray(src.read_batch(B)[0])).to(DEV) for _ in range(3)]
     return eng, eng._hip_model, frames
 
@@ -726,17 +726,37 @@ def test_concurrent_plan_copies_bit_identical():
     assert int(bad) == 0, f"{int(bad)} of 180 concurrent runs differ from the sequential label maps"
 
 
-def test_plan_is_a_function_of_the_frame():
+@pytest.mark.parametrize("shape", ["257", "headline"])
+def test_plan_is_a_function_of_the_frame(shape, tmp_path, monkeypatch):
     """The default plan's label maps depend on the frame alone: the same frame after two
     different predecessor frames (and after its plan buffers were NaN-filled) gives
-    bit-identical labels (no history-dependent reads)."""
-    eng, hm, fr = _race_setup()
+    bit-identical labels (no history-dependent reads). ``headline``:
+    513^2 / 640x480 at B = 2 with the committed B = 32 picks (the kernels the headline runs:
+    stream spans, hidden-split bands, grouped ASPP), choices whose B = 32 variant has no
+    B = 2 counterpart timed afresh."""
+    if shape == "headline":
+        import json
+        from semantic_segmentation_server_amd.models.hip_model import TUNE_FILE_DEFAULT
+        picks = json.load(open(TUNE_FILE_DEFAULT))["mnv2:B=32:cam=640x480:in=513"]
+        tf = tmp_path / "tune.json"
+        tf.write_text(json.dumps({"mnv2:B=2:cam=640x480:in=513": picks}))
+        monkeypatch.setenv("SSA_TUNE_FILE", str(tf))
+        eng, hm, fr = _race_setup(2, 513, (640, 480))
+        cam = (480, 640)
+    else:
+        eng, hm, fr = _race_setup()
+        cam = (120, 160)
     a = [hm.segment(fr[0], eng.lut_x, eng.lut_y).clone()]
     hm.segment(fr[1], eng.lut_x, eng.lut_y)
     a.append(hm.segment(fr[0], eng.lut_x, eng.lut_y).clone())
     hm.segment(fr[2], eng.lut_x, eng.lut_y)
     a.append(hm.segment(fr[0], eng.lut_x, eng.lut_y).clone())
-    _, bufs = hm._plan(2, 120, 160)
+    if shape == "headline":  # the picks that ran are the headline's where the names exist
+        want = json.load(open(TUNE_FILE_DEFAULT))["mnv2:B=32:cam=640x480:in=513"]
+        same = [n for n, v in hm.choices.items() if want.get(n) == v]
+        assert any(v.startswith("stream") for v in hm.choices.values()), hm.choices
+        assert len(same) >= len(want) // 2, (same, hm.choices)
+    _, bufs = hm._plan(2, *cam)
     for n, t in bufs.items():  # activation buffers only (int tables are plan constants)
         if not isinstance(t, torch.Tensor) or not t.is_cuda or n.startswith(("pool_w", "aspp_proj_wt")):
             continue
