@@ -322,6 +322,18 @@ class HipDeepLab:
                         lambda frames, lx, ly, out0=out0, ty=ty, tx=tx, sbp=sbp: K.stem_block0(
                             frames, lx, ly, sbp, out0, H=H, W=W, tile=(ty, tx))])
                         for ty, tx in ((8, 16), (4, 16), (8, 8), (16, 16), (8, 32), (12, 16))]
+                    # row-streaming bands: every input pixel gathered once, every stem pixel
+                    # computed once (stem_band.hip); bit-identical to the tile kernel
+                    SH = OH
+                    for nbx in (3, 4, 5):
+                        for target in (256, 512, 1024):
+                            R = max(2, -(-B * nbx * SH // target))
+                            tag = f"stem_band{R}x{nbx}"
+                            if any(t == tag for t, _ in fused):
+                                continue
+                            fused.insert(0, (tag, [
+                                lambda frames, lx, ly, out0=out0, R=R, nbx=nbx, sbp=sbp: K.stem_band(
+                                    frames, lx, ly, sbp, out0, H=H, W=W, R=R, nbx=nbx)]))
                     sep = ("separate", [ops[stem_at], ops[stem_at + 1]])
                     ops[stem_at:stem_at + 2] = [Choice("stem+block0", fused + [sep])]
         # ---- ASPP

@@ -637,6 +637,29 @@ def stem_block0(frames, lut_x, lut_y, packed: dict, out, *, H, W, tile=(8, 16)):
     return out
 
 
+def stem_band(frames, lut_x, lut_y, packed: dict, out, *, H, W, R=16, nbx=3):
+    """Row-streaming stem + block 0 (csrc/hip/stem_band.hip): bands of R output rows x
+    ceil(SW / nbx) columns; same weights and bit-identical results as ``stem_block0``."""
+    B, Hc, Wc, _ = frames.shape
+    SH, SW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    TW = -(-SW // nbx)
+    if R < 1 or nbx < 1 or -(-(TW + 2) // 16) > 8:
+        raise ValueError("stem_band: R >= 1 and at most 8 column groups per band")
+    _chk(packed["ws"], torch.bfloat16, "ws", 32 * 48)
+    _chk(frames, torch.uint8, "frames", B * Hc * Wc * 3)
+    _chk(out, torch.bfloat16, "out", B * SH * SW * packed["Cout"])
+    _chk(lut_x, torch.int32, "lut_x", W)
+    _chk(lut_y, torch.int32, "lut_y", H)
+    if packed["Cout"] != 16:
+        raise ValueError("stem_band: block 0 projects to 16 channels")
+    P = packed
+    _hip_mod().stem_band(_ptr(frames), _ptr(lut_x), _ptr(lut_y), _ptr(P["ws"]), _ptr(P["bs"]),
+                         _ptr(P["wd_h"]), _ptr(P["bd_h"]), _ptr(P["wp_h"]), _ptr(P["bp"]),
+                         _ptr(out), B, Hc, Wc, H, W, SH, SW, R, nbx, _stream())
+    _dbg("stem_band")
+    return out
+
+
 def depthwise3x3(x, w, bias, out, *, B, IH, IW, C, OH, OW, stride=1, dil=1, act="relu6"):
     """x: [B,IH,IW,C] bf16; w: [9, C] fp32; out: [B,OH,OW,C] bf16."""
     _chk(x, torch.bfloat16, "x", B * IH * IW * C)

@@ -914,6 +914,55 @@ def test_stem_block0_fused(cam, H, tile):
     assert _rel(_nchw(out).cpu(), ref) < 2e-2
 
 
+@pytest.mark.parametrize("cam,H", [((640, 480), 513), ((160, 120), 129), ((200, 150), 97),
+                                   ((96, 160), 129)])
+@pytest.mark.parametrize("R,nbx", [(16, 3), (5, 4), (33, 5), (7, 1), (300, 2)])
+def test_stem_band(cam, H, R, nbx):
+    """Row-streaming stem + block 0: bit-identical to the tile kernel (same arithmetic:
+    one gather per input pixel, one stem evaluation per stem pixel, depthwise bias-first in
+    tap order), incl. the letterbox LUT path (letterbox rows below the frame, a portrait
+    camera letterboxed on the right) and bands cut at the image borders; and vs the fp32
+    torch layers."""
+    from semantic_segmentation_server_amd.models.layers import ConvBNAct, init_random
+    from semantic_segmentation_server_amd.models.mobilenetv2 import InvertedResidual, IRSpec
+    from semantic_segmentation_server_amd.ops import reference_ops as R_
+    K = _hip()
+    SH = (H - 1) // 2 + 1
+    if -(-(-(-SH // nbx) + 2) // 16) > 8:
+        pytest.skip("band wider than 8 column groups")
+    stem = ConvBNAct(3, 32, 3, 2, act="relu6")
+    blk = InvertedResidual(IRSpec(32, 16, 1, 1, 1))
+    init_random(stem, seed=5)
+    init_random(blk, seed=6)
+    for m in list(stem.modules()) + list(blk.modules()):
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.uniform_(-0.2, 0.2)
+            m.running_var.uniform_(0.5, 2.0)
+    stem.eval(); blk.eval()
+    Wc, Hc = cam
+    g = torch.Generator().manual_seed(4)
+    frames = torch.randint(0, 256, (2, Hc, Wc, 3), generator=g, dtype=torch.uint8)
+    lx, ly, *_ = R_.letterbox_luts(Wc, Hc, H, H)
+    dwf, dbf = blk.dw.fold()
+    pwf, pbf = blk.project.fold()
+    P = K.pack_stem_block0(stem, dwf[:, 0], dbf, pwf[:, :, 0, 0], pbf, DEV)
+    lxd = torch.tensor(np.array(lx), dtype=torch.int32, device=DEV)
+    lyd = torch.tensor(np.array(ly), dtype=torch.int32, device=DEV)
+    fd = frames.to(DEV)
+    want = torch.full((2, SH, SH, 16), float("nan"), dtype=torch.bfloat16, device=DEV)
+    K.stem_block0(fd, lxd, lyd, P, want, H=H, W=H, tile=(8, 16))
+    out = torch.full((2, SH, SH, 16), float("nan"), dtype=torch.bfloat16, device=DEV)
+    K.stem_band(fd, lxd, lyd, P, out, H=H, W=H, R=R, nbx=nbx)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    assert torch.equal(out, want), (out.float() - want.float()).abs().max().item()
+    if H <= 129:
+        x = R_.preprocess(frames, torch.from_numpy(np.array(lx)), torch.from_numpy(np.array(ly)))
+        with torch.no_grad():
+            ref = blk(stem(x))
+        assert _rel(_nchw(out).cpu(), ref) < 2e-2
+
+
 @pytest.mark.parametrize("cin,cout,stride,dil,H,tile", [
     (64, 64, 1, 1, 33, (11, 11)),    # residual, CinP 64
     (64, 96, 1, 1, 33, (5, 11)),
