@@ -16,6 +16,8 @@
 #   profb1       sequential kernel trace of the B=1 step -> b1_layer_times.txt
 #   pmc          3 SQ counter passes over the sequential B=32 step -> pmc_summary.txt
 #   race         concurrent-plan determinism check (scripts/debug_race.py)
+#   share8       the dp8 bench path with 8 ranks sharing this one GPU (SSA_SHARE_GPU=1, gloo;
+#                completes end to end -- its throughput is not a scaling number)
 #   repro        packed-f32 co-residence reproducer, both builds (csrc/tools/packed_f32_repro.hip)
 #   retune:LIST  re-time the named choices (comma list) at B = ${TUNE_B:-32} on top of the committed
 #                picks -> $O/tune.json (copy into assets/tune_mi355x.json to commit)
@@ -76,6 +78,10 @@ for step in "$@"; do
              done
              python3 scripts/pmc_summary.py $O/pmc1 $O/pmc2 $O/pmc3 > $O/pmc_summary.txt 2>&1; head -60 $O/pmc_summary.txt ;;
     race)    timeout -k 10 600 python scripts/debug_race.py $RACE_ARGS > $O/race.txt 2>&1 || { tail -20 $O/race.txt; exit 5; }; tail -5 $O/race.txt ;;
+    share8)  SSA_SHARE_GPU=1 timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+               --master-addr 127.0.0.1 --master-port 29581 bench.py --gpus 8 --steps 10 --warmup 3 --rpc 300 \
+               > $O/share8.json 2> $O/share8.err || { grep -v "^\[Gloo\]" $O/share8.err | tail -30; exit 5; }
+             cut -c1-600 $O/share8.json ;;
     repro)   for b in repro_pk repro_nopk; do timeout -k 10 300 tools/bin/$b ${REPRO_REPS:-400} > $O/$b.txt 2>&1 \
                || { tail -5 $O/$b.txt; exit 7; }; cat $O/$b.txt; done ;;
     retune:*) [ -f $O/tune.json ] || cp assets/tune_mi355x.json $O/tune.json

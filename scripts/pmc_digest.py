@@ -1,4 +1,4 @@
-"""Compact per-kernel digest of the PMC passes (scripts/gpu_pmc.sh) for one step:
+"""Compact per-kernel digest of the PMC passes (scripts/gpu.sh ... pmc) for one step:
 time, MFMA-busy share, wave wait share, LDS bank-conflict share, L2 hit rate,
 HBM read/write requests.  python scripts/pmc_digest.py gpurun_out/pmc1 ... pmc4"""
 import os

@@ -498,15 +498,19 @@ def _small_cfg(**kw):
     return C.Config(**base)
 
 
-def test_hip_model_headline_shape_matches_torch():
-    """The headline shape (513^2, 640x480 camera) at B = 16 with the committed MI355X picks:
-    grids large enough that several workgroups of a kernel share a CU (the small-shape test
-    below runs most kernels at one workgroup per CU). Bound relative to stock PyTorch bf16
-    on the same GPU, as below."""
+@pytest.mark.parametrize("B", [32, 16, 8, 1])
+def test_hip_model_headline_shape_matches_torch(B):
+    """The headline shape (513^2, 640x480 camera) with the committed MI355X picks of that
+    batch size -- B = 32 is the plan bench.py runs, B = 1 the batch-1 /
+    latency plan: grids large enough that several workgroups of a kernel share a CU (the
+    small-shape test below runs most kernels at one workgroup per CU). Bound relative to
+    stock PyTorch bf16 on the same GPU, as below, plus the argmax agreement."""
     from semantic_segmentation_server_amd.models.deeplab import build_model
-    from semantic_segmentation_server_amd.models.hip_model import HipDeepLab
+    from semantic_segmentation_server_amd.models.hip_model import TUNE_FILE_DEFAULT, HipDeepLab
     from semantic_segmentation_server_amd.ops import reference_ops as R
-    S, B = 513, 16
+    import json
+    S = 513
+    assert f"mnv2:B={B}:cam=640x480:in=513" in json.load(open(TUNE_FILE_DEFAULT))
     model = build_model("mnv2", 21, calibrate_hw=129)
     cfg = _small_cfg(input_size=S)
     hm = HipDeepLab(model, torch.device(DEV), cfg)
@@ -520,10 +524,20 @@ def test_hip_model_headline_shape_matches_torch():
         bf_logits = copy.deepcopy(model).to(DEV, torch.bfloat16)(x.to(torch.bfloat16)).float().cpu()
     dl = hm.logits(frames.to(DEV), torch.tensor(lx, device=DEV), torch.tensor(ly, device=DEV))
     torch.cuda.synchronize()
+    saved = json.load(open(TUNE_FILE_DEFAULT))[f"mnv2:B={B}:cam=640x480:in=513"]
+    assert all(saved.get(n) == v for n, v in hm.choices.items() if n in saved), \
+        "the plan under test is not the committed one"
     got = _nchw(dl.float()).cpu()
     e_hip, e_bf = _rel(got, ref_logits), _rel(bf_logits, ref_logits)
     print(f"headline shape B={B}: rel err hip={e_hip:.4f} torch-bf16={e_bf:.4f}")
     assert e_hip < 1.5 * e_bf + 0.01, (e_hip, e_bf)
+    ref_lab = R.upsample_argmax(ref_logits, S, S)
+    hip_lab = R.upsample_argmax(got, S, S)
+    bf_lab = R.upsample_argmax(bf_logits, S, S)
+    a_hip = (hip_lab == ref_lab).float().mean().item()
+    a_bf = (bf_lab == ref_lab).float().mean().item()
+    print(f"  argmax agreement with fp32: hip={a_hip:.4f} torch-bf16={a_bf:.4f}")
+    assert a_hip > a_bf - 0.02
     # deterministic: a second run of the same plan gives the same logits bit for bit
     dl2 = hm.logits(frames.to(DEV), torch.tensor(lx, device=DEV), torch.tensor(ly, device=DEV))
     torch.cuda.synchronize()
