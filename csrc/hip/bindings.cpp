@@ -381,14 +381,18 @@ PYBIND11_MODULE(_hip, m) {
   m.def("postprocess",
         [](uintptr_t labels, int B, int H, int W, int crop_h, int crop_w, uintptr_t palette,
            int thr, double min_area, int num_bins, int K, uintptr_t ws, uintptr_t records,
-           uintptr_t stream) {
+           uintptr_t stream, int accum) {
           PostParams p;
+          p.accum = accum;
           p.labels = P<const uint8_t>(labels); p.B = B; p.H = H; p.W = W;
           p.crop_h = crop_h; p.crop_w = crop_w; p.palette = P<const int32_t>(palette);
           p.thr = thr; p.min_area = min_area; p.num_bins = num_bins; p.K = K;
           p.ws = P<void>(ws); p.records = P<float>(records);
           postprocess(p, S(stream));
-        });
+        },
+        py::arg("labels"), py::arg("B"), py::arg("H"), py::arg("W"), py::arg("crop_h"), py::arg("crop_w"),
+        py::arg("palette"), py::arg("thr"), py::arg("min_area"), py::arg("num_bins"), py::arg("K"),
+        py::arg("ws"), py::arg("records"), py::arg("stream"), py::arg("accum") = 0);
 
   m.attr("ACT_NONE") = (int)ACT_NONE;
   m.attr("ACT_RELU") = (int)ACT_RELU;

@@ -288,6 +288,7 @@ struct PostParams {
   // workspace (caller-allocated, sizes from post_workspace_bytes)
   void* ws = nullptr;
   float* records = nullptr;         // [B, 1 + 5K] packed output
+  int accum = 0;                    // accumulation pass: 0 = pixel strips, 1 = 32x32 tiles (LDS-staged labels)
 };
 size_t post_workspace_bytes(int B, int H, int W, int K, int num_bins);
 

@@ -984,6 +984,182 @@ __global__ __launch_bounds__(kAccThreads) void k_accum(KArgs a) {
   }
 }
 
+// Tile variant of k_accum (round 4): one 256-thread block per 32 x 32 CCL tile of a frame.
+// The strip kernel resolves every label it touches through the dependent global chain
+// L -> tile-local root -> cidx (fin()), per 256-pixel round, for the quad corners and again
+// in the hole-ring checks; round 3's ablations put ~60 of its ~112 us per 32 frames on those
+// loads. Here the block stages the final labels, the mask and the classes of its tile plus
+// the halo the per-pixel logic reads (2 columns left / right, 2 rows above, 1 below) in LDS
+// first -- every global load of the chain issued at once, one round trip per chain level
+// for the whole tile -- and the per-pixel logic below is k_accum's, reading LDS. Same
+// pieces, same keys, same hash-table flush: identical sums.
+constexpr int kAT = 32;                            // accumulation tile (= the CCL tile width)
+constexpr int kARW = kAT + 4, kARH = kAT + 3;      // staged region incl. the halo
+constexpr int kARN = kARW * kARH;
+constexpr int kAPT = (kARN + 255) / 256;           // staged pixels per thread
+
+__global__ __launch_bounds__(256) void k_accum_tiles(KArgs a) {
+  __shared__ AccTable T;
+  __shared__ int sfin[kARN];
+  __shared__ uint8_t smask[kARN], scls[kARN];
+  const int b = blockIdx.z;
+  const int cw = a.cw, ch = a.ch, bins = a.bins;
+  const int x0 = blockIdx.x * kAT, y0 = blockIdx.y * kAT;
+  FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
+  f.fb = f.flag[0];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kHash; i += 256) {
+    T.q.key[i] = 0; T.q.s00[i] = 0; T.q.s10[i] = 0; T.q.s01[i] = 0;
+  }
+  for (int i = tid; i < kHistHash; i += 256) {
+    T.hkey[i] = 0; T.hcnt[i] = 0;
+  }
+  if (tid == 0) T.maxd = 65536;
+  const uint8_t* lab = a.labels + (size_t)b * a.H * a.W;
+  {  // stage: all first-level loads, then all second-level (cidx) loads
+    int lv[kAPT];
+#pragma unroll
+    for (int k = 0; k < kAPT; ++k) {
+      const int i = tid + k * 256;
+      const int gx = x0 - 2 + i % kARW, gy = y0 - 2 + i / kARW;
+      const bool in = i < kARN && gx >= 0 && gx < cw && gy >= 0 && gy < ch;
+      lv[k] = 0;
+      if (in) {
+        const int q = gy * cw + gx;
+        lv[k] = f.L[q + 1];
+        smask[i] = f.mask[q];
+        int c = lab[gy * a.W + gx];
+        scls[i] = (uint8_t)(c >= bins ? bins - 1 : c);
+      } else if (i < kARN) {
+        smask[i] = 0;
+        scls[i] = 0;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kAPT; ++k) {
+      const int i = tid + k * 256;
+      if (i < kARN) sfin[i] = lv[k] == 0 ? 0 : (f.fb ? lv[k] : f.cidx[lv[k] - 1]);
+    }
+  }
+  __syncthreads();
+  auto LI = [&](int gx, int gy) { return (gy - y0 + 2) * kARW + (gx - x0 + 2); };
+  const int tx = tid & 31, ty0 = tid >> 5;
+#pragma unroll 1
+  for (int k = 0; k < kAT / 8; ++k) {
+    const int x = x0 + tx, y = y0 + ty0 + 8 * k;
+    const bool own = x < cw && y < ch;
+    int fnode = 0, f00 = 0;
+    long long f10 = 0, f01 = 0;
+    int bn[2] = {0, 0}, b00[2] = {0, 0};
+    long long b10[2] = {0, 0}, b01[2] = {0, 0};
+    int hkey = 0, rkey[4] = {0, 0, 0, 0};
+    if (own) {
+      const int i0 = LI(x, y);
+      const bool m0 = smask[i0] != 0;
+      const int n0 = sfin[i0];
+      const int np = n0;
+      const int c = scls[i0];
+      if (np != 0) hkey = (np * bins + c) * 2;
+      if (x + 1 < cw && y + 1 < ch) {
+        const int TX[4] = {1, 2, 1, 2}, TY[4] = {1, 1, 2, 2};
+        const int node[4] = {n0, sfin[i0 + 1], sfin[i0 + kARW], sfin[i0 + kARW + 1]};
+        const bool fg[4] = {m0, smask[i0 + 1] != 0, smask[i0 + kARW] != 0, smask[i0 + kARW + 1] != 0};
+        int nf = 0, missing = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (fg[q]) { ++nf; fnode = node[q]; } else { missing = q; }
+        }
+        const long long X = x, Y = y;
+        if (nf == 4) {
+          f00 = 2; f10 = 6 * X + 3; f01 = 6 * Y + 3;
+        } else if (nf == 3) {
+          const int o = 3 - missing;  // triangle of the opposite corner
+          f00 = 1; f10 = 3 * X + TX[o]; f01 = 3 * Y + TY[o];
+        } else {
+          fnode = 0;
+        }
+        int nb = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (fg[q] || node[q] == 0) continue;
+          bool first = true;
+          int cnt = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (!fg[j] && node[j] == node[q]) {
+              ++cnt;
+              if (j < q) first = false;
+            }
+          }
+          if (!first) continue;
+          if (nb < 2) {
+            bn[nb] = node[q];
+            if (cnt >= 2) { b00[nb] = 2; b10[nb] = 6 * X + 3; b01[nb] = 6 * Y + 3; }
+            else { b00[nb] = 1; b10[nb] = 3 * X + TX[q]; b01[nb] = 3 * Y + TY[q]; }
+            ++nb;
+          }
+        }
+      }
+      // hole rings, counted from the hole side exactly as in k_accum
+      if (!m0 && np != 0) {
+        const int nx[4] = {x - 1, x + 1, x, x}, ny[4] = {y, y, y - 1, y + 1};
+        const bool okn[4] = {x > 0, x + 1 < cw, y > 0, y + 1 < ch};
+        bool fgn[4], any = false;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          fgn[q] = okn[q] && smask[LI(nx[q], ny[q])];
+          any |= fgn[q];
+        }
+        if (any) {
+          const int par = parent_of(f, cw, np);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (!fgn[q]) continue;
+            const int rx = nx[q], ry = ny[q];
+            int px[3] = {-1, -1, -1}, py[3] = {0, 0, 0};
+            if (q == 0) {
+              if (rx > 0) { px[0] = rx - 1; py[0] = ry; }
+            } else if (q == 2) {
+              if (rx > 0) { px[0] = rx - 1; py[0] = ry; }
+              if (rx + 1 < cw) { px[1] = rx + 1; py[1] = ry; }
+              if (ry > 0) { px[2] = rx; py[2] = ry - 1; }
+            } else if (q == 3) {
+              if (rx > 0) { px[0] = rx - 1; py[0] = ry; }
+              if (rx + 1 < cw) { px[1] = rx + 1; py[1] = ry; }
+            }
+            const int ir = LI(rx, ry);
+            bool first = true;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+              if (px[j] < 0) continue;
+              const int iq = LI(px[j], py[j]);
+              if (!smask[iq] && sfin[iq] == np) first = false;
+            }
+            if (sfin[ir] != par || !first) continue;
+            rkey[q] = (np * bins + scls[ir]) * 2 + 1;
+          }
+        }
+      }
+    }
+    agg_add(T, f, cw, fnode, f00, f10, f01);
+    agg_add(T, f, cw, bn[0], b00[0], b10[0], b01[0]);
+    agg_add(T, f, cw, bn[1], b00[1], b10[1], b01[1]);
+    hagg(T, f, cw, bins, hkey);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (__any(rkey[q] > 0)) hagg(T, f, cw, bins, rkey[q]);
+  }
+  __syncthreads();
+  for (int i = tid; i < kHash; i += 256) {
+    const int node = T.q.key[i];
+    if (node != 0) moments_up(f, cw, node, T.q.s00[i], (long long)T.q.s10[i], (long long)T.q.s01[i], T.maxd);
+  }
+  for (int i = tid; i < kHistHash; i += 256) {
+    const int key = T.hkey[i];
+    if (key != 0) hist_up(f, cw, bins, key, T.hcnt[i], T.maxd);
+  }
+}
+
 // ---------------------------------------------------------------- select
 // assign_frame (k_records, one workgroup per frame) hands the record slots to the first K passing
 // contours in raster order of their discovery pixel: the passing roots of the root
@@ -1296,7 +1472,12 @@ void postprocess(const PostParams& p, hipStream_t s) {
   const int qtarget = qb_env ? std::max(1, atoi(qb_env)) : std::max(kQuadBlocks, 2048 / p.B);
   const int rounds = std::max(1, N / (256 * qtarget));
   const int qblocks = cdiv(N, 256 * rounds) * (256 / kAccThreads);
-  if (st++ < stages) hipLaunchKernelGGL(k_accum, dim3(qblocks, p.B), dim3(kAccThreads), 0, s, a);
+  if (st++ < stages) {
+    if (p.accum == 1)
+      hipLaunchKernelGGL(k_accum_tiles, dim3(cdiv(p.crop_w, kAT), cdiv(p.crop_h, kAT), p.B), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL(k_accum, dim3(qblocks, p.B), dim3(kAccThreads), 0, s, a);
+  }
   if (st++ < stages) hipLaunchKernelGGL(k_records, dim3(p.B), dim3(1024), 0, s, a);
   check_launch("postprocess");
 }

@@ -3,7 +3,7 @@
 // with rocprofv3) on identical label maps without the Python stack:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I csrc/hip csrc/tools/post_bench.hip \
 //         csrc/hip/postprocess.hip -o post_bench
-//   ./post_bench [reps] [maps.bin [only]]
+//   ./post_bench [reps] [maps.bin [only]]      (SSA_POST_ACCUM=0|1 env: strips / tiles pass)
 // (maps.bin: raw [32, 513, 513] uint8 label maps, e.g. the bench model's output dumped by
 // scripts/label_stats.py, timed as a fourth kind "file")
 // Maps: B = 32 frames of 513 x 513 cropped to 513 x 385 (the headline's 640x480
@@ -112,6 +112,7 @@ int main(int argc, char** argv) {
     p.labels = dlab; p.B = B; p.H = H; p.W = W; p.crop_h = ch; p.crop_w = cw;
     p.palette = dpal; p.thr = 127; p.min_area = 0.002 * H * W; p.num_bins = bins; p.K = K;
     p.ws = ws; p.records = drec;
+    p.accum = getenv("SSA_POST_ACCUM") ? atoi(getenv("SSA_POST_ACCUM")) : 1;
     for (int i = 0; i < 3; ++i) postprocess(p, s);
     chk(hipEventRecord(e0, s), "rec");
     for (int i = 0; i < reps; ++i) postprocess(p, s);

@@ -18,6 +18,7 @@
 #   race         concurrent-plan determinism check (scripts/debug_race.py)
 #   share8       the dp8 bench path with 8 ranks sharing this one GPU (SSA_SHARE_GPU=1, gloo;
 #                completes end to end -- its throughput is not a scaling number)
+#   postab       post-processing harness (tools/bin/post_bench), strips vs tiles accumulation
 #   repro        packed-f32 co-residence reproducer, both builds (csrc/tools/packed_f32_repro.hip)
 #   retune:LIST  re-time the named choices (comma list) at B = ${TUNE_B:-32} on top of the committed
 #                picks -> $O/tune.json (copy into assets/tune_mi355x.json to commit)
@@ -82,6 +83,8 @@ for step in "$@"; do
                --master-addr 127.0.0.1 --master-port 29581 bench.py --gpus 8 --steps 10 --warmup 3 --rpc 300 \
                > $O/share8.json 2> $O/share8.err || { grep -v "^\[Gloo\]" $O/share8.err | tail -30; exit 5; }
              cut -c1-600 $O/share8.json ;;
+    postab)  for m in 0 1; do SSA_POST_ACCUM=$m timeout -k 10 120 tools/bin/post_bench 50 > $O/post_accum$m.txt 2>&1 \
+               || { tail -5 $O/post_accum$m.txt; exit 7; }; echo "accum=$m"; cat $O/post_accum$m.txt; done ;;
     repro)   for b in repro_pk repro_nopk; do timeout -k 10 300 tools/bin/$b ${REPRO_REPS:-400} > $O/$b.txt 2>&1 \
                || { tail -5 $O/$b.txt; exit 7; }; cat $O/$b.txt; done ;;
     retune:*) [ -f $O/tune.json ] || cp assets/tune_mi355x.json $O/tune.json

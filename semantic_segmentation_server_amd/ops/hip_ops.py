@@ -913,7 +913,9 @@ def post_workspace_bytes(B, H, W, K, bins) -> int:
 
 
 def postprocess(labels, palette, ws, records, *, B, H, W, crop_h, crop_w, min_area, K, bins,
-                thr=127):
+                thr=127, accum=0):
+    """Device contour statistics (csrc/hip/postprocess.hip). ``accum``: the accumulation
+    pass over pixel strips (0) or LDS-staged 32 x 32 tiles (1); identical records."""
     _chk(labels, torch.uint8, "labels", B * H * W)
     _chk(palette, torch.int32, "palette", 256 * 3)
     _chk(ws, torch.uint8, "ws", post_workspace_bytes(B, H, W, K, bins))
@@ -921,7 +923,7 @@ def postprocess(labels, palette, ws, records, *, B, H, W, crop_h, crop_w, min_ar
     if not (0 < crop_h <= H and 0 < crop_w <= W):
         raise ValueError("bad crop")
     _hip_mod().postprocess(_ptr(labels), B, H, W, crop_h, crop_w, _ptr(palette), thr,
-                           float(min_area), bins, K, _ptr(ws), _ptr(records), _stream())
+                           float(min_area), bins, K, _ptr(ws), _ptr(records), _stream(), int(accum))
     _dbg('postprocess')
     return records
 

@@ -6,6 +6,8 @@ packed records (1 + 5K floats per frame) and unpacks them in push order.
 """
 from __future__ import annotations
 
+import os
+
 from typing import Dict, Sequence
 
 import numpy as np
@@ -23,6 +25,8 @@ class DevicePostprocess:
         self.palette = torch.tensor(np.asarray(palette, np.int32).reshape(256, 3), device=device)
         self._bufs: Dict[int, tuple] = {}
         self._host: Dict[int, torch.Tensor] = {}
+        # accumulation pass: LDS-staged 32 x 32 tiles (1) or pixel strips (0)
+        self.accum = int(os.environ.get("SSA_POST_ACCUM", "1"))
 
     def _buffers(self, B: int):
         if B not in self._bufs:
@@ -47,7 +51,8 @@ class DevicePostprocess:
                 raise ValueError("DevicePostprocess.run: out must be a contiguous [B, 1 + 5K] fp32 buffer")
             rec = out
         hip_ops.postprocess(labels, self.palette, ws, rec, B=B, H=self.H, W=self.W, crop_h=crop_h,
-                            crop_w=crop_w, min_area=min_area, K=self.K, bins=self.bins, thr=self.thr)
+                            crop_w=crop_w, min_area=min_area, K=self.K, bins=self.bins, thr=self.thr,
+                            accum=self.accum)
         return rec
 
     def fetch(self, rec: torch.Tensor, frame_ids: Sequence[int], ts: Sequence[float],

@@ -361,10 +361,18 @@ def test_upsample_argmax(h, H, K, variant):
     assert agree > 0.9999, agree
 
 
+@pytest.fixture(params=[1, 0], ids=["tiles", "strips"])
+def post_accum(request, monkeypatch):
+    """Both accumulation passes of the device post-processing (LDS-staged 32 x 32 tiles,
+    the default since round 4, and round 3's pixel strips) must give the spec's records."""
+    monkeypatch.setenv("SSA_POST_ACCUM", str(request.param))
+    return request.param
+
+
 @pytest.mark.parametrize("seed,h,w,min_area", [(0, 513, 513, 0.05 * 513 * 513), (1, 384, 513, 13158.45),
                                                (2, 97, 131, 0.0), (3, 64, 64, 10.0),
                                                (4, 200, 300, 100.0)])
-def test_device_postprocess_matches_spec(seed, h, w, min_area):
+def test_device_postprocess_matches_spec(seed, h, w, min_area, post_accum):
     from semantic_segmentation_server_amd.labels import pascal_colormap
     from semantic_segmentation_server_amd.postprocess.components import component_segments
     from semantic_segmentation_server_amd.postprocess.device import DevicePostprocess
@@ -396,7 +404,7 @@ def test_device_postprocess_matches_spec(seed, h, w, min_area):
 
 
 @pytest.mark.parametrize("block,period,min_area", [(3, 4, 100.0), (4, 5, 100.0), (4, 5, 3000.0)])
-def test_device_postprocess_many_components(block, period, min_area):
+def test_device_postprocess_many_components(block, period, min_area, post_accum):
     """Lattice masks with 10-16k components per frame (plus a few large blobs,
     the only contours above min_area): the 3x3 / period-4 lattice overflows the
     per-frame LDS merge (global union-find fallback), the others stay on the
@@ -430,7 +438,7 @@ def test_device_postprocess_many_components(block, period, min_area):
 
 
 @pytest.mark.parametrize("K", [8, 64])
-def test_device_postprocess_overflow_deterministic(K):
+def test_device_postprocess_overflow_deterministic(K, post_accum):
     """More contours pass min_area than there are record slots: the device keeps the
     first K by discovery key (same rule as the spec's ``max_records``), flags the frame
     with a negative count, and gives identical records on every run."""
@@ -466,7 +474,7 @@ def test_device_postprocess_overflow_deterministic(K):
     assert rec[2, 0] == 0
 
 
-def test_device_postprocess_deep_nesting():
+def test_device_postprocess_deep_nesting(post_accum):
     """Concentric 3-px rings nest ~80 contours deep (> the 32-entry ancestor chains of
     k_finalize): the record order must still be findContours pre-order."""
     from semantic_segmentation_server_amd.labels import pascal_colormap
