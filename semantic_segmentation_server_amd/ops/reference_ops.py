@@ -75,3 +75,22 @@ def upsample_argmax(logits: torch.Tensor, H: int, W: int) -> torch.Tensor:
     then argmax over K (first max wins, as ``tf.argmax``/``np.argmax``)."""
     up = F.interpolate(logits.float(), size=(H, W), mode="bilinear", align_corners=True)
     return up.argmax(1).to(torch.uint8)
+
+
+def decisive_agreement(got: torch.Tensor, ref: torch.Tensor, k: float = 4.0) -> Tuple[float, float]:
+    """Argmax agreement of ``got`` with ``ref`` (both (N, K, h, w) logits) on the pixels
+    whose ``ref`` decision is not a near-tie at the measured error: top-1 minus top-2
+    margin > ``k`` x the RMS of ``got - ref``. Returns (agreement, fraction of pixels
+    tested). With random-init weights most logits sit within a few bf16 ulps of each
+    other, so the plain argmax agreement of any bf16 run (stock PyTorch included: 0.77 /
+    0.90 on the same frame in two processes, MIOpen solver choice) is noise; a decision
+    with a margin of several error-sigmas must not flip."""
+    got, ref = got.float(), ref.float()
+    sigma = (got - ref).pow(2).mean().sqrt()
+    top2 = ref.topk(2, dim=1).values
+    mask = (top2[:, 0] - top2[:, 1]) > k * sigma
+    frac = mask.float().mean().item()
+    if not bool(mask.any()):
+        return 1.0, 0.0
+    agree = (got.argmax(1) == ref.argmax(1))[mask].float().mean().item()
+    return agree, frac

@@ -544,8 +544,13 @@ def test_hip_model_headline_shape_matches_torch(B):
     bf_lab = R.upsample_argmax(bf_logits, S, S)
     a_hip = (hip_lab == ref_lab).float().mean().item()
     a_bf = (bf_lab == ref_lab).float().mean().item()
-    print(f"  argmax agreement with fp32: hip={a_hip:.4f} torch-bf16={a_bf:.4f}")
-    assert a_hip > a_bf - 0.02
+    d_hip, frac = R.decisive_agreement(got, ref_logits)
+    print(f"  argmax agreement with fp32: hip={a_hip:.4f} torch-bf16={a_bf:.4f}; "
+          f"decisive pixels ({frac:.3f} of all) hip={d_hip:.4f}")
+    # plain argmax agreement is near-tie noise with random-init weights (torch-bf16 itself
+    # measured 0.77 and 0.90 on this frame in two processes); decisions with a margin of
+    # several error-sigmas must hold
+    assert d_hip >= 0.995 and frac > 0.05, (d_hip, frac)
     # deterministic: a second run of the same plan gives the same logits bit for bit
     dl2 = hm.logits(frames.to(DEV), torch.tensor(lx, device=DEV), torch.tensor(ly, device=DEV))
     torch.cuda.synchronize()
