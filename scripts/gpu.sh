@@ -22,6 +22,7 @@
 #   repro        packed-f32 co-residence reproducer, both builds (csrc/tools/packed_f32_repro.hip)
 #   retune:LIST  re-time the named choices (comma list) at B = ${TUNE_B:-32} on top of the committed
 #                picks -> $O/tune.json (copy into assets/tune_mi355x.json to commit)
+#   retuneall:B  re-time EVERY choice of the B-frame plan (SSA_RETUNE=1) -> $O/tune.json
 #   py:SCRIPT    python SCRIPT (args in PY_ARGS)
 # Extra env: BENCH_ARGS is appended to every bench.py call.
 set -o pipefail
@@ -92,6 +93,12 @@ for step in "$@"; do
                timeout -k 10 600 python bench.py --batch ${TUNE_B:-32} --steps 5 --warmup 2 --rpc 0 \
                > $O/retune_b${TUNE_B:-32}.json 2> $O/retune_b${TUNE_B:-32}.err || { tail -20 $O/retune_b${TUNE_B:-32}.err; exit 8; }
              grep "autotune" $O/retune_b${TUNE_B:-32}.err | grep -v "picks from" | cut -c1-1500 ;;
+    retuneall:*) [ -f $O/tune.json ] || cp assets/tune_mi355x.json $O/tune.json
+             b=${step#retuneall:}
+             SSA_TUNE_FILE=$O/tune.json SSA_RETUNE=1 SSA_LOG_AUTOTUNE=1 \
+               timeout -k 10 600 python bench.py --batch $b --steps 5 --warmup 2 --rpc 0 \
+               > $O/retuneall_b$b.json 2> $O/retuneall_b$b.err || { tail -20 $O/retuneall_b$b.err; exit 8; }
+             grep "autotune" $O/retuneall_b$b.err | grep -v "picks from" | cut -c1-300 ;;
     py:*)    timeout -k 10 ${PY_TIMEOUT:-600} python -u ${step#py:} $PY_ARGS > $O/$(basename ${step#py:} .py).txt 2>&1 \
                || { tail -30 $O/$(basename ${step#py:} .py).txt; exit 6; }; tail -${PY_TAIL:-40} $O/$(basename ${step#py:} .py).txt ;;
     *)       echo "unknown step $step"; exit 9 ;;
