@@ -42,7 +42,7 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("stream"), py::arg("variant") = 0, py::arg("perm") = 0, py::arg("Mp") = 0);
 
   m.def("conv_gemm_grouped",
-        [](py::list groups, uintptr_t order, int nblocks, int variant, uintptr_t stream) {
+        [](py::list groups, uintptr_t order, int nblocks, int variant, uintptr_t stream, int ks, uintptr_t part) {
           // groups: tuples (in, w, bias, img_bias, res, out, B, IH, IW, Cin, OH, OW, Cout,
           //                 KH, KW, stride, dil, ldo, co_off, ldr, act, perm, Mp)
           std::vector<ConvParams> ps;
@@ -61,10 +61,10 @@ PYBIND11_MODULE(_hip, m) {
             ps.push_back(p);
           }
           conv_gemm_grouped(ps.data(), (int)ps.size(), P<const int>(order), nblocks, variant,
-                            S(stream));
+                            S(stream), ks, P<float>(part));
         },
         py::arg("groups"), py::arg("order"), py::arg("nblocks"), py::arg("variant"),
-        py::arg("stream"));
+        py::arg("stream"), py::arg("ks") = 1, py::arg("part") = 0);
 
   m.def("bias_act", [](uintptr_t in, uintptr_t bias, uintptr_t img_bias, uintptr_t out, long long M,
                        int N, int HW, int act, uintptr_t stream) {
@@ -118,9 +118,12 @@ PYBIND11_MODULE(_hip, m) {
   m.def("fused_ir_stream",
         [](uintptr_t in, uintptr_t w, uintptr_t bp, uintptr_t table, uintptr_t out, int B, int H,
            int W, int Cin, int hidP, int Cout, int dil, int residual, int nspan, int WR, int WCP,
-           int hstride, int nh_max, uintptr_t stream, uintptr_t trace, int variant) {
+           int hstride, int nh_max, uintptr_t stream, uintptr_t trace, int variant, int hsplit,
+           uintptr_t part) {
           FusedSpanParams p;
           p.trace = P<long long>(trace);
+          p.hsplit = hsplit;
+          p.part = P<float>(part);
           p.npi = variant;  // 0: 8 waves; 1: group 8 on the expansion waves (G8A); 2: 12 waves
           p.in = P<const bf16>(in); p.w = P<const void>(w); p.bp = P<const float>(bp);
           p.table = P<const int>(table); p.out = P<bf16>(out);
@@ -132,8 +135,17 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("in"), py::arg("w"), py::arg("bp"), py::arg("table"), py::arg("out"), py::arg("B"),
         py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("hidP"), py::arg("Cout"), py::arg("dil"),
         py::arg("residual"), py::arg("nspan"), py::arg("WR"), py::arg("WCP"), py::arg("hstride"),
-        py::arg("nh_max"), py::arg("stream"), py::arg("trace") = 0, py::arg("variant") = 0);
+        py::arg("nh_max"), py::arg("stream"), py::arg("trace") = 0, py::arg("variant") = 0,
+        py::arg("hsplit") = 1, py::arg("part") = 0);
   m.def("fused_ir_stream_lds", &fused_ir_stream_lds);
+  m.def("stream_combine",
+        [](uintptr_t part, uintptr_t bp, uintptr_t res, uintptr_t out, int HS, long long M, int Cout,
+           uintptr_t stream, int act) {
+          stream_combine(P<const float>(part), P<const float>(bp), P<const bf16>(res), P<bf16>(out), HS, M, Cout,
+                         S(stream), act);
+        },
+        py::arg("part"), py::arg("bp"), py::arg("res"), py::arg("out"), py::arg("HS"), py::arg("M"),
+        py::arg("Cout"), py::arg("stream"), py::arg("act") = 0);
   m.def("fused_ir_band",
         [](uintptr_t in, uintptr_t blob, uintptr_t out, int B, int IH, int IW, int Cin, int OH, int OW,
            int Cout, int hidP, int stride, int residual, int R, int nslot, int blob_bytes, int o_be,

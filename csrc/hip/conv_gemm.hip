@@ -39,7 +39,9 @@ struct ConvArgs {
 constexpr int kMaxConvGroup = 4;
 struct ConvGroupArgs {
   ConvArgs g[kMaxConvGroup];
-  const int* order;  // [nblocks] (group << 24) | tile
+  const int* order;  // [nblocks] (group << 24) | (K slice << 20) | tile
+  int ks;            // K slices per tile (split-K for small batches); 1 = no split
+  float* part;       // ks > 1: fp32 partials [ks][B * OH * OW][ldo] (no bias / act), else null
 };
 
 template <int MT, int NT>
@@ -484,7 +486,8 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // ASPP tiles run at one workgroup per CU, where one stage of lookahead leaves the
 // L2/MALL latency exposed).
 template <int MT, int NT, int ST, int WM, int WN, int BK = 64>
-__device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char* smem) {
+__device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char* smem, int ks = 1, int kslice = 0,
+                                          float* part = nullptr) {
   constexpr int NW = WM * WN;                            // waves: WM (pixels) x WN (channels)
   constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN, ROWB = BK * 2;  // BK bf16 per stage row
   constexpr int CPR = ROWB / 16, RPG = 1024 / ROWB;      // 16-B chunks per row, rows per glds
@@ -550,9 +553,12 @@ __device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char
   for (int t = 0; t < taps; ++t)
     if ((tapmask >> t) & 1) { tl |= (unsigned long long)t << (4 * ntap); ++ntap; }
   const int cch = cdiv_dev(a.Cin, BK);
-  const int total = ntap * cch;
+  // split-K (small batches: a batch-1 ASPP grid is 40 tiles of up to 45 stages): this block
+  // runs stages [s0, s1) of the tile's (tap, channel-chunk) sequence
+  const int s0 = kslice * (ntap * cch) / ks, s1 = (kslice + 1) * (ntap * cch) / ks;
+  const int total = s1 - s0;
 
-  int is_tap = 0, is_c = 0;  // issue cursor
+  int is_tap = s0 / cch, is_c = s0 - (s0 / cch) * cch;  // issue cursor
   // per-tap state of the cursor, recomputed only when it moves to the next tap: the rows'
   // source offsets (element index of channel 0 for this tap, -1 = padding -> zero page) and
   // the tap's weight offset. Round 2 recomputed the bounds and offsets for every 64-channel
@@ -572,7 +578,7 @@ __device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char
     }
     wtap = t * a.Cin;
   };
-  if (ntap > 0) set_tap();
+  if (total > 0) set_tap();
   auto issue = [&](int stage) {
     const int c = is_c * BK + lc * 8;
     const bool cok = c < a.Cin;
@@ -638,6 +644,22 @@ __device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char
     }
   }
 
+  if (part) {  // split-K: fp32 partial of this slice, bias / activation in the combine
+    const size_t slab = (size_t)a.B * a.OH * a.OW * a.ldo;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int mg = m0 + wm * 16 * MT + i * 16 + r16;
+      if (mg >= M) continue;
+      const int m = a.perm ? a.perm[mg] : mg;
+      if (m < 0) continue;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = n0 + wn * 16 * NT + j * 16 + kq * 4;
+        if (n < a.Cout) *reinterpret_cast<f32x4*>(part + kslice * slab + (size_t)m * a.ldo + a.co_off + n) = acc[i][j];
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
     const int mg = m0 + wm * 16 * MT + i * 16 + r16;
@@ -701,12 +723,12 @@ template <int MT, int NT, int ST, int WM = 2, int WN = 2, int BK = 64>
 __global__ __launch_bounds__(64 * WM * WN) void conv_glds_group_kernel(ConvGroupArgs ga) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int e = __builtin_amdgcn_readfirstlane(ga.order[blockIdx.x]);
-  const int t = e & 0xffffff;
+  const int t = e & 0xfffff, ksl = (e >> 20) & 15;
   switch (e >> 24) {  // constant indices: each arm reads its ConvArgs straight from kernarg
-    case 0: glds_tile<MT, NT, ST, WM, WN, BK>(ga.g[0], t, smem); break;
-    case 1: glds_tile<MT, NT, ST, WM, WN, BK>(ga.g[1], t, smem); break;
-    case 2: glds_tile<MT, NT, ST, WM, WN, BK>(ga.g[2], t, smem); break;
-    default: glds_tile<MT, NT, ST, WM, WN, BK>(ga.g[3], t, smem); break;
+    case 0: glds_tile<MT, NT, ST, WM, WN, BK>(ga.g[0], t, smem, ga.ks, ksl, ga.part); break;
+    case 1: glds_tile<MT, NT, ST, WM, WN, BK>(ga.g[1], t, smem, ga.ks, ksl, ga.part); break;
+    case 2: glds_tile<MT, NT, ST, WM, WN, BK>(ga.g[2], t, smem, ga.ks, ksl, ga.part); break;
+    default: glds_tile<MT, NT, ST, WM, WN, BK>(ga.g[3], t, smem, ga.ks, ksl, ga.part); break;
   }
 }
 
@@ -881,10 +903,18 @@ static ConvArgs to_args(const ConvParams& p) {
 }
 
 void conv_gemm_grouped(const ConvParams* ps, int n, const int* order, int nblocks, int variant,
-                       hipStream_t s) {
+                       hipStream_t s, int ks, float* part) {
   if (n < 1 || n > kMaxConvGroup) throw std::invalid_argument("conv_gemm_grouped: 1..4 convs");
   if (!order || nblocks < 1) throw std::invalid_argument("conv_gemm_grouped: empty tile order");
+  if (ks < 1 || ks > 16 || (ks > 1 && part == nullptr))
+    throw std::invalid_argument("conv_gemm_grouped: ks in [1, 16], a partials buffer for ks > 1");
+  if (ks > 1)
+    for (int i = 0; i < n; ++i)
+      if (ps[i].ldo != ps[0].ldo || ps[i].Cout % 4 || (ps[i].ldo | ps[i].co_off) % 4)
+        throw std::invalid_argument("conv_gemm_grouped: split-K needs one ldo and 4-aligned channels");
   ConvGroupArgs ga{};
+  ga.ks = ks;
+  ga.part = ks > 1 ? part : nullptr;
   for (int i = 0; i < kMaxConvGroup; ++i) {
     const ConvParams& p = ps[i < n ? i : 0];
     if (p.Cin % 8 != 0 || p.KH * p.KW > 16 || p.Cout != ps[0].Cout)

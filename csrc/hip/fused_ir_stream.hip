@@ -61,6 +61,8 @@ struct StreamArgs {
   const bf16* in; const char* w; const float* bp; const int* table; bf16* out;
   int B, H, W, Cin, Cout, NC, S, dil, residual, WCP, WR, hstride;
   long long* trace;  // debug: s_memtime stamps [block][wave 0 / 4][64], nullptr normally
+  int HS;            // hidden splits: workgroups per span, each a contiguous range of chunks
+  float* part;       // HS > 1: fp32 projection partials [HS][B * H * W][Cout] (no bias)
 };
 
 // Debug timeline (a.trace != nullptr): lane 0 of waves 0 (expansion) and 4 (its SIMD
@@ -262,14 +264,21 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r16 = lane & 15, kq = lane >> 4;
-  const int b = blockIdx.x / a.S, j = blockIdx.x - (blockIdx.x / a.S) * a.S;
+  // block -> (image b, span j, hidden slice hs); the HS slices of a span are adjacent
+  const int hs = blockIdx.x % a.HS, bj = blockIdx.x / a.HS;
+  const int b = bj / a.S, j = bj - (bj / a.S) * a.S;
   const int* tb = a.table + (size_t)j * a.hstride;
   const int p0 = tb[0], p1 = tb[1], wy0 = tb[2], nh = tb[3];
-  const int HW = a.H * a.W, d = DIL, NC = a.NC;
+  const int HW = a.H * a.W, d = DIL;
+  // this workgroup's chunks [cb, cb + NC): batch 1 has B * S = 16..32 workgroups for 256
+  // CUs, so the hidden chunks of a span are split over HS workgroups whose fp32 partial
+  // projections stream_combine sums (+ bias, residual) in a fixed order
+  const int cb = hs * a.NC / a.HS, NC = (hs + 1) * a.NC / a.HS - cb;
+  const char* wsrc = a.w + (size_t)cb * CHB;
   const bf16* inb = a.in + (size_t)b * HW * a.Cin;
 
   auto issue = [&](int c) {
-    const char* src = a.w + (size_t)c * CHB + lane * 16;
+    const char* src = wsrc + (size_t)c * CHB + lane * 16;
     char* dst = ring + (c % kNSL) * CHB;
 #pragma unroll
     for (int q = 0; q < MP; ++q) {
@@ -427,6 +436,16 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
     step_barrier();
     const int C8 = NSP * 2, c0 = h * NSP * 16;  // 8-channel units per pixel in the slice
     const int units = (p1 - p0) * C8;
+    if (a.HS > 1) {  // fp32 partial of this hidden slice, bias / residual added by the combine
+      float* pb = a.part + ((size_t)hs * a.B * HW + (size_t)b * HW + p0) * a.Cout + c0;
+      for (int u = tid; u < units; u += kNT) {
+        const int px = u / C8, c = (u - px * C8) * 8;
+        float* q = pb + (size_t)px * a.Cout + c;
+        *reinterpret_cast<f32x4*>(q) = *reinterpret_cast<const f32x4*>(O + px * OS + c);
+        *reinterpret_cast<f32x4*>(q + 4) = *reinterpret_cast<const f32x4*>(O + px * OS + c + 4);
+      }
+      continue;
+    }
     bf16* outb = a.out + ((size_t)b * HW + p0) * a.Cout + c0;
     const bf16* resb = inb + (size_t)p0 * a.Cin + c0;
     for (int u = tid; u < units; u += kNT) {
@@ -460,7 +479,7 @@ void launch_stream(const StreamArgs& a, hipStream_t st) {
           "fused_ir_stream attr");
     attr = true;
   }
-  hipLaunchKernelGGL((fused_ir_stream_kernel<KS, NS, XQ, DIL, WCP, MODE>), dim3(a.B * a.S),
+  hipLaunchKernelGGL((fused_ir_stream_kernel<KS, NS, XQ, DIL, WCP, MODE>), dim3(a.B * a.S * a.HS),
                      dim3(64 * stream_waves(MODE)), lds, st, a);
   check_launch("fused_ir_stream");
 }
@@ -483,8 +502,11 @@ void fused_ir_stream(const FusedSpanParams& p, hipStream_t st) {
   if (p.S < 1 || (p.H * p.W + p.S - 1) / p.S > kGB * 4 * 16) throw std::invalid_argument("fused_ir_stream: span too long");
   if (p.H * p.W >= (1 << 19)) throw std::invalid_argument("fused_ir_stream: map too large for the halo table");
   if (p.nh_max > kXQ * 4 * 16) throw std::invalid_argument("fused_ir_stream: halo over 320 pixels");
+  if (p.hsplit < 1 || p.hsplit > p.hidP / 32 || (p.hsplit > 1 && p.part == nullptr))
+    throw std::invalid_argument("fused_ir_stream: hsplit in [1, hidP / 32], partials buffer for hsplit > 1");
   StreamArgs a{p.in, reinterpret_cast<const char*>(p.w), p.bp, p.table, p.out, p.B, p.H, p.W, p.Cin,
-               p.Cout, p.hidP / 32, p.S, p.dil, p.residual, p.WCP, p.WR, p.hstride, p.trace};
+               p.Cout, p.hidP / 32, p.S, p.dil, p.residual, p.WCP, p.WR, p.hstride, p.trace,
+               p.hsplit, p.part};
   const int KS = p.Cin / 32, NS = p.Cout / 16;
   // instantiated for the 33-wide maps of the headline (window pitch W + 16 = 49) at
   // dilation 1 (halo <= 16 groups: 4 rounds per expansion wave) and 2 (<= 20: 5 rounds)
@@ -517,6 +539,48 @@ void fused_ir_stream(const FusedSpanParams& p, hipStream_t st) {
 #undef STREAM
 #undef STREAM12
   throw std::invalid_argument("fused_ir_stream: no instantiation for this (Cin, Cout)");
+}
+
+// out = act(sum_h part[h] + bias (+ residual)), bf16: the combine of the hidden-split stream
+// and of the split-K grouped ASPP GEMM (fixed summation order h = 0..HS-1, so the result is
+// a function of the inputs alone)
+__global__ __launch_bounds__(256) void stream_combine_kernel(const float* __restrict__ part, const float* __restrict__ bp,
+                                                             const bf16* __restrict__ res, bf16* __restrict__ out,
+                                                             int HS, long long M, int Cout, int relu) {
+  const long long units = M * (Cout / 8);
+  const long long slab = M * Cout;
+  for (long long u = blockIdx.x * 256ll + threadIdx.x; u < units; u += (long long)gridDim.x * 256) {
+    const long long m = u / (Cout / 8);
+    const int c = (int)(u - m * (Cout / 8)) * 8;
+    const float* q = part + m * Cout + c;
+    f32x4 s0 = *reinterpret_cast<const f32x4*>(bp + c), s1 = *reinterpret_cast<const f32x4*>(bp + c + 4);
+    for (int h = 0; h < HS; ++h) {
+      s0 += *reinterpret_cast<const f32x4*>(q + h * slab);
+      s1 += *reinterpret_cast<const f32x4*>(q + h * slab + 4);
+    }
+    bf16x8 r = zero8();
+    if (res) r = ld8(res + m * Cout + c);
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = s0[e] + (float)r[e];
+      v[e + 4] = s1[e] + (float)r[e + 4];
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16)(relu ? fmaxf(v[e], 0.f) : v[e]);
+    st8(out + m * Cout + c, o);
+  }
+}
+
+void stream_combine(const float* part, const float* bp, const bf16* res, bf16* out, int HS, long long M, int Cout,
+                    hipStream_t st, int act) {
+  if (act != 0 && act != 1) throw std::invalid_argument("stream_combine: act 0 (none) or 1 (relu)");
+  if (Cout % 8 || HS < 1 || M < 1) throw std::invalid_argument("stream_combine: Cout % 8, HS >= 1");
+  const long long units = M * (Cout / 8);
+  const int grid = (int)std::min<long long>((units + 255) / 256, 2048);
+  hipLaunchKernelGGL(stream_combine_kernel, dim3(grid), dim3(256), 0, st, part, bp, res, out, HS, M, Cout, act);
+  check_launch("stream_combine");
 }
 
 }  // namespace ssa

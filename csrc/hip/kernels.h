@@ -31,7 +31,7 @@ void conv_gemm(const ConvParams& p, hipStream_t s);
 // conv's GEMM, BM x BN of the variant: 5 128x256, 6 256x256, 8 128x256 3-stage,
 // 10 128x128 4-stage, 11 128x128 2-stage).
 void conv_gemm_grouped(const ConvParams* ps, int n, const int* order, int nblocks, int variant,
-                       hipStream_t s);
+                       hipStream_t s, int ks = 1, float* part = nullptr);
 
 // Pointwise conv, weight-streamed (pw_conv.hip). w is host-packed per 64-channel
 // chunk: weights in MFMA fragment order [4][ceil(K/32)][64 lanes][8] bf16 followed by
@@ -135,6 +135,8 @@ struct FusedSpanParams {
   int xslots = 0;             // halo groups beyond 16 (their X lives in LDS; xg == 3 only)
   long long* trace = nullptr; // debug s_memtime timeline [B*S][2][64]
   int nh_max = 0;             // largest halo of the table (fused_ir_stream: <= 320)
+  int hsplit = 1;             // fused_ir_stream: workgroups per span over the hidden chunks
+  float* part = nullptr;      // hsplit > 1: fp32 partials [hsplit][B*H*W][Cout]
 };
 void fused_ir_span(const FusedSpanParams& p, hipStream_t s);
 size_t fused_ir_span_lds(int Cin, int Cout, int WR, int WCP, int xslots);
@@ -142,6 +144,9 @@ size_t fused_ir_span_lds(int Cin, int Cout, int WR, int WCP, int xslots);
 // expansion waves 0-3, depthwise+projection waves 4-7, LDS-DMA chunk ring.
 void fused_ir_stream(const FusedSpanParams& p, hipStream_t s);
 size_t fused_ir_stream_lds(int Cin, int Cout, int WR, int WCP);
+// sum of the hidden-split partials + bias (+ residual) -> bf16 [M, Cout]
+void stream_combine(const float* part, const float* bp, const bf16* res, bf16* out, int HS, long long M, int Cout,
+                    hipStream_t st, int act = 0);
 // Row-streaming fused inverted residual (fused_ir_band.hip): blocks with Cin <= 32,
 // stride 1/2, dilation 1. blob: host-packed weights (hip_ops.pack_fused_band) with the
 // section offsets below; R output rows per band, nslot E row buffers (1 or 2).

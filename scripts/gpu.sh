@@ -29,6 +29,8 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 REPO=$PWD
 export SSA_NO_AUTOBUILD=1
+# the trace steps run from /tmp: a relative tune file must not silently vanish there
+[ -n "$SSA_TUNE_FILE" ] && export SSA_TUNE_FILE=$(realpath -m "$SSA_TUNE_FILE")
 O=gpurun_out/${1:?outdir}
 shift
 mkdir -p $O

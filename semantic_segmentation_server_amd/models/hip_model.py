@@ -102,18 +102,35 @@ class Choice:
         if len(self.variants) < 2:
             return
         times = []
+        graph = os.environ.get("SSA_TUNE_GRAPH", "1") == "1"
         for _, ops in self.variants:
             for _ in range(2):
                 for op in ops:
                     op(*args)
             st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            g = None
+            if graph:
+                # time the variant replayed from a hipGraph, as the engine runs it: timed from
+                # Python, every kernel under ~16 us measured the host's launch path instead
+                # (all batch-1 variants of blocks 7-10 read 16-17 us, r4 retune tables)
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for _ in range(reps):
+                        for op in ops:
+                            op(*args)
+                g.replay()
             st.record()
-            for _ in range(reps):
-                for op in ops:
-                    op(*args)
+            if g is not None:
+                g.replay()
+            else:
+                for _ in range(reps):
+                    for op in ops:
+                        op(*args)
             en.record()
             en.synchronize()
             times.append(st.elapsed_time(en) / reps)
+            del g
         self.pick = min(range(len(times)), key=times.__getitem__)
         self.times = times
 
@@ -389,6 +406,20 @@ class HipDeepLab:
                 bufs[f"aspp_order{gv}"] = order
                 grouped.append((f"grouped_v{gv}", [
                     lambda *_, convs=convs, order=order, gv=gv: K.conv_gemm_grouped(convs, order, gv)]))
+                # small batches: split-K (a batch-1 grid is ~40 tiles of up to 45 K stages for
+                # 256 CUs); fp32 partials + one combine (bias, ReLU) over the concat buffer
+                ks_opts = (2, 4, 6) if B <= 2 else (2, 3) if B <= 8 else ()
+                if ks_opts and gv in (5, 17, 18) and A * (len(self.aspp_atrous) + 1) == self.cat_c:
+                    if "aspp_part" not in bufs:
+                        buf("aspp_part", max(ks_opts) * B * h * w * self.cat_c, dtype=torch.float32)
+                        bufs["aspp_bias_cat"] = torch.cat(
+                            [b0b.float()] + [ab.float() for (_, ab), _ in self.aspp_atrous]).to(dev).contiguous()
+                    for ks in ks_opts:
+                        order_k = K.grouped_tile_order(convs, gv, dev, ks=ks)
+                        bufs[f"aspp_order{gv}k{ks}"] = order_k
+                        grouped.append((f"grouped_v{gv}k{ks}", [
+                            lambda *_, convs=convs, order=order_k, gv=gv, ks=ks: K.conv_gemm_grouped(
+                                convs, order, gv, ks=ks, part=bufs["aspp_part"], bias_cat=bufs["aspp_bias_cat"])]))
                 # (branch-affine XCD orders, K.grouped_tile_order_branch, measured 6-16 us
                 # slower on every variant: profiles/r3_negative_results.txt)
             ops[aspp_at:] = [Choice("aspp.branches", grouped + [seq])]
@@ -548,6 +579,7 @@ class HipDeepLab:
 
     def _mnv2_block(self, ops, buf, i, blk, x, B, h, w, c):
         s = blk["spec"]
+        bufs_part: Dict[str, torch.Tensor] = {}
         hid = s.hidden
         inp = x
         unfused: List[Callable] = []
@@ -647,6 +679,21 @@ class HipDeepLab:
                         variants.insert(0, (f"stream{S}" + ("", "g", "w")[v], [
                             lambda *_, x=inp, out=out, tab=tab, sp=blk["span"], v=v: FS.fused_ir_stream(
                                 x, sp, tab, out, B=B, residual=s.residual, variant=v)]))
+                    # small batches: the hidden chunks of a span over hs workgroups (fp32
+                    # partials + stream_combine), so B * S * hs workgroups share the chip
+                    nc = -(-hid // 32)
+                    hs_opts = [hs for hs in (2, 3, 4, 6) if hs <= nc and B * S * hs <= 512] if B <= 8 else []
+                    if hs_opts:
+                        key = f"b{i}_part"
+                        if key not in bufs_part:
+                            bufs_part[key] = buf(key, max(hs_opts) * B * h * w * s.cout, dtype=torch.float32)
+                        part = bufs_part[key]
+                        for hs in hs_opts:
+                            for v in ((0, 2) if s.cout <= 96 and s.dilation == 1 else (0,)):
+                                variants.insert(0, (f"stream{S}" + ("", "g", "w")[v] + f"h{hs}", [
+                                    lambda *_, x=inp, out=out, tab=tab, sp=blk["span"], v=v, hs=hs, part=part:
+                                    FS.fused_ir_stream(x, sp, tab, out, B=B, residual=s.residual, variant=v,
+                                                       hsplit=hs, part=part)]))
         if blk["expand"] is not None and FB.band_supported(s.cin, hid, s.cout, s.stride, s.dilation, OW):
             # row-streaming bands: every input row expanded once into an on-chip fp16 row
             if "band" not in blk:

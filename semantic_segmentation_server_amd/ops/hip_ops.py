@@ -158,7 +158,7 @@ def _tile_taps(B: int, H: int, W: int, k: int, dil: int, BM: int,
     return sum(((tile >> t) & 1) for t in range(k * k))
 
 
-def grouped_tile_order(convs: List[dict], variant: int, device=None, xcds: int = 1) -> torch.Tensor:
+def grouped_tile_order(convs: List[dict], variant: int, device=None, xcds: int = 1, ks: int = 1) -> torch.Tensor:
     """Block -> tile table of ``conv_gemm_grouped``: every tile of every conv as
     (group << 24) | tile, heaviest first (work = live taps x 64-channel K chunks;
     longest-processing-time order, so the short 1x1 / edge tiles fill the tail).
@@ -176,9 +176,11 @@ def grouped_tile_order(convs: List[dict], variant: int, device=None, xcds: int =
         ntm = taps.numel()
         for tm in range(ntm):
             for n in range(tn):
-                ent.append((g << 24) | (tm * tn + n))
-                cost.append(int(taps[tm]) * kch)
-                part.append(min(xcds - 1, tm * xcds // max(1, ntm)))
+                stages = int(taps[tm]) * kch
+                for sl in range(ks):  # K slice sl runs stages [sl*S/ks, (sl+1)*S/ks) (split-K)
+                    ent.append((g << 24) | (sl << 20) | (tm * tn + n))
+                    cost.append((sl + 1) * stages // ks - sl * stages // ks)
+                    part.append(min(xcds - 1, tm * xcds // max(1, ntm)))
     if xcds <= 1:
         idx = sorted(range(len(ent)), key=lambda i: (-cost[i], i))
         return torch.tensor([ent[i] for i in idx], dtype=torch.int32).to(device).contiguous()
@@ -264,11 +266,17 @@ def grouped_tile_order_branch(convs: List[dict], variant: int, device=None, xcds
     return torch.tensor(out, dtype=torch.int32).to(device).contiguous()
 
 
-def conv_gemm_grouped(convs: List[dict], order: torch.Tensor, variant: int = 5) -> None:
+def conv_gemm_grouped(convs: List[dict], order: torch.Tensor, variant: int = 5, ks: int = 1,
+                      part: Optional[torch.Tensor] = None, bias_cat: Optional[torch.Tensor] = None) -> None:
     """Up to 4 independent stride-1 'same' NHWC convs with one Cout (the ASPP branches)
     in ONE LDS-DMA grid, tiles in the ``grouped_tile_order`` table. Each conv is a
     dict of conv_gemm's arguments: x, w, bias, out, B, IH, IW, Cin, OH, OW, Cout, k,
-    dil, ldo, co_off, act, and optionally perm (tap_group_perm with the variant's BM)."""
+    dil, ldo, co_off, act, and optionally perm (tap_group_perm with the variant's BM).
+
+    ``ks`` > 1 (split-K, small batches): the order table (``grouped_tile_order(..., ks=)``)
+    carries ks K slices per tile; their fp32 partials go to ``part`` [ks, B*OH*OW, ldo]
+    and stream_combine adds them, ``bias_cat`` (the branches' biases at their co_off) and
+    the shared activation into ``out``: the convs must tile [0, ldo) of one output."""
     if not 1 <= len(convs) <= 4:
         raise ValueError("conv_gemm_grouped: 1..4 convs")
     if variant not in GROUP_TILE:
@@ -307,13 +315,33 @@ def conv_gemm_grouped(convs: List[dict], order: torch.Tensor, variant: int = 5) 
     _chk(order, torch.int32, "order")
     if not getattr(order, "_ssa_checked", False):  # every block maps to a real tile
         oc = order.cpu().long()
-        g, t = oc >> 24, oc & 0xFFFFFF
+        g, t, sl = oc >> 24, oc & 0xFFFFF, (oc >> 20) & 15
         lim = torch.tensor(tiles)[g.clamp(0, len(tiles) - 1)]
-        if (g < 0).any() or (g >= len(convs)).any() or (t >= lim).any():
+        if (g < 0).any() or (g >= len(convs)).any() or (t >= lim).any() or (sl >= ks).any():
             raise ValueError("conv_gemm_grouped: order entry out of range")
+        if oc.numel() != sum(tiles) * ks:
+            raise ValueError("conv_gemm_grouped: the order table must list every tile's K slices once")
         order._ssa_checked = True
-    _hip_mod().conv_gemm_grouped(groups, _ptr(order), order.numel(), variant, _stream())
+    if ks > 1:
+        c0 = convs[0]
+        ldo, Mo = c0.get("ldo", c0["Cout"]), c0["B"] * c0["OH"] * c0["OW"]
+        if part is None or bias_cat is None:
+            raise ValueError("conv_gemm_grouped: split-K needs part and bias_cat")
+        if len({c.get("act") for c in convs}) != 1 or c0.get("act") not in (None, "relu"):
+            raise ValueError("conv_gemm_grouped: split-K needs one activation (none / relu)")
+        if sorted(c.get("co_off", 0) for c in convs) != list(range(0, ldo, c0["Cout"])):
+            raise ValueError("conv_gemm_grouped: split-K convs must tile the output channels")
+        if any(c["out"].data_ptr() != c0["out"].data_ptr() or c.get("ldo", c["Cout"]) != ldo for c in convs):
+            raise ValueError("conv_gemm_grouped: split-K convs must share one output")
+        _chk(part, torch.float32, "part", ks * Mo * ldo)
+        _chk(bias_cat, torch.float32, "bias_cat", ldo)
+    _hip_mod().conv_gemm_grouped(groups, _ptr(order), order.numel(), variant, _stream(), int(ks),
+                                 _ptr(part) if ks > 1 else 0)
     _dbg('conv_gemm_grouped')
+    if ks > 1:
+        _hip_mod().stream_combine(_ptr(part), _ptr(bias_cat), 0, _ptr(c0["out"]), int(ks), Mo, ldo, _stream(),
+                                  1 if c0.get("act") == "relu" else 0)
+        _dbg('stream_combine')
 
 
 def bias_act(x, bias, out, *, M: int, N: int, HW: int = 1, img_bias=None, act=None):

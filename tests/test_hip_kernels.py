@@ -139,6 +139,44 @@ def test_conv_gemm_grouped_aspp(B, H, W, Cin, Cout, variant):
     assert torch.all(out[..., 4 * Cout:] == 7.0)
 
 
+@pytest.mark.parametrize("B,variant,ks", [(1, 18, 2), (1, 17, 4), (1, 5, 6), (2, 18, 6), (3, 17, 3)])
+def test_conv_gemm_grouped_aspp_splitk(B, variant, ks):
+    """Split-K grouped ASPP (batch-1 plans): the K slices' fp32 partials + stream_combine
+    (bias, ReLU) vs F.conv2d per branch, bit-identical on a rerun, uneven stage splits
+    (a 1x1 branch of 5 stages over 6 slices: empty slices write zeros)."""
+    K = _hip()
+    g = torch.Generator().manual_seed(12)
+    H = W = 33
+    Cin, Cout = 320, 256
+    x = torch.randn(B, Cin, H, W, generator=g).to(torch.bfloat16)
+    xd = _nhwc(x).to(DEV)
+    ldo = 4 * Cout
+    out = torch.full((B, H, W, ldo), float("nan"), dtype=torch.bfloat16, device=DEV)
+    BM = K.GROUP_TILE[variant][0]
+    convs, refs, biases = [], [], []
+    for j, (k, rate) in enumerate(((1, 1), (3, 6), (3, 12), (3, 18))):
+        w = (torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5).to(torch.bfloat16)
+        b = torch.randn(Cout, generator=g)
+        biases.append(b)
+        refs.append(F.relu(F.conv2d(x.float(), w.float(), b, 1, rate * (k // 2), rate)))
+        convs.append(dict(x=xd, w=w.permute(0, 2, 3, 1).contiguous().to(DEV), bias=b.to(DEV), out=out,
+                          B=B, IH=H, IW=W, Cin=Cin, OH=H, OW=W, Cout=Cout, k=k, dil=rate, ldo=ldo,
+                          co_off=j * Cout, act="relu",
+                          perm=K.tap_group_perm(B, H, W, 3, rate, BM, DEV) if k == 3 else None))
+    order = K.grouped_tile_order(convs, variant, DEV, ks=ks)
+    part = torch.full((ks * B * H * W * ldo,), float("nan"), dtype=torch.float32, device=DEV)
+    bias_cat = torch.cat(biases).to(DEV)
+    K.conv_gemm_grouped(convs, order, variant, ks=ks, part=part, bias_cat=bias_cat)
+    torch.cuda.synchronize()
+    for j, ref in enumerate(refs):
+        assert _rel(_nchw(out[..., j * Cout:(j + 1) * Cout]).cpu(), ref) < 1e-2, j
+    first = out.clone()
+    out.fill_(float("nan"))
+    K.conv_gemm_grouped(convs, order, variant, ks=ks, part=part, bias_cat=bias_cat)
+    torch.cuda.synchronize()
+    assert torch.equal(first.view(torch.int16), out.view(torch.int16))
+
+
 @pytest.mark.parametrize("img", [True, False])
 def test_bias_act(img):
     """GEMM epilogue: act(x + bias + per-image bias) vs torch."""
@@ -1318,6 +1356,21 @@ def test_fused_ir_stream(cin, cout, dil, H, S):
         FS.fused_ir_stream(xd, packed, table, out2, B=B, residual=spec.residual, variant=variant)
         torch.cuda.synchronize()
         assert torch.equal(out.view(torch.int16), out2.view(torch.int16)), variant
+    # hidden split (batch-1 plans): the span's chunks over hs workgroups + stream_combine;
+    # uneven chunk ranges (hs = 4 over 5 / 9 / 15 / 18 / 30 chunks) included
+    nc = packed["hidP"] // 32
+    for hs in (2, 4, nc):
+        part = torch.full((hs * B * H * W * cout,), float("nan"), dtype=torch.float32, device=DEV)
+        out = torch.full((B, H, W, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
+        FS.fused_ir_stream(xd, packed, table, out, B=B, residual=spec.residual, hsplit=hs, part=part)
+        torch.cuda.synchronize()
+        assert torch.isfinite(out).all(), hs
+        assert _rel(_nchw(out).cpu(), ref) < 2e-2, hs
+        assert _rel(out.cpu().float(), torch.from_numpy(emu)) < 5e-3, hs
+        out2 = torch.full_like(out, float("nan"))
+        FS.fused_ir_stream(xd, packed, table, out2, B=B, residual=spec.residual, hsplit=hs, part=part)
+        torch.cuda.synchronize()
+        assert torch.equal(out.view(torch.int16), out2.view(torch.int16)), hs
 
 
 @pytest.mark.parametrize("M,HW,ncls,ldo,img", [
