@@ -10,6 +10,7 @@
 #   bench        driver window x2 (python bench.py --steps 20 --warmup 5)
 #   bench100     100 timed steps, RPC under load
 #   b1           batch-1 bench (400 steps)
+#   b1lat        batch-1 bench at lag 0 (each step's records collected in the step: latency mode)
 #   cfg4         DeepLabv3-ResNet50 1025^2 int8 B=8 (60 steps) and bf16
 #   cfg5         4 camera streams x 8 frames (batched step)
 #   prof         sequential kernel trace of the B=32 step -> layer_times.txt
@@ -18,7 +19,7 @@
 #   race         concurrent-plan determinism check (scripts/debug_race.py)
 #   share8       the dp8 bench path with 8 ranks sharing this one GPU (SSA_SHARE_GPU=1, gloo;
 #                completes end to end -- its throughput is not a scaling number)
-#   postab       post-processing harness (tools/bin/post_bench), strips vs tiles accumulation
+#   postab       post-processing harness (tools/bin/post_bench), strips vs 32^2 / 64^2 tile accumulation
 #   repro        packed-f32 co-residence reproducer, both builds (csrc/tools/packed_f32_repro.hip)
 #   retune:LIST  re-time the named choices (comma list) at B = ${TUNE_B:-32} on top of the committed
 #                picks -> $O/tune.json (copy into assets/tune_mi355x.json to commit)
@@ -68,6 +69,7 @@ for step in "$@"; do
     bench)   bench d1 300 --steps 20 --warmup 5 && bench d2 300 --steps 20 --warmup 5 || exit 2 ;;
     bench100) bench s100 300 --steps 100 --warmup 10 || exit 2 ;;
     b1)      bench b1 300 --batch 1 --steps 400 --warmup 50 --rpc 0 || exit 2 ;;
+    b1lat)   bench b1lat 300 --batch 1 --lag 0 --steps 400 --warmup 50 --rpc 0 || exit 2 ;;
     cfg4)    bench c4i8 400 --arch resnet50 --input_size 1025 --camera 2048x1024 --batch 8 --dtype int8 --steps 60 --warmup 5 --rpc 0 \
                && bench c4bf 400 --arch resnet50 --input_size 1025 --camera 2048x1024 --batch 8 --steps 60 --warmup 5 --rpc 0 || exit 2 ;;
     cfg5)    bench c5 300 --streams 4 --batch 32 --steps 100 --warmup 10 --rpc 0 || exit 2 ;;
@@ -86,7 +88,7 @@ for step in "$@"; do
                --master-addr 127.0.0.1 --master-port 29581 bench.py --gpus 8 --steps 10 --warmup 3 --rpc 300 \
                > $O/share8.json 2> $O/share8.err || { grep -v "^\[Gloo\]" $O/share8.err | tail -30; exit 5; }
              cut -c1-600 $O/share8.json ;;
-    postab)  for m in 0 1; do SSA_POST_ACCUM=$m timeout -k 10 120 tools/bin/post_bench 50 > $O/post_accum$m.txt 2>&1 \
+    postab)  for m in 0 1 2; do SSA_POST_ACCUM=$m timeout -k 10 120 tools/bin/post_bench 50 > $O/post_accum$m.txt 2>&1 \
                || { tail -5 $O/post_accum$m.txt; exit 7; }; echo "accum=$m"; cat $O/post_accum$m.txt; done ;;
     repro)   for b in repro_pk repro_nopk; do timeout -k 10 300 tools/bin/$b ${REPRO_REPS:-400} > $O/$b.txt 2>&1 \
                || { tail -5 $O/$b.txt; exit 7; }; cat $O/$b.txt; done ;;
