@@ -42,7 +42,8 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("stream"), py::arg("variant") = 0, py::arg("perm") = 0, py::arg("Mp") = 0);
 
   m.def("conv_gemm_grouped",
-        [](py::list groups, uintptr_t order, int nblocks, int variant, uintptr_t stream, int ks, uintptr_t part) {
+        [](py::list groups, uintptr_t order, int nblocks, int variant, uintptr_t stream, int ks, uintptr_t part,
+           uintptr_t cnt, int cnt_stride) {
           // groups: tuples (in, w, bias, img_bias, res, out, B, IH, IW, Cin, OH, OW, Cout,
           //                 KH, KW, stride, dil, ldo, co_off, ldr, act, perm, Mp)
           std::vector<ConvParams> ps;
@@ -61,10 +62,11 @@ PYBIND11_MODULE(_hip, m) {
             ps.push_back(p);
           }
           conv_gemm_grouped(ps.data(), (int)ps.size(), P<const int>(order), nblocks, variant,
-                            S(stream), ks, P<float>(part));
+                            S(stream), ks, P<float>(part), P<int>(cnt), cnt_stride);
         },
         py::arg("groups"), py::arg("order"), py::arg("nblocks"), py::arg("variant"),
-        py::arg("stream"), py::arg("ks") = 1, py::arg("part") = 0);
+        py::arg("stream"), py::arg("ks") = 1, py::arg("part") = 0, py::arg("cnt") = 0,
+        py::arg("cnt_stride") = 0);
 
   m.def("bias_act", [](uintptr_t in, uintptr_t bias, uintptr_t img_bias, uintptr_t out, long long M,
                        int N, int HW, int act, uintptr_t stream) {
@@ -119,11 +121,12 @@ PYBIND11_MODULE(_hip, m) {
         [](uintptr_t in, uintptr_t w, uintptr_t bp, uintptr_t table, uintptr_t out, int B, int H,
            int W, int Cin, int hidP, int Cout, int dil, int residual, int nspan, int WR, int WCP,
            int hstride, int nh_max, uintptr_t stream, uintptr_t trace, int variant, int hsplit,
-           uintptr_t part) {
+           uintptr_t part, uintptr_t cnt) {
           FusedSpanParams p;
           p.trace = P<long long>(trace);
           p.hsplit = hsplit;
           p.part = P<float>(part);
+          p.cnt = P<int>(cnt);
           p.npi = variant;  // 0: 8 waves; 1: group 8 on the expansion waves (G8A); 2: 12 waves
           p.in = P<const bf16>(in); p.w = P<const void>(w); p.bp = P<const float>(bp);
           p.table = P<const int>(table); p.out = P<bf16>(out);
@@ -136,7 +139,7 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("hidP"), py::arg("Cout"), py::arg("dil"),
         py::arg("residual"), py::arg("nspan"), py::arg("WR"), py::arg("WCP"), py::arg("hstride"),
         py::arg("nh_max"), py::arg("stream"), py::arg("trace") = 0, py::arg("variant") = 0,
-        py::arg("hsplit") = 1, py::arg("part") = 0);
+        py::arg("hsplit") = 1, py::arg("part") = 0, py::arg("cnt") = 0);
   m.def("fused_ir_stream_lds", &fused_ir_stream_lds);
   m.def("stream_combine",
         [](uintptr_t part, uintptr_t bp, uintptr_t res, uintptr_t out, int HS, long long M, int Cout,

@@ -42,6 +42,8 @@ struct ConvGroupArgs {
   const int* order;  // [nblocks] (group << 24) | (K slice << 20) | tile
   int ks;            // K slices per tile (split-K for small batches); 1 = no split
   float* part;       // ks > 1: fp32 partials [ks][B * OH * OW][ldo] (no bias / act), else null
+  int* cnt;          // ks > 1, in-launch combine: per-tile tickets [group][cnt_stride], else null
+  int cnt_stride;
 };
 
 template <int MT, int NT>
@@ -487,7 +489,7 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // L2/MALL latency exposed).
 template <int MT, int NT, int ST, int WM, int WN, int BK = 64>
 __device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char* smem, int ks = 1, int kslice = 0,
-                                          float* part = nullptr) {
+                                          float* part = nullptr, int* cnt = nullptr) {
   constexpr int NW = WM * WN;                            // waves: WM (pixels) x WN (channels)
   constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN, ROWB = BK * 2;  // BK bf16 per stage row
   constexpr int CPR = ROWB / 16, RPG = 1024 / ROWB;      // 16-B chunks per row, rows per glds
@@ -658,6 +660,44 @@ __device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char
         if (n < a.Cout) *reinterpret_cast<f32x4*>(part + kslice * slab + (size_t)m * a.ldo + a.co_off + n) = acc[i][j];
       }
     }
+    if (cnt) {
+      // in-launch combine (the split-K recipe of cdna_hip_programming.md): drain, release,
+      // draw a ticket; the tile's last arriving slice acquires, resets the ticket and sums
+      // the ks slabs in slice order (+ bias, activation) into the bf16 output
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // every wave's stores drained, every LDS read of the K loop done
+      int* s_flag = reinterpret_cast<int*>(smem);
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int t = __hip_atomic_fetch_add(cnt + bid, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = t == ks - 1;
+        if (last) {
+          __hip_atomic_store(cnt + bid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *s_flag = last;
+      }
+      __syncthreads();
+      if (*reinterpret_cast<volatile int*>(s_flag)) {
+        constexpr int NTH = 64 * NW, Q = BN / 4;
+        for (int idx = tid; idx < BM * Q; idx += NTH) {
+          const int r = idx / Q, n = n0 + (idx - r * Q) * 4;
+          const int mg = m0 + r;
+          if (mg >= M || n >= a.Cout) continue;
+          const int m = a.perm ? a.perm[mg] : mg;
+          if (m < 0) continue;
+          const float* q = part + (size_t)m * a.ldo + a.co_off + n;
+          f32x4 v = *reinterpret_cast<const f32x4*>(a.bias + n);
+          for (int sl = 0; sl < ks; ++sl) v += *reinterpret_cast<const f32x4*>(q + sl * slab);
+          bf16x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = (bf16)apply_act(v[e], a.act);
+          *reinterpret_cast<bf16x4*>(a.out + (size_t)m * a.ldo + a.co_off + n) = o;
+        }
+      }
+    }
     return;
   }
 #pragma unroll
@@ -725,10 +765,13 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_glds_group_kernel(ConvGroup
   const int e = __builtin_amdgcn_readfirstlane(ga.order[blockIdx.x]);
   const int t = e & 0xfffff, ksl = (e >> 20) & 15;
   switch (e >> 24) {  // constant indices: each arm reads its ConvArgs straight from kernarg
-    case 0: glds_tile<MT, NT, ST, WM, WN, BK>(ga.g[0], t, smem, ga.ks, ksl, ga.part); break;
-    case 1: glds_tile<MT, NT, ST, WM, WN, BK>(ga.g[1], t, smem, ga.ks, ksl, ga.part); break;
-    case 2: glds_tile<MT, NT, ST, WM, WN, BK>(ga.g[2], t, smem, ga.ks, ksl, ga.part); break;
-    default: glds_tile<MT, NT, ST, WM, WN, BK>(ga.g[3], t, smem, ga.ks, ksl, ga.part); break;
+    case 0: glds_tile<MT, NT, ST, WM, WN, BK>(ga.g[0], t, smem, ga.ks, ksl, ga.part, ga.cnt); break;
+    case 1: glds_tile<MT, NT, ST, WM, WN, BK>(ga.g[1], t, smem, ga.ks, ksl, ga.part,
+                                              ga.cnt ? ga.cnt + ga.cnt_stride : nullptr); break;
+    case 2: glds_tile<MT, NT, ST, WM, WN, BK>(ga.g[2], t, smem, ga.ks, ksl, ga.part,
+                                              ga.cnt ? ga.cnt + 2 * ga.cnt_stride : nullptr); break;
+    default: glds_tile<MT, NT, ST, WM, WN, BK>(ga.g[3], t, smem, ga.ks, ksl, ga.part,
+                                               ga.cnt ? ga.cnt + 3 * ga.cnt_stride : nullptr); break;
   }
 }
 
@@ -903,7 +946,7 @@ static ConvArgs to_args(const ConvParams& p) {
 }
 
 void conv_gemm_grouped(const ConvParams* ps, int n, const int* order, int nblocks, int variant,
-                       hipStream_t s, int ks, float* part) {
+                       hipStream_t s, int ks, float* part, int* cnt, int cnt_stride) {
   if (n < 1 || n > kMaxConvGroup) throw std::invalid_argument("conv_gemm_grouped: 1..4 convs");
   if (!order || nblocks < 1) throw std::invalid_argument("conv_gemm_grouped: empty tile order");
   if (ks < 1 || ks > 16 || (ks > 1 && part == nullptr))
@@ -915,6 +958,8 @@ void conv_gemm_grouped(const ConvParams* ps, int n, const int* order, int nblock
   ConvGroupArgs ga{};
   ga.ks = ks;
   ga.part = ks > 1 ? part : nullptr;
+  ga.cnt = ks > 1 ? cnt : nullptr;
+  ga.cnt_stride = cnt_stride;
   for (int i = 0; i < kMaxConvGroup; ++i) {
     const ConvParams& p = ps[i < n ? i : 0];
     if (p.Cin % 8 != 0 || p.KH * p.KW > 16 || p.Cout != ps[0].Cout)

@@ -63,6 +63,8 @@ struct StreamArgs {
   long long* trace;  // debug: s_memtime stamps [block][wave 0 / 4][64], nullptr normally
   int HS;            // hidden splits: workgroups per span, each a contiguous range of chunks
   float* part;       // HS > 1: fp32 projection partials [HS][B * H * W][Cout] (no bias)
+  int* cnt;          // HS > 1, in-launch combine: per-span arrival tickets [B * S] (zero between
+                     // launches: the last arriver resets its word), else null (stream_combine)
 };
 
 // Debug timeline (a.trace != nullptr): lane 0 of waves 0 (expansion) and 4 (its SIMD
@@ -465,6 +467,54 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
       st8(outb + (size_t)px * a.Cout + c, o);
     }
   }
+  if (a.HS > 1 && a.cnt) {
+    // in-launch combine (cdna_hip_programming.md, split-K reduction recipe): every wave
+    // drains its partial stores, one lane releases them at agent scope and draws a ticket;
+    // the span's last arriver acquires, resets the ticket and sums the HS slabs in the
+    // fixed order h = 0..HS-1 (+ bias, residual) into the bf16 output -- the stream_combine
+    // launch (4.5-5.6 us per block at batch 1, profiles/r4_b1_layer_times.txt) disappears
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave's partial stores drained; O is no longer read
+    int* s_flag = reinterpret_cast<int*>(smem);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int t = __hip_atomic_fetch_add(a.cnt + bj, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = t == a.HS - 1;
+      if (last) {
+        __hip_atomic_store(a.cnt + bj, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *s_flag = last;
+    }
+    __syncthreads();
+    if (*reinterpret_cast<volatile int*>(s_flag)) {
+      const int C8 = a.Cout / 8, units = (p1 - p0) * C8;
+      const size_t slab = (size_t)a.B * HW * a.Cout;
+      const float* pb = a.part + ((size_t)b * HW + p0) * a.Cout;
+      bf16* outb = a.out + ((size_t)b * HW + p0) * a.Cout;
+      const bf16* resb = inb + (size_t)p0 * a.Cin;
+      for (int u = tid; u < units; u += kNT) {
+        const int px = u / C8, c = (u - px * C8) * 8;
+        f32x4 s0 = *reinterpret_cast<const f32x4*>(a.bp + c), s1 = *reinterpret_cast<const f32x4*>(a.bp + c + 4);
+        const float* q = pb + (size_t)px * a.Cout + c;
+        for (int h = 0; h < a.HS; ++h) {
+          s0 += *reinterpret_cast<const f32x4*>(q + h * slab);
+          s1 += *reinterpret_cast<const f32x4*>(q + h * slab + 4);
+        }
+        bf16x8 r = zero8();
+        if (a.residual) r = ld8(resb + (size_t)px * a.Cin + c);
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] = (bf16)(s0[e] + (float)r[e]);
+          o[e + 4] = (bf16)(s1[e] + (float)r[e + 4]);
+        }
+        st8(outb + (size_t)px * a.Cout + c, o);
+      }
+    }
+  }
   STREAM_STAMP(63);
 }
 
@@ -506,7 +556,7 @@ void fused_ir_stream(const FusedSpanParams& p, hipStream_t st) {
     throw std::invalid_argument("fused_ir_stream: hsplit in [1, hidP / 32], partials buffer for hsplit > 1");
   StreamArgs a{p.in, reinterpret_cast<const char*>(p.w), p.bp, p.table, p.out, p.B, p.H, p.W, p.Cin,
                p.Cout, p.hidP / 32, p.S, p.dil, p.residual, p.WCP, p.WR, p.hstride, p.trace,
-               p.hsplit, p.part};
+               p.hsplit, p.part, p.hsplit > 1 ? p.cnt : nullptr};
   const int KS = p.Cin / 32, NS = p.Cout / 16;
   // instantiated for the 33-wide maps of the headline (window pitch W + 16 = 49) at
   // dilation 1 (halo <= 16 groups: 4 rounds per expansion wave) and 2 (<= 20: 5 rounds)

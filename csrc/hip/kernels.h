@@ -31,7 +31,8 @@ void conv_gemm(const ConvParams& p, hipStream_t s);
 // conv's GEMM, BM x BN of the variant: 5 128x256, 6 256x256, 8 128x256 3-stage,
 // 10 128x128 4-stage, 11 128x128 2-stage).
 void conv_gemm_grouped(const ConvParams* ps, int n, const int* order, int nblocks, int variant,
-                       hipStream_t s, int ks = 1, float* part = nullptr);
+                       hipStream_t s, int ks = 1, float* part = nullptr, int* cnt = nullptr,
+                       int cnt_stride = 0);
 
 // Pointwise conv, weight-streamed (pw_conv.hip). w is host-packed per 64-channel
 // chunk: weights in MFMA fragment order [4][ceil(K/32)][64 lanes][8] bf16 followed by
@@ -137,6 +138,8 @@ struct FusedSpanParams {
   int nh_max = 0;             // largest halo of the table (fused_ir_stream: <= 320)
   int hsplit = 1;             // fused_ir_stream: workgroups per span over the hidden chunks
   float* part = nullptr;      // hsplit > 1: fp32 partials [hsplit][B*H*W][Cout]
+  int* cnt = nullptr;         // hsplit > 1: per-span tickets [B*S] for the in-launch combine (null:
+                              // the caller runs stream_combine)
 };
 void fused_ir_span(const FusedSpanParams& p, hipStream_t s);
 size_t fused_ir_span_lds(int Cin, int Cout, int WR, int WCP, int xslots);
@@ -293,7 +296,7 @@ struct PostParams {
   // workspace (caller-allocated, sizes from post_workspace_bytes)
   void* ws = nullptr;
   float* records = nullptr;         // [B, 1 + 5K] packed output
-  int accum = 0;                    // accumulation pass: 0 = pixel strips, 1 = 32x32 tiles (LDS-staged labels)
+  int accum = 0;                    // accumulation pass: 0 = pixel strips, 1 / 2 = 32x32 / 64x64 tiles (LDS-staged labels)
 };
 size_t post_workspace_bytes(int B, int H, int W, int K, int num_bins);
 

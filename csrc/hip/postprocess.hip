@@ -993,12 +993,15 @@ __global__ __launch_bounds__(kAccThreads) void k_accum(KArgs a) {
 // first -- every global load of the chain issued at once, one round trip per chain level
 // for the whole tile -- and the per-pixel logic below is k_accum's, reading LDS. Same
 // pieces, same keys, same hash-table flush: identical sums.
-constexpr int kAT = 32;                            // accumulation tile (= the CCL tile width)
-constexpr int kARW = kAT + 4, kARH = kAT + 3;      // staged region incl. the halo
-constexpr int kARN = kARW * kARH;
-constexpr int kAPT = (kARN + 255) / 256;           // staged pixels per thread
-
+// AT = 64 (accum mode 2): a quarter of the blocks, so a quarter of the per-(block, component)
+// flushes -- single-lane global atomics up the border tree, one per ancestor level -- for
+// the same per-pixel work.
+template <int AT>
 __global__ __launch_bounds__(256) void k_accum_tiles(KArgs a) {
+  constexpr int kAT = AT;                            // accumulation tile (32 = the CCL tile width)
+  constexpr int kARW = kAT + 4, kARH = kAT + 3;      // staged region incl. the halo
+  constexpr int kARN = kARW * kARH;
+  constexpr int kAPT = (kARN + 255) / 256;           // staged pixels per thread
   __shared__ AccTable T;
   __shared__ int sfin[kARN];
   __shared__ uint8_t smask[kARN], scls[kARN];
@@ -1043,10 +1046,10 @@ __global__ __launch_bounds__(256) void k_accum_tiles(KArgs a) {
   }
   __syncthreads();
   auto LI = [&](int gx, int gy) { return (gy - y0 + 2) * kARW + (gx - x0 + 2); };
-  const int tx = tid & 31, ty0 = tid >> 5;
+  const int tx = tid % kAT, ty0 = tid / kAT;  // 256 / kAT rows per round
 #pragma unroll 1
-  for (int k = 0; k < kAT / 8; ++k) {
-    const int x = x0 + tx, y = y0 + ty0 + 8 * k;
+  for (int k = 0; k < kAT * kAT / 256; ++k) {
+    const int x = x0 + tx, y = y0 + ty0 + (256 / kAT) * k;
     const bool own = x < cw && y < ch;
     int fnode = 0, f00 = 0;
     long long f10 = 0, f01 = 0;
@@ -1408,6 +1411,7 @@ void postprocess(const PostParams& p, hipStream_t s) {
     throw std::invalid_argument("postprocess: crop * classes too large for 32-bit histogram keys");
   if (p.crop_h > p.H || p.crop_w > p.W || p.crop_h <= 0 || p.crop_w <= 0)
     throw std::invalid_argument("postprocess: bad crop");
+  if (p.accum < 0 || p.accum > 2) throw std::invalid_argument("postprocess: accum 0 (strips), 1 (32^2 tiles), 2 (64^2)");
   KArgs a;
   a.labels = p.labels;
   a.B = p.B; a.H = p.H; a.W = p.W; a.ch = p.crop_h; a.cw = p.crop_w;
@@ -1474,7 +1478,9 @@ void postprocess(const PostParams& p, hipStream_t s) {
   const int qblocks = cdiv(N, 256 * rounds) * (256 / kAccThreads);
   if (st++ < stages) {
     if (p.accum == 1)
-      hipLaunchKernelGGL(k_accum_tiles, dim3(cdiv(p.crop_w, kAT), cdiv(p.crop_h, kAT), p.B), dim3(256), 0, s, a);
+      hipLaunchKernelGGL(k_accum_tiles<32>, dim3(cdiv(p.crop_w, 32), cdiv(p.crop_h, 32), p.B), dim3(256), 0, s, a);
+    else if (p.accum == 2)
+      hipLaunchKernelGGL(k_accum_tiles<64>, dim3(cdiv(p.crop_w, 64), cdiv(p.crop_h, 64), p.B), dim3(256), 0, s, a);
     else
       hipLaunchKernelGGL(k_accum, dim3(qblocks, p.B), dim3(kAccThreads), 0, s, a);
   }

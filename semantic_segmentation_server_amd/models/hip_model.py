@@ -414,12 +414,17 @@ class HipDeepLab:
                         buf("aspp_part", max(ks_opts) * B * h * w * self.cat_c, dtype=torch.float32)
                         bufs["aspp_bias_cat"] = torch.cat(
                             [b0b.float()] + [ab.float() for (_, ab), _ in self.aspp_atrous]).to(dev).contiguous()
+                    ntile = max(-(-(c["perm"].numel() if c.get("perm") is not None else B * h * w) // BM)
+                                for c in convs) * -(-A // K.GROUP_TILE[gv][1])
+                    cnt = buf(f"aspp_cnt{gv}", 4 * ntile, dtype=torch.int32)
                     for ks in ks_opts:
                         order_k = K.grouped_tile_order(convs, gv, dev, ks=ks)
                         bufs[f"aspp_order{gv}k{ks}"] = order_k
-                        grouped.append((f"grouped_v{gv}k{ks}", [
-                            lambda *_, convs=convs, order=order_k, gv=gv, ks=ks: K.conv_gemm_grouped(
-                                convs, order, gv, ks=ks, part=bufs["aspp_part"], bias_cat=bufs["aspp_bias_cat"])]))
+                        for inl in (False, True):  # in-launch combine by each tile's last K slice
+                            grouped.append((f"grouped_v{gv}k{ks}" + ("c" if inl else ""), [
+                                lambda *_, convs=convs, order=order_k, gv=gv, ks=ks, cnt=(cnt if inl else None):
+                                K.conv_gemm_grouped(convs, order, gv, ks=ks, part=bufs["aspp_part"],
+                                                    bias_cat=bufs["aspp_bias_cat"], cnt=cnt)]))
                 # (branch-affine XCD orders, K.grouped_tile_order_branch, measured 6-16 us
                 # slower on every variant: profiles/r3_negative_results.txt)
             ops[aspp_at:] = [Choice("aspp.branches", grouped + [seq])]
@@ -688,12 +693,16 @@ class HipDeepLab:
                         if key not in bufs_part:
                             bufs_part[key] = buf(key, max(hs_opts) * B * h * w * s.cout, dtype=torch.float32)
                         part = bufs_part[key]
+                        # per-span arrival tickets of the in-launch combine ("...c" variants)
+                        cnt = buf(f"b{i}_cnt{S}", B * S, dtype=torch.int32)
                         for hs in hs_opts:
                             for v in ((0, 2) if s.cout <= 96 and s.dilation == 1 else (0,)):
-                                variants.insert(0, (f"stream{S}" + ("", "g", "w")[v] + f"h{hs}", [
-                                    lambda *_, x=inp, out=out, tab=tab, sp=blk["span"], v=v, hs=hs, part=part:
-                                    FS.fused_ir_stream(x, sp, tab, out, B=B, residual=s.residual, variant=v,
-                                                       hsplit=hs, part=part)]))
+                                for inl in (False, True):
+                                    variants.insert(0, (f"stream{S}" + ("", "g", "w")[v] + f"h{hs}" + ("c" if inl else ""), [
+                                        lambda *_, x=inp, out=out, tab=tab, sp=blk["span"], v=v, hs=hs, part=part,
+                                        cnt=(cnt if inl else None): FS.fused_ir_stream(
+                                            x, sp, tab, out, B=B, residual=s.residual, variant=v, hsplit=hs,
+                                            part=part, cnt=cnt)]))
         if blk["expand"] is not None and FB.band_supported(s.cin, hid, s.cout, s.stride, s.dilation, OW):
             # row-streaming bands: every input row expanded once into an on-chip fp16 row
             if "band" not in blk:

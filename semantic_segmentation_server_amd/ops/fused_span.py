@@ -148,7 +148,8 @@ def fused_ir_span(x: torch.Tensor, packed: Dict, table: Dict, out: torch.Tensor,
 
 def fused_ir_stream(x: torch.Tensor, packed: Dict, table: Dict, out: torch.Tensor, *, B: int,
                     residual: bool, trace: Optional[torch.Tensor] = None, variant: int = 0,
-                    hsplit: int = 1, part: Optional[torch.Tensor] = None) -> torch.Tensor:
+                    hsplit: int = 1, part: Optional[torch.Tensor] = None,
+                    cnt: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Launch fused_ir_stream_kernel (csrc/hip/fused_ir_stream.hip): the same spans and
     chunk images as fused_ir_span, run by wave-specialised expansion / depthwise+projection
     waves over an LDS-DMA chunk ring. x [B, H, W, Cin] bf16, out [B, H, W, Cout] bf16.
@@ -157,7 +158,9 @@ def fused_ir_stream(x: torch.Tensor, packed: Dict, table: Dict, out: torch.Tenso
     hsplit > 1: each span's hidden chunks are split over ``hsplit`` workgroups (batch 1 has
     B * S = 16..32 workgroups for 256 CUs and the kernel time is one workgroup's serial chunk
     loop, r4 retune tables); their fp32 partials go to ``part`` [hsplit, B*H*W, Cout] and
-    stream_combine sums them (+ bias, residual) into ``out``."""
+    stream_combine sums them (+ bias, residual) into ``out``; with ``cnt`` (int32 [B*S],
+    zeroed once: each span's last arriving workgroup resets its word) the span's last
+    arriving workgroup does that sum inside the launch instead (no combine kernel)."""
     from .hip_ops import _chk, _dbg, _hip_mod, _ptr, _stream
     H, W = table["H"], table["W"]
     Cin, Cout = packed["Cin"], packed["Cout"]
@@ -174,14 +177,17 @@ def fused_ir_stream(x: torch.Tensor, packed: Dict, table: Dict, out: torch.Tenso
         if part is None:
             raise ValueError("fused_ir_stream: hsplit > 1 needs a partials buffer")
         _chk(part, torch.float32, "part", hsplit * B * H * W * Cout)
+        if cnt is not None:
+            _chk(cnt, torch.int32, "cnt", B * table["S"])
     _hip_mod().fused_ir_stream(_ptr(x), _ptr(packed["w"]), _ptr(packed["bp"]), _ptr(table["table"]),
                                _ptr(out), B, H, W, Cin, packed["hidP"], Cout, table["dil"],
                                int(bool(residual)), table["S"], table["WR"], table["WCP"],
                                table["hstride"], table["nh_max"], _stream(),
                                0 if trace is None else _ptr(trace), int(variant), int(hsplit),
-                               0 if hsplit <= 1 else _ptr(part))
+                               0 if hsplit <= 1 else _ptr(part),
+                               0 if (hsplit <= 1 or cnt is None) else _ptr(cnt))
     _dbg("fused_ir_stream")
-    if hsplit > 1:
+    if hsplit > 1 and cnt is None:
         M = B * H * W
         _hip_mod().stream_combine(_ptr(part), _ptr(packed["bp"]), _ptr(x) if residual else 0, _ptr(out),
                                   int(hsplit), M, Cout, _stream())

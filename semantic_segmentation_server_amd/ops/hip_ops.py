@@ -267,7 +267,8 @@ def grouped_tile_order_branch(convs: List[dict], variant: int, device=None, xcds
 
 
 def conv_gemm_grouped(convs: List[dict], order: torch.Tensor, variant: int = 5, ks: int = 1,
-                      part: Optional[torch.Tensor] = None, bias_cat: Optional[torch.Tensor] = None) -> None:
+                      part: Optional[torch.Tensor] = None, bias_cat: Optional[torch.Tensor] = None,
+                      cnt: Optional[torch.Tensor] = None) -> None:
     """Up to 4 independent stride-1 'same' NHWC convs with one Cout (the ASPP branches)
     in ONE LDS-DMA grid, tiles in the ``grouped_tile_order`` table. Each conv is a
     dict of conv_gemm's arguments: x, w, bias, out, B, IH, IW, Cin, OH, OW, Cout, k,
@@ -276,7 +277,10 @@ def conv_gemm_grouped(convs: List[dict], order: torch.Tensor, variant: int = 5, 
     ``ks`` > 1 (split-K, small batches): the order table (``grouped_tile_order(..., ks=)``)
     carries ks K slices per tile; their fp32 partials go to ``part`` [ks, B*OH*OW, ldo]
     and stream_combine adds them, ``bias_cat`` (the branches' biases at their co_off) and
-    the shared activation into ``out``: the convs must tile [0, ldo) of one output."""
+    the shared activation into ``out``: the convs must tile [0, ldo) of one output. With
+    ``cnt`` (int32, >= 4 x the largest conv's tile count, zeroed once: the last arriver of
+    each tile resets its word) the tile's last arriving K slice does that sum inside the
+    launch (no combine kernel; ``bias_cat`` is then unused)."""
     if not 1 <= len(convs) <= 4:
         raise ValueError("conv_gemm_grouped: 1..4 convs")
     if variant not in GROUP_TILE:
@@ -335,10 +339,13 @@ def conv_gemm_grouped(convs: List[dict], order: torch.Tensor, variant: int = 5, 
             raise ValueError("conv_gemm_grouped: split-K convs must share one output")
         _chk(part, torch.float32, "part", ks * Mo * ldo)
         _chk(bias_cat, torch.float32, "bias_cat", ldo)
+        if cnt is not None:
+            _chk(cnt, torch.int32, "cnt", 4 * max(tiles))
     _hip_mod().conv_gemm_grouped(groups, _ptr(order), order.numel(), variant, _stream(), int(ks),
-                                 _ptr(part) if ks > 1 else 0)
+                                 _ptr(part) if ks > 1 else 0, _ptr(cnt) if (ks > 1 and cnt is not None) else 0,
+                                 max(tiles))
     _dbg('conv_gemm_grouped')
-    if ks > 1:
+    if ks > 1 and cnt is None:
         _hip_mod().stream_combine(_ptr(part), _ptr(bias_cat), 0, _ptr(c0["out"]), int(ks), Mo, ldo, _stream(),
                                   1 if c0.get("act") == "relu" else 0)
         _dbg('stream_combine')

@@ -175,6 +175,15 @@ def test_conv_gemm_grouped_aspp_splitk(B, variant, ks):
     K.conv_gemm_grouped(convs, order, variant, ks=ks, part=part, bias_cat=bias_cat)
     torch.cuda.synchronize()
     assert torch.equal(first.view(torch.int16), out.view(torch.int16))
+    # in-launch combine by each tile's last arriving K slice: same fixed-order sums, so
+    # bit-identical to the combine kernel; tickets reset for the next launch
+    cnt = torch.zeros(4 * 1024, dtype=torch.int32, device=DEV)
+    for rep in range(3):
+        out.fill_(float("nan"))
+        K.conv_gemm_grouped(convs, order, variant, ks=ks, part=part, bias_cat=bias_cat, cnt=cnt)
+        torch.cuda.synchronize()
+        assert torch.equal(first.view(torch.int16), out.view(torch.int16)), rep
+        assert int(cnt.abs().sum()) == 0, rep
 
 
 @pytest.mark.parametrize("img", [True, False])
@@ -399,10 +408,11 @@ def test_upsample_argmax(h, H, K, variant):
     assert agree > 0.9999, agree
 
 
-@pytest.fixture(params=[1, 0], ids=["tiles", "strips"])
+@pytest.fixture(params=[1, 2, 0], ids=["tiles", "tiles64", "strips"])
 def post_accum(request, monkeypatch):
-    """Both accumulation passes of the device post-processing (LDS-staged 32 x 32 tiles,
-    the default since round 4, and round 3's pixel strips) must give the spec's records."""
+    """Every accumulation pass of the device post-processing (LDS-staged 32 x 32 tiles,
+    the default since round 4, 64 x 64 tiles, and round 3's pixel strips) must give the
+    spec's records."""
     monkeypatch.setenv("SSA_POST_ACCUM", str(request.param))
     return request.param
 
@@ -1371,6 +1381,17 @@ def test_fused_ir_stream(cin, cout, dil, H, S):
         FS.fused_ir_stream(xd, packed, table, out2, B=B, residual=spec.residual, hsplit=hs, part=part)
         torch.cuda.synchronize()
         assert torch.equal(out.view(torch.int16), out2.view(torch.int16)), hs
+        # in-launch combine (each span's last arriving workgroup sums the slabs): the same
+        # fixed-order arithmetic as stream_combine, so bit-identical; the tickets come back
+        # zeroed, so repeated launches (graph replays) agree too
+        cnt = torch.zeros(B * S, dtype=torch.int32, device=DEV)
+        for rep in range(3):
+            out3 = torch.full_like(out, float("nan"))
+            FS.fused_ir_stream(xd, packed, table, out3, B=B, residual=spec.residual, hsplit=hs, part=part,
+                               cnt=cnt)
+            torch.cuda.synchronize()
+            assert torch.equal(out.view(torch.int16), out3.view(torch.int16)), (hs, rep)
+            assert int(cnt.abs().sum()) == 0, (hs, rep)
 
 
 @pytest.mark.parametrize("M,HW,ncls,ldo,img", [
