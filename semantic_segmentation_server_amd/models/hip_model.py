@@ -291,6 +291,7 @@ class HipDeepLab:
 
         def buf(name, *shape, dtype=torch.bfloat16):
             # zeroed for tidiness only: no picked kernel reads plan bytes it did not write
+            # (plan constants kept among the buffers are named const_*, pool_w*)
             # (scripts/debug_poison.py run B: NaN-filled buffers give bit-identical labels;
             # tests/test_hip_kernels.py::test_plan_is_a_function_of_the_frame, at 257^2 and
             # at the headline 513^2 / 640x480 shape with the B = 32 plan's kernels)
@@ -412,7 +413,7 @@ class HipDeepLab:
                 if ks_opts and gv in (5, 17, 18) and A * (len(self.aspp_atrous) + 1) == self.cat_c:
                     if "aspp_part" not in bufs:
                         buf("aspp_part", max(ks_opts) * B * h * w * self.cat_c, dtype=torch.float32)
-                        bufs["aspp_bias_cat"] = torch.cat(
+                        bufs["const_aspp_bias_cat"] = torch.cat(
                             [b0b.float()] + [ab.float() for (_, ab), _ in self.aspp_atrous]).to(dev).contiguous()
                     ntile = max(-(-(c["perm"].numel() if c.get("perm") is not None else B * h * w) // BM)
                                 for c in convs) * -(-A // K.GROUP_TILE[gv][1])
@@ -424,7 +425,7 @@ class HipDeepLab:
                             grouped.append((f"grouped_v{gv}k{ks}" + ("c" if inl else ""), [
                                 lambda *_, convs=convs, order=order_k, gv=gv, ks=ks, cnt=(cnt if inl else None):
                                 K.conv_gemm_grouped(convs, order, gv, ks=ks, part=bufs["aspp_part"],
-                                                    bias_cat=bufs["aspp_bias_cat"], cnt=cnt)]))
+                                                    bias_cat=bufs["const_aspp_bias_cat"], cnt=cnt)]))
                 # (branch-affine XCD orders, K.grouped_tile_order_branch, measured 6-16 us
                 # slower on every variant: profiles/r3_negative_results.txt)
             ops[aspp_at:] = [Choice("aspp.branches", grouped + [seq])]

@@ -25,8 +25,19 @@ class DevicePostprocess:
         self.palette = torch.tensor(np.asarray(palette, np.int32).reshape(256, 3), device=device)
         self._bufs: Dict[int, tuple] = {}
         self._host: Dict[int, torch.Tensor] = {}
-        # accumulation pass: LDS-staged 32 x 32 tiles (1) or pixel strips (0)
-        self.accum = int(os.environ.get("SSA_POST_ACCUM", "1"))
+        # accumulation pass: pixel strips (0), LDS-staged 32 x 32 (1) or 64 x 64 (2) tiles;
+        # unset: by batch size (accum_for)
+        env = os.environ.get("SSA_POST_ACCUM")
+        self.accum = int(env) if env is not None else None
+
+    def accum_for(self, B: int) -> int:
+        """The accumulation pass for a batch of B frames: the strips at batch <= 2 (a
+        frame is 221 tiles for 256 CUs there: 19.7 us strips vs 26.9 us tiles at batch 1,
+        profiles/r3h_b1_layer_times.txt, r4_b1_layer_times.txt), the 32 x 32 tiles above
+        (94.5 vs 124.6 us at batch 32, r4a_layer_times.txt vs r3_v7_layer_times.txt)."""
+        if self.accum is not None:
+            return self.accum
+        return 0 if B <= 2 else 1
 
     def _buffers(self, B: int):
         if B not in self._bufs:
@@ -52,7 +63,7 @@ class DevicePostprocess:
             rec = out
         hip_ops.postprocess(labels, self.palette, ws, rec, B=B, H=self.H, W=self.W, crop_h=crop_h,
                             crop_w=crop_w, min_area=min_area, K=self.K, bins=self.bins, thr=self.thr,
-                            accum=self.accum)
+                            accum=self.accum_for(B))
         return rec
 
     def fetch(self, rec: torch.Tensor, frame_ids: Sequence[int], ts: Sequence[float],
