@@ -11,6 +11,7 @@
 #   bench100     100 timed steps, RPC under load
 #   b1           batch-1 bench (400 steps)
 #   b1lat        batch-1 bench at lag 0 (each step's records collected in the step: latency mode)
+#   b1lag1       batch-1 bench at lag 1
 #   cfg4         DeepLabv3-ResNet50 1025^2 int8 B=8 (60 steps) and bf16
 #   cfg5         4 camera streams x 8 frames (batched step)
 #   prof         sequential kernel trace of the B=32 step -> layer_times.txt
@@ -70,6 +71,7 @@ for step in "$@"; do
     bench100) bench s100 300 --steps 100 --warmup 10 || exit 2 ;;
     b1)      bench b1 300 --batch 1 --steps 400 --warmup 50 --rpc 0 || exit 2 ;;
     b1lat)   bench b1lat 300 --batch 1 --lag 0 --steps 400 --warmup 50 --rpc 0 || exit 2 ;;
+    b1lag1)  bench b1lag1 300 --batch 1 --lag 1 --steps 400 --warmup 50 --rpc 0 || exit 2 ;;
     cfg4)    bench c4i8 400 --arch resnet50 --input_size 1025 --camera 2048x1024 --batch 8 --dtype int8 --steps 60 --warmup 5 --rpc 0 \
                && bench c4bf 400 --arch resnet50 --input_size 1025 --camera 2048x1024 --batch 8 --steps 60 --warmup 5 --rpc 0 || exit 2 ;;
     cfg5)    bench c5 300 --streams 4 --batch 32 --steps 100 --warmup 10 --rpc 0 || exit 2 ;;
