@@ -97,9 +97,12 @@ def main() -> int:
     import torch as _t
     world = int(os.environ.get("WORLD_SIZE", "1"))
     gpu = _t.cuda.is_available() and a.backend != "cpu"
+    # SSA_SHARE_GPU=1 (rehearsal: several ranks on one GPU): RCCL refuses two ranks on one
+    # device, so the auto choice is the gloo group with the host-memory gather
+    share = os.environ.get("SSA_SHARE_GPU", "0") == "1"
     pg = a.pg if a.pg != "auto" else (
-        "nccl" if gpu and (a.ingest == "scatter" or a.gather == "rccl" or
-                           (a.gather == "auto" and world > 1)) else "gloo")
+        "nccl" if gpu and not share and (a.ingest == "scatter" or a.gather == "rccl" or
+                                         (a.gather == "auto" and world > 1)) else "gloo")
     ctx = D.init(pg, device="cuda" if _t.cuda.is_available() and a.backend != "cpu" else "auto")
     cam_w, cam_h = (int(v) for v in a.camera.split("x"))
     cfg = C.Config(arch=a.arch, aspp=a.aspp, input_size=a.input_size, backend=a.backend,

@@ -27,6 +27,7 @@ re-forming. ``--inject_fault rank:step`` raises on that (launch) rank / step (te
 from __future__ import annotations
 
 import logging
+import os
 import signal
 import threading
 import time
@@ -68,7 +69,9 @@ class DistributedServer:
         self.gather = cfg.gather
         if self.gather == "auto" and cfg.degrade:
             self.gather = "host"
-        pg = "nccl" if gpu and (cfg.ingest == "scatter" or self.gather in ("auto", "rccl")) else "gloo"
+        # SSA_SHARE_GPU=1 (several ranks on one GPU, a rehearsal): RCCL refuses that, gloo
+        share = os.environ.get("SSA_SHARE_GPU", "0") == "1"
+        pg = "nccl" if gpu and not share and (cfg.ingest == "scatter" or self.gather in ("auto", "rccl")) else "gloo"
         self.ctx = ctx or D.init(pg, timeout_s=cfg.rank_timeout,
                                  device="cuda" if torch.cuda.is_available() and cfg.device != "cpu"
                                  else "auto")
