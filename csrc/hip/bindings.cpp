@@ -140,7 +140,8 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("residual"), py::arg("nspan"), py::arg("WR"), py::arg("WCP"), py::arg("hstride"),
         py::arg("nh_max"), py::arg("stream"), py::arg("trace") = 0, py::arg("variant") = 0,
         py::arg("hsplit") = 1, py::arg("part") = 0, py::arg("cnt") = 0);
-  m.def("fused_ir_stream_lds", &fused_ir_stream_lds);
+  m.def("fused_ir_stream_lds", &fused_ir_stream_lds, py::arg("Cin"), py::arg("Cout"), py::arg("WR"),
+        py::arg("WCP"), py::arg("nsl") = 0);
   m.def("stream_combine",
         [](uintptr_t part, uintptr_t bp, uintptr_t res, uintptr_t out, int HS, long long M, int Cout,
            uintptr_t stream, int act) {

@@ -47,7 +47,7 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // waves per workgroup: 8 (4 expansion + 4 depthwise/projection) or, for the MODE-2
 // variant, 12 (4 + 8: two depthwise/projection waves per SIMD hide each other's LDS and
 // VALU latency -- the same lever that took the grouped ASPP GEMM from 8 to 16 waves)
-__host__ __device__ constexpr int stream_waves(int mode) { return mode == 2 ? 12 : 8; }
+__host__ __device__ constexpr int stream_waves(int mode) { return (mode & 3) == 2 ? 12 : 8; }
 constexpr int kHdr = 4;    // span table header: p0, p1, wy0, nh
 constexpr int kXQ = 5;     // halo groups per expansion wave (<= 20 groups = 320 halo px)
 constexpr int kGB = 3;     // output groups per depthwise+projection wave (<= 12 groups)
@@ -248,12 +248,15 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
   // MODE 0: 8 waves, the ninth output group split over the projection waves;
   // 1 (G8A): 8 waves, the ninth group on the expansion waves; 2: 12 waves, projection
   // wave b owns group b, wave 7 also the ninth group
-  constexpr bool G8A = MODE == 1;
+  // MODE & 4: a 3-slot chunk ring (one chunk of DMA lookahead) for the blocks whose default is
+  // 4 slots: 72 instead of 81 KiB for blocks 7-9, so two workgroups -- of one plan copy or of
+  // two slots' concurrent steps -- can share a CU's 160 KiB of LDS
+  constexpr bool G8A = (MODE & 3) == 1;
   constexpr int kNW = stream_waves(MODE), kNT = 64 * kNW;
   constexpr int NPC = 2 * KS + NS + 1;          // 1 KiB pieces per chunk image
   constexpr int CHB = NPC * 1024;
   constexpr int WEB = 2 * KS * 1024, WPB = NS * 1024;
-  constexpr int kNSL = stream_nsl(NS);
+  constexpr int kNSL = (MODE & 4) ? 3 : stream_nsl(NS);
   constexpr int LAG = kNSL - 2;
   // every wave issues MP pieces per chunk (the last piece duplicated where NPC % 8 != 0:
   // identical bytes to the same slot), so the counted waits are compile-time constants
@@ -297,7 +300,7 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
   // two role-private arrays by itself: 190..256 VGPRs + spills against max(A, BC))
   constexpr int NS3 = NS >= 10 ? NS / 2 : NS;
   constexpr int Q8 = (NS + 3) / 4;  // G8A: group-8 subtiles per expansion wave
-  constexpr int NRA = XQ * KS + (G8A ? Q8 : 0), NRB = (G8A || MODE == 2) ? 2 * NS : 2 * NS + NS3;
+  constexpr int NRA = XQ * KS + (G8A ? Q8 : 0), NRB = (G8A || (MODE & 3) == 2) ? 2 * NS : 2 * NS + NS3;
   constexpr int NR = NRA > NRB ? NRA : NRB;
   f32x4 R[NR];
   int hpos[kXQ];
@@ -339,7 +342,7 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
   // split it for the wide blocks, waves 2/3 compute a copy that is never stored.
   const bool expander = wid < 4;
   const int bw = wid - 4;
-  const int og[kGB] = {MODE == 2 ? bw : 3 - bw, MODE == 2 ? 8 : 7 - bw, 8};
+  const int og[kGB] = {(MODE & 3) == 2 ? bw : 3 - bw, (MODE & 3) == 2 ? 8 : 7 - bw, 8};
   const int n3 = NS3 == NS ? 0 : (bw & 1) * NS3;
   const bool own3 = NS3 == NS ? bw == 0 : bw < 2;
   int dpos[kGB];
@@ -378,7 +381,7 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
     } else if (t >= 1) {
       const int c = t - 1;
       const char* Wp = ring + (c % kNSL) * CHB + WEB;
-      if (MODE == 2) {
+      if ((MODE & 3) == 2) {
         const char* Ek = sE + (c & 1) * 4 * PLANE + kq * PLANE;
         dwproj_groups<1, NS, DIL, WCP, NR>(Wp, Wp + WPB, Ek, dpos8, 0, NS - 1, R, 0, lane, kq);
         if (bw == 7) {
@@ -419,9 +422,9 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
       for (int g = 0; g < 2; ++g)
 #pragma unroll
         for (int n = 0; n < NS; ++n)
-          if (n / NSP == h && (MODE != 2 || g == 0 || bw == 7))
+          if (n / NSP == h && ((MODE & 3) != 2 || g == 0 || bw == 7))
             *reinterpret_cast<f32x4*>(O + (og[g] * 16 + r16) * OS + (n - h * NSP) * 16 + kq * 4) = R[g * NS + n];
-      if (own3 && MODE == 0) {
+      if (own3 && (MODE & 3) == 0) {
 #pragma unroll
         for (int n = 0; n < NS3; ++n)
           if ((n3 + n) / NSP == h)
@@ -520,7 +523,7 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
 
 template <int KS, int NS, int XQ, int DIL, int WCP, int MODE>
 void launch_stream(const StreamArgs& a, hipStream_t st) {
-  const size_t lds = fused_ir_stream_lds(a.Cin, a.Cout, a.WR, a.WCP);
+  const size_t lds = fused_ir_stream_lds(a.Cin, a.Cout, a.WR, a.WCP, (MODE & 4) ? 3 : 0);
   if (lds > 160 * 1024) throw std::invalid_argument("fused_ir_stream: LDS over 160 KiB");
   static bool attr = false;
   if (!attr) {
@@ -536,9 +539,10 @@ void launch_stream(const StreamArgs& a, hipStream_t st) {
 
 }  // namespace
 
-size_t fused_ir_stream_lds(int Cin, int Cout, int WR, int WCP) {
+size_t fused_ir_stream_lds(int Cin, int Cout, int WR, int WCP, int nsl) {
   const int KS = Cin / 32, NS = (Cout + 15) / 16;
-  const size_t main = (size_t)stream_nsl(NS) * (2 * KS + NS + 1) * 1024 + 8 * (size_t)stream_plane_bytes(WR, WCP);
+  const size_t main = (size_t)(nsl > 0 ? nsl : stream_nsl(NS)) * (2 * KS + NS + 1) * 1024 +
+                      8 * (size_t)stream_plane_bytes(WR, WCP);
   const size_t otile = (size_t)kGB * 4 * 16 * (NS / stream_npass(NS) * 16 + 4) * 4;  // epilogue tile
   return main > otile ? main : otile;
 }
@@ -564,17 +568,24 @@ void fused_ir_stream(const FusedSpanParams& p, hipStream_t st) {
     throw std::invalid_argument("fused_ir_stream: W 33, dilation 1/2, halo <= 256/320 px");
   // an unknown variant, or the 12-wave variant where it is not instantiated, must not
   // silently launch another kernel under the requested name
-  if (p.npi < 0 || p.npi > 2) throw std::invalid_argument("fused_ir_stream: variant must be 0, 1 or 2");
-  if (p.npi == 2 && (p.dil != 1 || NS > 6))
+  // variants: 0 / 1 (G8A) / 2 (12 waves); + 4: the 3-slot chunk ring (blocks with NS <= 10)
+  if (!(p.npi == 0 || p.npi == 1 || p.npi == 2 || p.npi == 4 || p.npi == 6))
+    throw std::invalid_argument("fused_ir_stream: variant must be 0, 1, 2, 4 or 6");
+  if ((p.npi & 3) == 2 && (p.dil != 1 || NS > 6))
     throw std::invalid_argument("fused_ir_stream: the 12-wave variant needs dilation 1 and Cout <= 96");
+  if ((p.npi & 4) && NS > 10)
+    throw std::invalid_argument("fused_ir_stream: the 3-slot variant is for Cout <= 160 (wider blocks use 3 slots)");
   // 12-wave variant: blocks 7-12 (Cout <= 96; at Cout 160 the accumulators spill at 168 VGPRs)
 #define STREAM12(K_, N_) ((N_) <= 6 ? 2 : 0)
 #define STREAM(K_, N_)                                   \
   if (KS == K_ && NS == N_) {                            \
     if (p.dil == 1 && p.npi == 2) launch_stream<K_, N_, 4, 1, 49, STREAM12(K_, N_)>(a, st);  \
+    else if (p.dil == 1 && p.npi == 6) launch_stream<K_, N_, 4, 1, 49, 4 + STREAM12(K_, N_)>(a, st);  \
     else if (p.dil == 1 && p.npi == 1) launch_stream<K_, N_, 4, 1, 49, 1>(a, st);        \
+    else if (p.dil == 1 && p.npi == 4) launch_stream<K_, N_, 4, 1, 49, 4>(a, st);        \
     else if (p.dil == 1) launch_stream<K_, N_, 4, 1, 49, 0>(a, st);                      \
     else if (p.npi == 1) launch_stream<K_, N_, 5, 2, 49, 1>(a, st);                      \
+    else if (p.npi == 4) launch_stream<K_, N_, 5, 2, 49, 4>(a, st);                      \
     else launch_stream<K_, N_, 5, 2, 49, 0>(a, st);                                      \
     return;                                              \
   }

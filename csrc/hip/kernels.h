@@ -146,7 +146,7 @@ size_t fused_ir_span_lds(int Cin, int Cout, int WR, int WCP, int xslots);
 // Wave-specialised variant over the same spans / chunk images (fused_ir_stream.hip):
 // expansion waves 0-3, depthwise+projection waves 4-7, LDS-DMA chunk ring.
 void fused_ir_stream(const FusedSpanParams& p, hipStream_t s);
-size_t fused_ir_stream_lds(int Cin, int Cout, int WR, int WCP);
+size_t fused_ir_stream_lds(int Cin, int Cout, int WR, int WCP, int nsl = 0);
 // sum of the hidden-split partials + bias (+ residual) -> bf16 [M, Cout]
 void stream_combine(const float* part, const float* bp, const bf16* res, bf16* out, int HS, long long M, int Cout,
                     hipStream_t st, int act = 0);

@@ -115,7 +115,9 @@ class Choice:
                 # (all batch-1 variants of blocks 7-10 read 16-17 us, r4 retune tables)
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                # thread-local capture: a plan built lazily while another thread (feeder,
+                # result collector) uses the device must not invalidate their calls
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
                     for _ in range(reps):
                         for op in ops:
                             op(*args)
@@ -681,8 +683,12 @@ class HipDeepLab:
                             x, sp, tab, out, B=B, residual=s.residual, npi=npi)]))
                 if FS.stream_supported(s.cin, s.cout, 1, h, w, S, s.dilation):
                     # wave-specialised: expansion waves | depthwise+projection waves
-                    for v in ((0, 1, 2) if s.cout <= 96 and s.dilation == 1 else (0, 1)):
-                        variants.insert(0, (f"stream{S}" + ("", "g", "w")[v], [
+                    # 4 / 6: the 3-slot chunk ring (72 instead of 81 KiB for blocks 7-9: two
+                    # workgroups per CU)
+                    vs = ((0, 1, 2) if s.cout <= 96 and s.dilation == 1 else (0, 1)) + \
+                        ((4,) if s.cout <= 160 else ()) + ((6,) if s.cout <= 96 and s.dilation == 1 else ())
+                    for v in vs:
+                        variants.insert(0, (f"stream{S}" + {0: "", 1: "g", 2: "w", 4: "r3", 6: "wr3"}[v], [
                             lambda *_, x=inp, out=out, tab=tab, sp=blk["span"], v=v: FS.fused_ir_stream(
                                 x, sp, tab, out, B=B, residual=s.residual, variant=v)]))
                     # small batches: the hidden chunks of a span over hs workgroups (fp32

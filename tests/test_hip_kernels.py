@@ -1354,7 +1354,9 @@ def test_fused_ir_stream(cin, cout, dil, H, S):
     table = FS.span_table(H, W, S, dil, DEV)
     xd = _nhwc(x).to(DEV)
     emu = FS.emulate_fused_span(_nhwc(x).float().numpy(), packed, table, residual=spec.residual)
-    for variant in ((0, 1, 2) if cout <= 96 and dil == 1 else (0, 1)):
+    variants = ((0, 1, 2) if cout <= 96 and dil == 1 else (0, 1)) + ((4,) if cout <= 160 else ()) + \
+        ((6,) if cout <= 96 and dil == 1 else ())  # 4 / 6: the 3-slot chunk ring
+    for variant in variants:
         out = torch.full((B, H, W, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
         FS.fused_ir_stream(xd, packed, table, out, B=B, residual=spec.residual, variant=variant)
         torch.cuda.synchronize()
