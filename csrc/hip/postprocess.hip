@@ -12,8 +12,9 @@
 //                BGR2GRAY on RGB (fixed point) -> > thr, then union-find in LDS:
 //                foreground 8-connected, background 4-connected; zeroes the counters
 //   k_ccl_edges  cross-tile unions as pairs of tile-local roots
-//   k_ccl_merge  one workgroup per frame: union-find over those pairs in LDS (or, for
-//                frames past its caps, a global union-find across the tile edges);
+//   k_ccl_merge  one workgroup per frame: union-find over those pairs in LDS (frames past
+//                its caps: flagged for k_fb_unite / k_fb_relabel, a global union-find
+//                across the tile edges and a relabel, grid-wide);
 //                image-border background joins the virtual "outside" node 0; final
 //                labels of the tile-local roots (component root = raster index of its
 //                first pixel + 1, 0 = outside); roots zero their accumulators
@@ -360,10 +361,10 @@ __global__ __launch_bounds__(kCclThreads) void k_ccl_local(KArgs a, const int32_
 //   afterwards (fin(): L -> tile-local root -> cidx): no full-frame relabelling pass
 //   (round 2's k_compress, 22 us per 32 frames).
 // Frames past kMergeCap roots or kEdgeCap pairs take the global union-find (device-
-// coherent pointer chasing) across the tile edges and a relabelling pass instead, both
-// run by the merge workgroup; fin() then reads the final label straight from L. (Round
-// 2 launched that fallback as its own full-grid kernel: 5-8 us per 32 frames that
-// almost never need it.)
+// coherent pointer chasing) across the tile edges and a relabelling pass instead:
+// k_ccl_merge flags them and two grid kernels (k_fb_unite, k_fb_relabel) do the work,
+// leaving at once for unflagged frames; fin() then reads the final label straight from L.
+// (Round 3 ran the fallback inside the merge workgroup: 813 us per flagged frame.)
 __device__ __forceinline__ void emit_pairs(FrameWS& f, int n, const int (&pa)[3], const int (&pb)[3]) {
   // wave-aggregated append of this lane's n pairs
   int incl = n;
@@ -528,28 +529,7 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(KArgs a) {
   const int E = f.nslot[2];
   const int N = ch * cw;
   if (tid == 0) f.flag[0] = (R > kMergeCap || E > kEdgeCap) ? 1 : 0;
-  if (R > kMergeCap || E > kEdgeCap) {
-    for (int p = tid; p < N; p += 1024) ccl_boundary_pixel(a, f, p);
-    __threadfence();
-    __syncthreads();
-    // Read-only traversal: a path-halving store here could overwrite another thread's
-    // final root store with a stale grandparent (observed: 1 pixel in ~1M left pointing
-    // at a non-root). Every concurrent store below writes a root, so plain traversal
-    // always terminates at the true root.
-    for (int p = tid; p < N; p += 1024) {
-      const int r = find_root(f.L, p + 1);
-      __hip_atomic_store(f.L + p + 1, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (r == p + 1) add_root(f, a.bins, p, s_nr);
-    }
-    __syncthreads();
-    const int nr = *s_nr;
-    for (int i = tid; i < nr; i += 1024) {
-      const int p = f.rlist[i];
-      f.rpar[p] = p % cw > 0 ? ld_relaxed(f.L + p) : 0;
-    }
-    if (tid == 0) f.nslot[3] = nr;
-    return;
-  }
+  if (R > kMergeCap || E > kEdgeCap) return;  // k_fb_unite / k_fb_relabel take the frame
   const int OUT = R;
   for (int i = tid; i <= R; i += 1024) {
     par[i] = i;
@@ -649,6 +629,43 @@ __device__ __forceinline__ void ccl_boundary_pixel(KArgs& a, FrameWS& f, int p) 
       const int prev = (y == 0 || y == a.ch - 1) ? (x > 0 && (x % TW) != 0 ? p - 1 : -1)
                                                  : ((y % TH) != 0 ? p - a.cw : -1);
       if (prev < 0 || f.mask[prev] || lroot(prev) != lroot(p)) unite(f.L, me, 0);
+    }
+  }
+}
+
+// Fallback for frames past the LDS merge's caps (more than kMergeCap tile-local roots or
+// kEdgeCap cross-tile pairs: speckled maps). Round 3 ran it inside k_ccl_merge, one
+// workgroup per frame: 813 us for a frame of ~12k components (the lattice maps
+// of csrc/tools/post_bench.hip). Here two grid kernels that every frame's blocks leave at
+// once unless k_ccl_merge flagged the frame: the global union-find across the tile edges,
+// then the relabel (every pixel's root, read-only traversal: concurrent stores only ever
+// write roots), the roots' accumulators zeroed and listed, and each root's border-tree
+// parent (the final label of the pixel left of it, resolved by the same traversal).
+constexpr int kFbBlocks = 96;  // blocks per frame (grid-stride over the frame's pixels)
+
+__global__ __launch_bounds__(256) void k_fb_unite(KArgs a) {
+  FrameWS f = frame_ws(a.ws, a.lay, a.B, blockIdx.y);
+  if (__builtin_amdgcn_readfirstlane(f.flag[0]) == 0) return;
+  const int N = a.ch * a.cw;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < N; p += gridDim.x * 256) ccl_boundary_pixel(a, f, p);
+}
+
+__global__ __launch_bounds__(256) void k_fb_relabel(KArgs a) {
+  FrameWS f = frame_ws(a.ws, a.lay, a.B, blockIdx.y);
+  if (__builtin_amdgcn_readfirstlane(f.flag[0]) == 0) return;
+  const int N = a.ch * a.cw;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < N; p += gridDim.x * 256) {
+    const int r = find_root(f.L, p + 1);
+    __hip_atomic_store(f.L + p + 1, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (r == p + 1) {
+      f.slot[p] = -1;
+      f.t00[p] = 0;
+      f.t10[p] = 0;
+      f.t01[p] = 0;
+      int* h = f.th + (size_t)p * a.bins;
+      for (int c = 0; c < a.bins; ++c) h[c] = 0;
+      f.rpar[p] = p % a.cw > 0 ? find_root(f.L, p) : 0;
+      f.rlist[atomicAdd(f.nslot + 3, 1)] = p;  // nslot[3] zeroed by k_ccl_local
     }
   }
 }
@@ -1462,6 +1479,11 @@ void postprocess(const PostParams& p, hipStream_t s) {
       attr = true;
     }
     if (st++ < stages) hipLaunchKernelGGL(k_ccl_merge, dim3(p.B), dim3(1024), lds, s, a);
+    if (st++ < stages) {  // no-ops unless k_ccl_merge flagged the frame (caps exceeded)
+      const dim3 gfb(std::min(kFbBlocks, cdiv(N, 256)), p.B);
+      hipLaunchKernelGGL(k_fb_unite, gfb, dim3(256), 0, s, a);
+      hipLaunchKernelGGL(k_fb_relabel, gfb, dim3(256), 0, s, a);
+    }
   }
   // strip-privatised pass: kQuadBlocks strips per frame (SSA_QUAD_BLOCKS overrides, tuning)
   // rounds of 256 pixels per block chosen first, so no block ends with a near-empty round

@@ -51,6 +51,12 @@ static void make_maps(std::vector<uint8_t>& m, int B, int H, int W, int ch, int 
         for (int x = 200; x < cw; ++x) f[y * W + x] = 12;
       continue;
     }
+    if (kind == 4) {  // lattice: 3x3 person blocks at period 4 -> one fg pixel each after the
+                      // blur, ~12k components per frame: past the LDS merge's caps (fallback)
+      for (int y = 0; y < ch; ++y)
+        for (int x = 0; x < cw; ++x) f[y * W + x] = (y % 4 < 3 && x % 4 < 3) ? 15 : 0;
+      continue;
+    }
     const int nb = 3 + (int)(U(rng) * 8);
     for (int k = 0; k < nb; ++k) {
       const float cx = U(rng) * cw, cy = U(rng) * ch, rx = 10 + U(rng) * 90, ry = 10 + U(rng) * 90;
@@ -91,12 +97,15 @@ int main(int argc, char** argv) {
   chk(hipEventCreate(&e0), "ev");
   chk(hipEventCreate(&e1), "ev");
   printf("workspace %.1f MB/frame\n", wsb / (double)B / 1e6);
-  const char* names[4] = {"flat", "planted", "noisy", "file"};
-  const int kinds = argc > 2 ? 4 : 3, k0 = argc > 3 ? 3 : 0;  // argv[3]: the file kind only
+  const char* names[5] = {"flat", "planted", "noisy", "file", "lattice"};
+  // kinds 0-2 and 4 (lattice: the union-find fallback); 3 = argv[2]'s maps (argv[3]: only those)
+  std::vector<int> kinds = {0, 1, 2, 4};
+  if (argc > 2) kinds.push_back(3);
+  if (argc > 3) kinds = {3};
   std::vector<float> rec((size_t)B * (1 + 5 * K));
-  for (int kind = k0; kind < kinds; ++kind) {
+  for (int kind : kinds) {
     std::vector<uint8_t> maps;
-    if (kind < 3) {
+    if (kind != 3) {
       make_maps(maps, B, H, W, ch, cw, kind, 1234 + kind);
     } else {
       maps.resize((size_t)B * H * W);

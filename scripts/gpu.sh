@@ -21,6 +21,7 @@
 #   share8       the dp8 bench path with 8 ranks sharing this one GPU (SSA_SHARE_GPU=1, gloo;
 #                completes end to end -- its throughput is not a scaling number)
 #   postab       post-processing harness (tools/bin/post_bench), strips vs 32^2 / 64^2 tile accumulation
+#   posttrace    post_bench (4 map kinds incl. the fallback-path lattice) under a kernel trace
 #   repro        packed-f32 co-residence reproducer, both builds (csrc/tools/packed_f32_repro.hip)
 #   retune:LIST  re-time the named choices (comma list) at B = ${TUNE_B:-32} on top of the committed
 #                picks -> $O/tune.json (copy into assets/tune_mi355x.json to commit)
@@ -92,6 +93,11 @@ for step in "$@"; do
              cut -c1-600 $O/share8.json ;;
     postab)  for m in 0 1 2; do SSA_POST_ACCUM=$m timeout -k 10 120 tools/bin/post_bench 50 > $O/post_accum$m.txt 2>&1 \
                || { tail -5 $O/post_accum$m.txt; exit 7; }; echo "accum=$m"; cat $O/post_accum$m.txt; done ;;
+    posttrace) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+               -d $REPO/$O/posttrace -o run --output-format csv -- $REPO/tools/bin/post_bench 20 \
+               > $REPO/$O/posttrace.log 2>&1) || { tail -5 $O/posttrace.log; exit 7; }
+             grep -E "us/call|workspace" $O/posttrace.log
+             head -12 $(ls $O/posttrace/*/run_kernel_stats.csv $O/posttrace/run_kernel_stats.csv 2>/dev/null | head -1) | cut -d, -f1-8 ;;
     repro)   for b in repro_pk repro_nopk; do timeout -k 10 300 tools/bin/$b ${REPRO_REPS:-400} > $O/$b.txt 2>&1 \
                || { tail -5 $O/$b.txt; exit 7; }; cat $O/$b.txt; done ;;
     retune:*) [ -f $O/tune.json ] || cp assets/tune_mi355x.json $O/tune.json
