@@ -273,6 +273,7 @@ class HipDeepLab:
         # set by the DP pipeline at world > 1: rank 0's autotune picks -> every rank
         self.pick_sync: Optional[Callable[[Optional[dict]], dict]] = None
         self._plans: Dict[tuple, Tuple[List[Callable], Dict[str, torch.Tensor]]] = {}
+        self._side_streams: List[torch.cuda.Stream] = []  # SSA_POOL_FORK side streams (one per plan)
         self._span_tables: Dict[tuple, dict] = {}
         self._labels_out: Optional[torch.Tensor] = None
         self._guards: list = []  # SSA_GUARD_BYTES debug bands (name, raw, guard, nbytes)
@@ -441,8 +442,29 @@ class HipDeepLab:
                 w1t = self.pool_w.t().contiguous()
                 w2t = self.proj_pool_w.t().contiguous()
                 bufs["pool_w1t"], bufs["pool_w2t"] = w1t, w2t
-                ops.append(lambda *_, x=x, h=h, w=w, c=c, w1t=w1t, w2t=w2t: K.aspp_pool(
+                pool_op = (lambda *_, x=x, h=h, w=w, c=c, w1t=w1t, w2t=w2t: K.aspp_pool(
                     x, gws, w1t, self.pool_b, w2t, img_bias, B=B, HW=h * w, C=c, N=A))
+                if os.environ.get("SSA_POOL_FORK", "0") == "1" and torch.cuda.is_available():
+                    # the pooling branch (GAP partials + per-image MLP: 32 + 32 small
+                    # workgroups, ~26 us of latency at B = 32) on a side stream forked before
+                    # the grouped branch GEMM and joined before the head: its few waves fit
+                    # beside the GEMM's 16 per CU instead of running after it (event fork /
+                    # join, captured into the hipGraph like the rest of the plan)
+                    side = torch.cuda.Stream(dev)
+                    ev_f, ev_j = torch.cuda.Event(), torch.cuda.Event()
+                    self._side_streams.append(side)
+
+                    def fork_op(*args, side=side, ev_f=ev_f, ev_j=ev_j, pool_op=pool_op):
+                        ev_f.record(torch.cuda.current_stream())
+                        side.wait_event(ev_f)
+                        with torch.cuda.stream(side):
+                            pool_op(*args)
+                        ev_j.record(side)
+
+                    ops.insert(aspp_at, fork_op)
+                    ops.append(lambda *_, ev_j=ev_j: torch.cuda.current_stream().wait_event(ev_j))
+                else:
+                    ops.append(pool_op)
             else:
                 gap = buf("gap", B, c, dtype=torch.float32)
                 pooled = buf("pooled", B, A, dtype=torch.float32)
