@@ -57,13 +57,16 @@ def main() -> int:
     p.add_argument("--camera", default="640x480")
     p.add_argument("--ingest", choices=["local", "scatter"], default="local")
     p.add_argument("--gather", choices=["auto", "host", "rccl"], default="auto",
-                   help="record gather to rank 0: auto = RCCL over xGMI when N > 1 (the "
-                        "multi-GPU data path), else none needed; host = pinned host + gloo")
+                   help="record gather to rank 0: auto = host (each rank's records are "
+                        "written to pinned memory by a kernel and gathered over gloo: no GPU "
+                        "time); rccl = RCCL gather over xGMI on the result stream")
     p.add_argument("--pg", choices=["auto", "nccl", "gloo"], default="auto",
-                   help="process-group backend; auto: RCCL (+ a gloo control group) when "
-                        "N > 1 on GPUs or an RCCL data path is requested, else gloo. Measured on "
-                        "one MI355X (world-size-1 groups, profiles/r2_pg_ab.txt): RCCL + RCCL "
-                        "gather 24.07k vs gloo + host gather 24.42k frames/s, equal within noise")
+                   help="process-group backend; auto: RCCL (+ a gloo control group) when an "
+                        "RCCL data path is requested (--ingest scatter, --gather rccl), else "
+                        "gloo. Measured on one MI355X with world-size-1 groups "
+                        "(profiles/r4_rccl_gather_ab.txt): gloo + host gather 33.8-33.9k, "
+                        "RCCL group + host gather 32.0k, RCCL group + RCCL gather 30.2-30.6k "
+                        "frames/s")
     p.add_argument("--contour_mode", choices=["fast", "exact", "none"], default="fast")
     p.add_argument("--no-graph", dest="graph", action="store_false")
     p.add_argument("--rpc", type=int, default=2000, help="GetSegmentedObjects calls to time (0: skip)")
@@ -101,8 +104,7 @@ def main() -> int:
     # device, so the auto choice is the gloo group with the host-memory gather
     share = os.environ.get("SSA_SHARE_GPU", "0") == "1"
     pg = a.pg if a.pg != "auto" else (
-        "nccl" if gpu and not share and (a.ingest == "scatter" or a.gather == "rccl" or
-                                         (a.gather == "auto" and world > 1)) else "gloo")
+        "nccl" if gpu and not share and (a.ingest == "scatter" or a.gather == "rccl") else "gloo")
     ctx = D.init(pg, device="cuda" if _t.cuda.is_available() and a.backend != "cpu" else "auto")
     cam_w, cam_h = (int(v) for v in a.camera.split("x"))
     cfg = C.Config(arch=a.arch, aspp=a.aspp, input_size=a.input_size, backend=a.backend,
@@ -164,12 +166,19 @@ def main() -> int:
     sync()
     rec0, fr0 = pipe.records_out, pipe.frames_done
     pipe.reset_observations()
+    w0, g0 = pipe.wait_s, pipe.gather_s
     t0 = time.perf_counter()
     run_steps(a.steps, a.warmup)
+    t_host = time.perf_counter() - t0  # the host's step loop (the final sync excluded)
     sync()
     D.barrier(ctx)
     sync()
     dt = time.perf_counter() - t0
+    # where rank 0's host thread spent the step loop: blocked on step-completion events,
+    # in the host (gloo) record gather, or busy (launches, unpack, hub push)
+    w_ms, g_ms = (pipe.wait_s - w0) / a.steps * 1e3, (pipe.gather_s - g0) / a.steps * 1e3
+    host_ms = {"busy": round(t_host / a.steps * 1e3 - w_ms - g_ms, 4), "event_wait": round(w_ms, 4),
+               "host_gather": round(g_ms, 4)}
     dt = D.allreduce_max(ctx, dt)
 
     frames_total = a.steps * a.batch * ctx.world
@@ -237,6 +246,7 @@ def main() -> int:
             "records_per_frame_under_rpc_load": (round(rpc["records"] / max(1, rpc["frames"]), 4)
                                                  if rpc and "records" in rpc else None),
             "warmup_s": round(warm_s, 2),
+            "host_ms_per_step": host_ms,
         }
         print(json.dumps(out), flush=True)
     D.destroy(ctx)

@@ -387,6 +387,10 @@ PYBIND11_MODULE(_hip, m) {
   m.def("copy_to_host", [](uintptr_t src, uintptr_t dst, long long nbytes, uintptr_t stream) {
     copy_to_host(P<const void>(src), P<void>(dst), nbytes, S(stream));
   });
+  m.def("pack_rows", [](uintptr_t dst, uintptr_t a, int aw, uintptr_t b, int bw, int rows,
+                        uintptr_t stream) {
+    pack_rows(P<void>(dst), P<const void>(a), aw, P<const void>(b), bw, rows, S(stream));
+  });
   m.def("poison_lds", [](uint32_t pat, int blocks, uintptr_t stream) {
     poison_lds(pat, blocks, S(stream));
   });

@@ -302,6 +302,10 @@ size_t post_workspace_bytes(int B, int H, int W, int K, int num_bins);
 
 // device buffer -> pinned (hipHostMalloc) host buffer by a kernel on stream s (no host block)
 void copy_to_host(const void* src, void* dst, long long nbytes, hipStream_t s);
+// dst[r] = [a[r] | b[r]] over `rows` rows of a_words / b_words 4-byte words (a, b: device or
+// pinned host memory).
+void pack_rows(void* dst, const void* a, int a_words, const void* b, int b_words, int rows,
+               hipStream_t s);
 
 // Debug only (debug_poison.hip): NaN-pattern fill of every CU's LDS / every SIMD's
 // VGPR+AGPR file, to expose kernels that read on-chip state they did not write.

@@ -477,6 +477,34 @@ void copy_to_host(const void* src, void* dst, long long nbytes, hipStream_t s) {
   check_launch("copy_to_host");
 }
 
+// dst row r = [a row r | b row r] (4-byte words). a/b may be device or pinned host memory:
+// the records + frame metadata of one step become ONE send buffer, so the RCCL gather to
+// rank 0 is a single collective and the metadata needs no H2D hipMemcpyAsync of its own.
+__global__ __launch_bounds__(256) void pack_rows_kernel(uint32_t* __restrict__ dst,
+                                                        const uint32_t* __restrict__ a, int aw,
+                                                        const uint32_t* __restrict__ b, int bw,
+                                                        int rows) {
+  const int w = aw + bw;
+  const long long n = (long long)rows * w;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / w;
+    const int c = (int)(i - r * w);
+    dst[i] = c < aw ? a[r * aw + c] : b[r * bw + (c - aw)];
+  }
+}
+
+void pack_rows(void* dst, const void* a, int a_words, const void* b, int b_words, int rows,
+               hipStream_t s) {
+  if (rows <= 0 || a_words < 0 || b_words < 0) throw std::invalid_argument("pack_rows: bad shape");
+  const long long n = (long long)rows * (a_words + b_words);
+  const int grid = (int)std::min<long long>(64, std::max<long long>(1, cdiv(n, 256)));
+  hipLaunchKernelGGL(pack_rows_kernel, dim3(grid), dim3(256), 0, s, static_cast<uint32_t*>(dst),
+                     static_cast<const uint32_t*>(a), a_words, static_cast<const uint32_t*>(b),
+                     b_words, rows);
+  check_launch("pack_rows");
+}
+
 void global_avgpool(const bf16* in, float* out, float* ws, int B, int HW, int C, hipStream_t s) {
   hipLaunchKernelGGL(gap_partial_kernel, dim3(B, kGapSlices, cdiv(C / 8, 64)), dim3(256), 0, s, in,
                      ws, HW, C);

@@ -18,7 +18,7 @@
 #   profb1       sequential kernel trace of the B=1 step -> b1_layer_times.txt
 #   pmc          3 SQ counter passes over the sequential B=32 step -> pmc_summary.txt
 #   race         concurrent-plan determinism check (scripts/debug_race.py)
-#   share8       the dp8 bench path with 8 ranks sharing this one GPU (SSA_SHARE_GPU=1, gloo;
+#   share8 / share:N  the dpN bench path with N ranks sharing this one GPU (SSA_SHARE_GPU=1, gloo;
 #                completes end to end -- its throughput is not a scaling number)
 #   postab       post-processing harness (tools/bin/post_bench), strips vs 32^2 / 64^2 tile accumulation
 #   posttrace    post_bench (4 map kinds incl. the fallback-path lattice) under a kernel trace
@@ -87,10 +87,11 @@ for step in "$@"; do
              done
              python3 scripts/pmc_summary.py $O/pmc1 $O/pmc2 $O/pmc3 > $O/pmc_summary.txt 2>&1; head -60 $O/pmc_summary.txt ;;
     race)    timeout -k 10 600 python scripts/debug_race.py $RACE_ARGS > $O/race.txt 2>&1 || { tail -20 $O/race.txt; exit 5; }; tail -5 $O/race.txt ;;
-    share8)  SSA_SHARE_GPU=1 timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
-               --master-addr 127.0.0.1 --master-port 29581 bench.py --gpus 8 --steps 10 --warmup 3 --rpc 300 \
-               > $O/share8.json 2> $O/share8.err || { grep -v "^\[Gloo\]" $O/share8.err | tail -30; exit 5; }
-             cut -c1-600 $O/share8.json ;;
+    share8|share:*) n=${step#share}; n=${n#:}
+             SSA_SHARE_GPU=1 timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
+               --master-addr 127.0.0.1 --master-port 29581 bench.py --gpus $n --steps 10 --warmup 3 --rpc 300 $BENCH_ARGS \
+               > $O/share$n.json 2> $O/share$n.err || { grep -v "^\[Gloo\]" $O/share$n.err | tail -30; exit 5; }
+             cut -c1-600 $O/share$n.json ;;
     postab)  for m in 0 1 2; do SSA_POST_ACCUM=$m timeout -k 10 120 tools/bin/post_bench 50 > $O/post_accum$m.txt 2>&1 \
                || { tail -5 $O/post_accum$m.txt; exit 7; }; echo "accum=$m"; cat $O/post_accum$m.txt; done ;;
     posttrace) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats \

@@ -1,6 +1,6 @@
 """World-size-1 rehearsal of the multi-GPU data path on one GPU:
 a real RCCL process group (SSA_FORCE_PG=1, backend nccl) with the gloo control group,
-the DP pipeline in its default gather mode (auto -> RCCL record + metadata gather to
+the DP pipeline with the RCCL record gather (one [records | metadata] collective to
 rank 0, then the pinned-host write kernel), lag 2 on slot-parallel plan copies; the
 records must equal an eager synchronous engine's on the same frames. ``scatter`` as the
 first argument: rank 0 uploads the node batch and RCCL-scatters it on the slot streams
@@ -39,7 +39,7 @@ for k in range(6):
 torch.cuda.synchronize()
 hub = ResultHub(1)
 ingest = sys.argv[1] if len(sys.argv) > 1 else "local"
-pipe = DataParallelPipeline(ctx, eng, 160, 120, 2, ingest, hub, lag=1)  # auto: lag 2, RCCL gather
+pipe = DataParallelPipeline(ctx, eng, 160, 120, 2, ingest, hub, lag=1, gather="rccl")  # auto: lag 2
 assert pipe.lag == 2 and eng.slot_parallel, (pipe.lag, eng.slot_parallel)
 got = []
 pipe.prefetch(batches[0].pin_memory())

@@ -60,8 +60,8 @@ class Config:
     # --- distributed ---
     gpus: int = 1
     ingest: str = "local"                  # local (per-rank H2D) | scatter (rank-0 RCCL scatter)
-    gather: str = "auto"                   # record gather to rank 0: auto (RCCL when the group
-                                           # is RCCL) | rccl | host (pinned host + gloo)
+    gather: str = "auto"                   # record gather to rank 0: auto (= host) | host
+                                           # (pinned host + gloo) | rccl (RCCL over xGMI)
     # --- observability ---
     profile: bool = False
     metrics_dump: Optional[str] = None
@@ -131,8 +131,8 @@ def add_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--gpus", type=int, default=d.gpus)
     p.add_argument("--ingest", choices=["local", "scatter"], default=d.ingest)
     p.add_argument("--gather", choices=["auto", "rccl", "host"], default=d.gather,
-                   help="per-step record gather to rank 0: RCCL over xGMI (auto at --gpus > 1) "
-                        "or pinned host memory over gloo")
+                   help="per-step record gather to rank 0: pinned host memory over gloo "
+                        "(auto; no GPU time) or RCCL over xGMI (rccl)")
     p.add_argument("--profile", action="store_true")
     p.add_argument("--metrics_dump", default=d.metrics_dump)
     p.add_argument("--log_level", default=d.log_level)

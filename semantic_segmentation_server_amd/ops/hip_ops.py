@@ -987,3 +987,22 @@ def copy_to_host(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
         raise ValueError("copy_to_host: byte sizes differ")
     _hip_mod().copy_to_host(src.data_ptr(), dst.data_ptr(), nb, _stream())
     return dst
+
+
+def pack_rows(dst: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """dst[r] = [a[r] | b[r]] by one kernel on the current stream. dst: contiguous CUDA
+    (rows, wa + wb) 4-byte tensor; a, b: contiguous (rows, w) 4-byte tensors on the device
+    or in PINNED host memory (the kernel reads those over the bus: no H2D memcpy)."""
+    if not dst.is_cuda:
+        raise ValueError("pack_rows: CUDA destination")
+    for t in (dst, a, b):
+        if t.dim() != 2 or t.element_size() != 4 or not t.is_contiguous():
+            raise ValueError("pack_rows: contiguous 2-D tensors of 4-byte elements required")
+        if not (t.is_cuda or t.is_pinned()):
+            raise ValueError("pack_rows: sources must be device or pinned host memory")
+    rows = dst.shape[0]
+    if a.shape[0] != rows or b.shape[0] != rows or dst.shape[1] != a.shape[1] + b.shape[1]:
+        raise ValueError(f"pack_rows: shapes {tuple(dst.shape)} != [{tuple(a.shape)} | {tuple(b.shape)}]")
+    _hip_mod().pack_rows(dst.data_ptr(), a.data_ptr(), a.shape[1], b.data_ptr(), b.shape[1], rows,
+                         _stream())
+    return dst

@@ -93,22 +93,24 @@ class DataParallelPipeline:
         records (synchronous).
 
         ``gather``: how the per-rank records reach rank 0.
-          * ``rccl`` (the default with an RCCL group, i.e. every multi-GPU run): RCCL
-            gather of the device records to rank 0's GPU on the stream that produced
-            them, then one D2H there (the X2 collective of SURVEY.md §2.5). The
-            frame metadata (ids, streams, capture times) travels the same way. The
-            communicator is created lazily by the first gather, after the engine's
-            streams exist (eager creation shifted the engine's streams onto a worse
-            hardware-queue mapping: 17.6k vs 21.4k frames/s at world size 1).
-          * ``host``: every rank copies its packed records (B x 1.3 KB) to pinned host
-            memory on the stream that produced them, and the host buffers are
-            gathered over the gloo group when the step is collected (the fallback,
-            and the CPU/gloo test path). At world size 1 the two measured equal
-            within noise (profiles/r2_pg_ab.txt: RCCL group + RCCL gather 24.07k,
-            gloo + host gather 24.42k frames/s).
-          * ``auto``: ``rccl`` when the process group is RCCL, else ``host``."""
+          * ``host`` (the default, ``auto``): every rank writes its packed records
+            (B x 1.3 KB) to pinned host memory with a kernel on the stream that produced
+            them, and the host buffers are gathered over the gloo group when the step is
+            collected. The message is tiny and latency-bound; this way it costs no GPU
+            time and ~0.3 ms of a host thread that is otherwise idle ~80 % of the step
+            (bench.py host_ms_per_step: busy 0.15-0.20 ms of a 0.95 ms step;
+            tests/test_distributed.py::test_gloo_record_gather_cost_world8).
+          * ``rccl``: RCCL gather of [records | metadata] rows (one send buffer, one
+            collective) to rank 0's GPU on the result stream, then one D2H there (the X2
+            collective of SURVEY.md §2.5). The communicator is created lazily by the first
+            gather, after the engine's streams exist (eager creation shifted the engine's
+            streams onto a worse hardware-queue mapping: 17.6k vs 21.4k frames/s at world
+            size 1). Measured at world size 1 it costs GPU time the host path does not:
+            30.2-30.6k vs 33.8-33.9k frames/s (profiles/r4_rccl_gather_ab.txt), so it is
+            opt-in; RCCL carries the frame scatter (``ingest="scatter"``), where the
+            payload (B x 921.6 KB per peer) belongs on xGMI."""
         if gather == "auto":
-            gather = "rccl" if (ctx.backend == "nccl" and engine.device.type == "cuda") else "host"
+            gather = "host"
         if gather not in ("host", "rccl"):
             raise ValueError("gather must be 'auto', 'host' or 'rccl'")
         self.ctx = ctx
@@ -151,11 +153,18 @@ class DataParallelPipeline:
         self.K = int(engine.cfg.max_segments)
         self.rec_width = 1 + 5 * self.K
         cdev = dev if ctx.backend == "nccl" else "cpu"
-        if ctx.is_root and ctx.initialized:
-            self.gather_buf = torch.empty((ctx.world, self.B, self.rec_width), dtype=torch.float32,
-                                          device=cdev)
-            self.meta_buf = torch.empty((ctx.world, self.B, 3), dtype=torch.float64, device=cdev)
-        self.meta = torch.zeros((self.B, 3), dtype=torch.float64, device=cdev)
+        # RCCL gather: one send row per frame = [packed record | float64 (id, stream, ts) as
+        # 6 words], so each step is ONE collective and ONE D2H on rank 0 (the metadata used
+        # to take an H2D memcpy and a second gather of its own: 30.1k vs 33.8k frames/s at
+        # world size 1 with the RCCL group, profiles/r4_rccl_gather_ab.txt)
+        self.comb_width = self.rec_width + 6
+        if gather == "rccl" and ctx.initialized:
+            self.send_buf = torch.empty((self.B, self.comb_width), dtype=torch.float32, device=cdev)
+            if ctx.is_root:
+                self.gather_buf = torch.empty((ctx.world, self.B, self.comb_width),
+                                              dtype=torch.float32, device=cdev)
+                self.host_all = [torch.empty((ctx.world, self.B, self.comb_width), dtype=torch.float32,
+                                             pin_memory=self.cuda) for _ in range(NS)]
         # host-side buffers are double-buffered: with lag=1 step k+1 refills them
         # while step k's async copies may still be queued behind its compute
         self.meta_host = [torch.zeros((self.B, 3), dtype=torch.float64, pin_memory=self.cuda)
@@ -167,9 +176,6 @@ class DataParallelPipeline:
                                       pin_memory=self.cuda) for _ in range(NS)]
         self.local_meta = [torch.empty((self.B, 3), dtype=torch.float64) for _ in range(NS)]
         self.host_meta_all = torch.empty((ctx.world, self.B, 3), dtype=torch.float64)
-        if ctx.is_root and ctx.initialized:
-            self.host_meta = [torch.empty((ctx.world, self.B, 3), dtype=torch.float64,
-                                          pin_memory=self.cuda) for _ in range(NS)]
         self._rslot = 0
         self._pending = []  # (slot, event, fids, streams, ts) of the steps not yet collected
         self.frames_done = 0
@@ -186,6 +192,10 @@ class DataParallelPipeline:
         self.stream_frames = {}
         self.stream_last_id = {}
         self.frame_order_errors = 0
+        # host time blocked on step-completion events / in the host (gloo) record gather:
+        # the rest of a step's wall time is the host's own work (bench.py reports both)
+        self.wait_s = 0.0
+        self.gather_s = 0.0
         self.rank_timeout_s = float(os.environ.get("SSA_RANK_TIMEOUT", "300"))
         hm = getattr(engine, "_hip_model", None)
         if hm is not None and hasattr(hm, "pick_sync") and ctx.world > 1 and ctx.initialized:
@@ -361,23 +371,16 @@ class DataParallelPipeline:
         with (torch.cuda.stream(rs) if rs is not None else contextlib.nullcontext()):
             if self.ctx.initialized:
                 mh = self.meta_host[slot]
-                mh[:, 0] = torch.tensor(fids, dtype=torch.float64)
-                mh[:, 1] = torch.tensor(strm, dtype=torch.float64)
-                mh[:, 2] = torch.tensor(tss, dtype=torch.float64)
-                self.meta.copy_(mh, non_blocking=True)
-                send = packed if self.ctx.backend == "nccl" else packed.cpu()
+                mh.copy_(torch.tensor([fids, strm, tss], dtype=torch.float64).t())
+                self._pack_send(packed, mh)
                 dst = list(self.gather_buf.unbind(0)) if self.ctx.is_root else None
-                dist.gather(send, dst, dst=0)
-                mdst = list(self.meta_buf.unbind(0)) if self.ctx.is_root else None
-                dist.gather(self.meta, mdst, dst=0)
-                src = self.gather_buf if self.ctx.is_root else None
+                dist.gather(self.send_buf, dst, dst=0)
+                src, hdst = (self.gather_buf, self.host_all[slot]) if self.ctx.is_root else (None, None)
             else:
-                src = packed.unsqueeze(0)
+                src, hdst = packed.unsqueeze(0), self.host_rec[slot]
             self.frames_done += B * self.ctx.world
             if self.ctx.is_root:
-                self._d2h(src, self.host_rec[slot])
-                if self.ctx.initialized:
-                    self._d2h(self.meta_buf, self.host_meta[slot])
+                self._d2h(src, hdst)
             # every rank (non-root ones too) records the step and goes through the lag
             # throttle: meta_host[slot] is rewritten only after the step that last used it
             # has been collected, i.e. after its H2D copy ran (VERDICT r3 Weak #4: non-root
@@ -387,6 +390,21 @@ class DataParallelPipeline:
                 ev = torch.cuda.Event()
                 ev.record(torch.cuda.current_stream(self.dev))
         return self._enqueue((slot, ev, fids, strm, tss))
+
+    def _pack_send(self, packed: torch.Tensor, meta_host: torch.Tensor) -> None:
+        """send_buf = [packed records | metadata words] on the current stream. HIP build:
+        one kernel that reads the pinned metadata over the bus (no H2D hipMemcpyAsync);
+        otherwise plain copies (the gloo/CPU test path)."""
+        rw = self.rec_width
+        mw = meta_host.view(torch.float32)
+        sb = self.send_buf
+        if sb.is_cuda and packed.is_cuda and packed.is_contiguous() and mw.is_pinned() \
+                and getattr(self.engine, "backend", "hip") == "hip":
+            from ..ops import hip_ops
+            hip_ops.pack_rows(sb, packed, mw)
+            return
+        sb[:, :rw].copy_(packed, non_blocking=self.cuda)
+        sb[:, rw:].copy_(mw, non_blocking=self.cuda)
 
     def _d2h(self, src: torch.Tensor, dst: torch.Tensor) -> None:
         """Device records -> pinned host buffer on the current stream. On the HIP build a
@@ -460,7 +478,9 @@ class DataParallelPipeline:
 
     def _collect_inner(self, pending) -> np.ndarray:
         slot, ev, fids, strm, tss = pending
+        t0 = time.perf_counter()
         self._wait_step(ev)
+        self.wait_s += time.perf_counter() - t0
         if self.gather_mode == "host":
             lm = self.local_meta[slot]
             lm[:, 0] = torch.tensor(fids, dtype=torch.float64)
@@ -469,9 +489,11 @@ class DataParallelPipeline:
             if self.ctx.initialized:  # every rank collects the same step: lockstep gathers
                 grp = self.ctx.cpu_group
                 root = self.ctx.is_root
+                t0 = time.perf_counter()
                 dist.gather(self.local_rec[slot], list(self.host_rec[slot].unbind(0)) if root else None,
                             dst=0, group=grp)
                 dist.gather(lm, list(self.host_meta_all.unbind(0)) if root else None, dst=0, group=grp)
+                self.gather_s += time.perf_counter() - t0
                 if not root:
                     return np.zeros(0, RECORD_DTYPE)
                 meta = self.host_meta_all.numpy().reshape(-1, 3)
@@ -489,11 +511,13 @@ class DataParallelPipeline:
         if not self.ctx.is_root:
             return np.zeros(0, RECORD_DTYPE)
         if self.ctx.initialized:
-            meta = self.host_meta[slot].numpy().reshape(-1, 3)
+            allw = self.host_all[slot].numpy().reshape(-1, self.comb_width)
+            flat = np.ascontiguousarray(allw[:, :self.rec_width])
+            meta = allw[:, self.rec_width:].copy().view(np.float64)
         else:
             meta = np.stack([np.asarray(fids, np.float64), np.asarray(strm, np.float64),
                              np.asarray(tss, np.float64)], 1)
-        flat = self.host_rec[slot].numpy().reshape(-1, self.rec_width)
+            flat = self.host_rec[slot].numpy().reshape(-1, self.rec_width)
         recs = unpack_records(flat, self.K, meta[:, 0].astype(np.int64), meta[:, 2],
                               meta[:, 1].astype(np.int64))
         self.records_out += len(recs)

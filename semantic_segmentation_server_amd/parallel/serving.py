@@ -66,12 +66,11 @@ class DistributedServer:
         # the group is re-formed; --no_degrade (or --gather rccl) keeps the
         # RCCL data path, which bench.py measures. The pipeline's completion wait polls
         # for a peer's abort key on that path, so a lost peer still surfaces as PeerLost.
-        self.gather = cfg.gather
-        if self.gather == "auto" and cfg.degrade:
-            self.gather = "host"
+        # (auto = host at any world size: the RCCL gather costs GPU time, see dp.py)
+        self.gather = "host" if cfg.gather == "auto" else cfg.gather
         # SSA_SHARE_GPU=1 (several ranks on one GPU, a rehearsal): RCCL refuses that, gloo
         share = os.environ.get("SSA_SHARE_GPU", "0") == "1"
-        pg = "nccl" if gpu and not share and (cfg.ingest == "scatter" or self.gather in ("auto", "rccl")) else "gloo"
+        pg = "nccl" if gpu and not share and (cfg.ingest == "scatter" or self.gather == "rccl") else "gloo"
         self.ctx = ctx or D.init(pg, timeout_s=cfg.rank_timeout,
                                  device="cuda" if torch.cuda.is_available() and cfg.device != "cpu"
                                  else "auto")

@@ -370,6 +370,28 @@ def test_maxpool_gap_matvec():
     assert torch.allclose(mv.cpu(), F.relu(gref @ wm.t() + bm), atol=1e-3)
 
 
+@pytest.mark.parametrize("rows,aw", [(32, 41), (1, 41), (7, 3)])
+def test_pack_rows_and_copy_to_host(rows, aw):
+    """The RCCL-gather send row [record | metadata] packed from a device tensor and a
+    PINNED host tensor (read by the kernel over the bus), then copied back to pinned
+    memory by copy_to_host: equal to the torch concatenation, bit for bit."""
+    from semantic_segmentation_server_amd.ops import hip_ops
+    g = torch.Generator().manual_seed(rows)
+    a = torch.randn(rows, aw, generator=g)
+    meta = torch.rand(rows, 3, generator=g, dtype=torch.float64).pin_memory()
+    dst = torch.full((rows, aw + 6), float("nan"), device=DEV)
+    hip_ops.pack_rows(dst, a.to(DEV), meta.view(torch.float32))
+    host = torch.empty(rows, aw + 6).pin_memory()
+    hip_ops.copy_to_host(dst, host)
+    torch.cuda.synchronize()
+    ref = torch.cat([a, meta.view(torch.float32)], 1)
+    assert torch.equal(dst.cpu().view(torch.int32), ref.view(torch.int32))
+    assert torch.equal(host.view(torch.int32), ref.view(torch.int32))
+    assert torch.equal(host[:, aw:].reshape(-1).clone().view(torch.float64).view(rows, 3), meta)
+    with pytest.raises(ValueError):
+        hip_ops.pack_rows(dst, a.to(DEV), meta.view(torch.float32)[:, :5].contiguous())
+
+
 @pytest.mark.parametrize("B,h,w,C,N", [(3, 33, 33, 320, 256), (2, 17, 13, 2048, 256), (1, 9, 7, 40, 24)])
 def test_aspp_pool(B, h, w, C, N):
     """GAP + relu(W1 gap + b1) + W2 pooled in two launches vs an fp32 torch reference
@@ -706,7 +728,7 @@ def test_engine_bound_input_graphs(split):
 
 @pytest.mark.parametrize("ingest", ["local", "scatter"])
 def test_rccl_world1_pipeline_records_match_eager(ingest):
-    """The multi-GPU default data path (RCCL process group + gloo control group, RCCL
+    """The RCCL data path (RCCL process group + gloo control group, RCCL
     record gather, lag 2 slot-parallel; with ``scatter`` also the RCCL frame scatter on
     the slot streams) rehearsed at world size 1 on this GPU (SSA_FORCE_PG=1): records
     equal the eager engine's (scripts/rccl_world1_check.py, in a child process so its
