@@ -175,7 +175,9 @@ class DataParallelPipeline:
         self.local_rec = [torch.empty((self.B, self.rec_width), dtype=torch.float32,
                                       pin_memory=self.cuda) for _ in range(NS)]
         self.local_meta = [torch.empty((self.B, 3), dtype=torch.float64) for _ in range(NS)]
-        self.host_meta_all = torch.empty((ctx.world, self.B, 3), dtype=torch.float64)
+        if gather == "host" and ctx.initialized:
+            self.host_send = torch.empty((self.B, self.comb_width), dtype=torch.float32)
+            self.host_gather = torch.empty((ctx.world, self.B, self.comb_width), dtype=torch.float32)
         self._rslot = 0
         self._pending = []  # (slot, event, fids, streams, ts) of the steps not yet collected
         self.frames_done = 0
@@ -489,15 +491,20 @@ class DataParallelPipeline:
             if self.ctx.initialized:  # every rank collects the same step: lockstep gathers
                 grp = self.ctx.cpu_group
                 root = self.ctx.is_root
+                # records and metadata as ONE gloo message per rank ([record | 6 metadata
+                # words] rows): one collective's latency per step instead of two
+                rw = self.rec_width
+                send = self.host_send
+                send[:, :rw].copy_(self.local_rec[slot])
+                send[:, rw:].copy_(lm.view(torch.float32))
                 t0 = time.perf_counter()
-                dist.gather(self.local_rec[slot], list(self.host_rec[slot].unbind(0)) if root else None,
-                            dst=0, group=grp)
-                dist.gather(lm, list(self.host_meta_all.unbind(0)) if root else None, dst=0, group=grp)
+                dist.gather(send, list(self.host_gather.unbind(0)) if root else None, dst=0, group=grp)
                 self.gather_s += time.perf_counter() - t0
                 if not root:
                     return np.zeros(0, RECORD_DTYPE)
-                meta = self.host_meta_all.numpy().reshape(-1, 3)
-                flat = self.host_rec[slot].numpy().reshape(-1, self.rec_width)
+                allw = self.host_gather.numpy().reshape(-1, self.comb_width)
+                flat = np.ascontiguousarray(allw[:, :rw])
+                meta = allw[:, rw:].copy().view(np.float64)
             else:
                 meta = lm.numpy()
                 flat = self.local_rec[slot].numpy()
