@@ -58,8 +58,8 @@ def init(backend: Optional[str] = None, timeout_s: float = 300.0,
     GPU whatever the backend: a gloo group driving GPU ranks) or "cpu".
     ``backend`` (or env SSA_PG_BACKEND): "nccl" (RCCL) or "gloo". With RCCL a gloo
     ``cpu_group`` is created beside it for host-side control traffic (heartbeat, pick
-    broadcast, metadata); the per-step data (record gather, frame scatter) goes over
-    RCCL (DataParallelPipeline)."""
+    broadcast, metadata, the default host record gather); the frame scatter and the
+    opt-in device record gather go over RCCL (DataParallelPipeline)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
