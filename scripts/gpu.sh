@@ -16,6 +16,7 @@
 #   cfg5         4 camera streams x 8 frames (batched step)
 #   prof         sequential kernel trace of the B=32 step -> layer_times.txt
 #   profb1       sequential kernel trace of the B=1 step -> b1_layer_times.txt
+#   profc4       config-4 (ResNet-50 1025^2 int8, B=8) kernel trace -> c4_roofline.txt
 #   pmc          3 SQ counter passes over the sequential B=32 step -> pmc_summary.txt
 #   race         concurrent-plan determinism check (scripts/debug_race.py)
 #   share8 / share:N  the dpN bench path with N ranks sharing this one GPU (SSA_SHARE_GPU=1, gloo;
@@ -78,6 +79,9 @@ for step in "$@"; do
     cfg5)    bench c5 300 --streams 4 --batch 32 --steps 100 --warmup 10 --rpc 0 || exit 2 ;;
     prof)    trace seq --steps 5 --warmup 2 || exit 3 ;;
     profb1)  trace b1seq --batch 1 --steps 20 --warmup 5 || exit 3 ;;
+    profc4)  trace c4seq --arch resnet50 --input_size 1025 --camera 2048x1024 --batch 8 --dtype int8 --steps 5 --warmup 2 || exit 3
+             python3 scripts/roofline_int8.py $(ls $O/c4seq/*/run_kernel_trace.csv 2>/dev/null || ls $O/c4seq/run_kernel_trace.csv) 8 \
+               > $O/c4_roofline.txt && head -3 $O/c4_roofline.txt && tail -3 $O/c4_roofline.txt ;;
     pmc)     i=0
              for set in "${PMC_SETS[@]}"; do
                i=$((i+1))
