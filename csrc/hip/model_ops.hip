@@ -333,10 +333,94 @@ __global__ __launch_bounds__(256) void stem_mfma_kernel(SMArgs a) {
   }
 }
 
+// Wave-per-channel-block variant (round 4, the 7x7 stem of config 4): wave w computes
+// output channels 16w .. 16w + 15 for EVERY pixel group of the tile, so it holds one
+// channel block's 13 weight fragments (26 VGPRs) instead of all four (104): the
+// all-blocks kernel above needs 180 VGPRs, i.e. 2 workgroups per CU, and spends its
+// time waiting on the gather with nothing else resident (328 us per 8 frames at 1025^2,
+// 2.4 % of the MFMA peak, profiles/r4_config4_roofline.txt). The price is 4x the LDS
+// reads of the input fragments (each wave reads every group's), which LDS absorbs; the
+// smaller per-wave state also lets a workgroup own bigger tiles (up to 32 x 32 pixels),
+// which cuts the gathered halo per output pixel.
+template <int KG>
+__global__ __launch_bounds__(256) void stem_mfma_ws_kernel(SMArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* IN = reinterpret_cast<bf16*>(smem);
+  const int IHT = (a.TY - 1) * a.stride + a.K, IWT = (a.TX - 1) * a.stride + a.K;
+  const int ntile = a.tiles_y * a.tiles_x;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = bid / ntile, t = bid % ntile;
+  const int oy0 = (t / a.tiles_x) * a.TY, ox0 = (t % a.tiles_x) * a.TX;
+  const int iy0 = oy0 * a.stride - a.K / 2, ix0 = ox0 * a.stride - a.K / 2;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int sub = __builtin_amdgcn_readfirstlane(tid >> 6);  // this wave's 16 channels
+  const int r16 = lane & 15, kq = lane >> 4;
+  const float inv_tx = 1.f / a.TX;
+  const uint8_t* fb = a.frames + (size_t)b * a.Hc * a.Wc * 3;
+  gather_letterbox_rgb0<6, 256>(IN, fb, a.lut_x, a.lut_y, a.Wc, a.H, a.W, iy0, ix0, IHT, IWT, tid);
+  s16x4m wf[KG];
+#pragma unroll
+  for (int m = 0; m < KG; ++m)
+    wf[m] = *reinterpret_cast<const s16x4m*>(a.w + (size_t)(sub * 16 + r16) * (KG * 16) + m * 16 + kq * 4);
+  const f32x4 bs = *reinterpret_cast<const f32x4*>(a.bias + sub * 16 + kq * 4);
+  int toff[KG];
+#pragma unroll
+  for (int m = 0; m < KG; ++m) {
+    const int tp = m * 4 + kq;
+    toff[m] = tp < a.K * a.K ? ((tp / a.K) * IWT + tp % a.K) * 4 : -1;
+  }
+  __syncthreads();
+  const s16x4m zs = {0, 0, 0, 0};
+  const int Cout = 64;
+  const int n = sub * 16 + kq * 4;
+  const int groups = (a.TY * a.TX + 15) / 16;
+#pragma unroll 2
+  for (int g = 0; g < groups; ++g) {
+    const int p = g * 16 + r16;
+    const int py = (int)(((float)p + 0.5f) * inv_tx), px = p - py * a.TX;
+    const int oy = oy0 + py, ox = ox0 + px;
+    const bool valid = p < a.TY * a.TX && oy < a.OH && ox < a.OW;
+    const int base = valid ? (py * a.stride * IWT + px * a.stride) * 4 : 0;
+    f32x4 acc = bs;
+#pragma unroll
+    for (int m = 0; m < KG; ++m) {
+      const s16x4m xf = toff[m] >= 0 ? *reinterpret_cast<const s16x4m*>(IN + base + toff[m]) : zs;
+      acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wf[m], xf, acc, 0, 0, 0);
+    }
+    if (!valid) continue;
+    const size_t pix = ((size_t)b * a.OH + oy) * a.OW + ox;
+    if (a.out_inv_scale > 0.f) {
+      char4 o;
+      o.x = (signed char)fminf(fmaxf(rintf(apply_act(acc[0], a.act) * a.out_inv_scale), -127.f), 127.f);
+      o.y = (signed char)fminf(fmaxf(rintf(apply_act(acc[1], a.act) * a.out_inv_scale), -127.f), 127.f);
+      o.z = (signed char)fminf(fmaxf(rintf(apply_act(acc[2], a.act) * a.out_inv_scale), -127.f), 127.f);
+      o.w = (signed char)fminf(fmaxf(rintf(apply_act(acc[3], a.act) * a.out_inv_scale), -127.f), 127.f);
+      *reinterpret_cast<char4*>(static_cast<int8_t*>(a.out) + pix * Cout + n) = o;
+    } else {
+      bf16x4 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = (bf16)apply_act(acc[q], a.act);
+      *reinterpret_cast<bf16x4*>(static_cast<bf16*>(a.out) + pix * Cout + n) = o;
+    }
+  }
+}
+
 void stem_mfma(const uint8_t* frames, const int32_t* lut_x, const int32_t* lut_y, const bf16* w,
                const float* bias, void* out, int B, int Hc, int Wc, int H, int W, int OH, int OW,
                int Cout, int K, int stride, int act, float out_inv_scale, int TY, int TX,
-               hipStream_t s) {
+               hipStream_t s, int mode) {
+  if (mode == 1) {  // wave per 16-channel block: 7x7 / 64-channel stem only
+    if (Cout != 64 || (K * K + 3) / 4 != 13) throw std::invalid_argument("stem_mfma ws: (Cout, K) must be (64, 7)");
+    if (TY < 1 || TX < 1 || TY * TX > 1024) throw std::invalid_argument("stem_mfma ws: bad tile");
+    const size_t lds = (size_t)((TY - 1) * stride + K) * ((TX - 1) * stride + K) * 8;
+    if (lds > 64 * 1024) throw std::invalid_argument("stem_mfma ws: tile too large");
+    SMArgs a{frames, lut_x, lut_y, w, bias, out, B, Hc, Wc, H, W, OH, OW, K, stride, act, TY, TX,
+             cdiv(OH, TY), cdiv(OW, TX), out_inv_scale};
+    hipLaunchKernelGGL((stem_mfma_ws_kernel<13>), dim3(B * a.tiles_y * a.tiles_x), dim3(256), lds, s, a);
+    check_launch("stem_mfma ws");
+    return;
+  }
+  if (mode != 0) throw std::invalid_argument("stem_mfma: mode must be 0 or 1");
   if (TY < 1 || TX < 1 || TY * TX > 256 || TX > 120) throw std::invalid_argument("stem_mfma: bad tile");
   const int IHT = (TY - 1) * stride + K, IWT = (TX - 1) * stride + K;
   const size_t lds = (size_t)IHT * IWT * 8;

@@ -107,13 +107,13 @@ for step in "$@"; do
                || { tail -5 $O/$b.txt; exit 7; }; cat $O/$b.txt; done ;;
     retune:*) [ -f $O/tune.json ] || cp assets/tune_mi355x.json $O/tune.json
              SSA_TUNE_FILE=$O/tune.json SSA_RETUNE_ONLY=${step#retune:} SSA_LOG_AUTOTUNE=1 \
-               timeout -k 10 600 python bench.py --batch ${TUNE_B:-32} --steps 5 --warmup 2 --rpc 0 \
+               timeout -k 10 600 python bench.py --batch ${TUNE_B:-32} --steps 5 --warmup 2 --rpc 0 $BENCH_ARGS \
                > $O/retune_b${TUNE_B:-32}.json 2> $O/retune_b${TUNE_B:-32}.err || { tail -20 $O/retune_b${TUNE_B:-32}.err; exit 8; }
              grep "autotune" $O/retune_b${TUNE_B:-32}.err | grep -v "picks from" | cut -c1-1500 ;;
     retuneall:*) [ -f $O/tune.json ] || cp assets/tune_mi355x.json $O/tune.json
              b=${step#retuneall:}
              SSA_TUNE_FILE=$O/tune.json SSA_RETUNE=1 SSA_LOG_AUTOTUNE=1 \
-               timeout -k 10 600 python bench.py --batch $b --steps 5 --warmup 2 --rpc 0 \
+               timeout -k 10 600 python bench.py --batch $b --steps 5 --warmup 2 --rpc 0 $BENCH_ARGS \
                > $O/retuneall_b$b.json 2> $O/retuneall_b$b.err || { tail -20 $O/retuneall_b$b.err; exit 8; }
              grep "autotune" $O/retuneall_b$b.err | grep -v "picks from" | cut -c1-300 ;;
     py:*)    timeout -k 10 ${PY_TIMEOUT:-600} python -u ${step#py:} $PY_ARGS > $O/$(basename ${step#py:} .py).txt 2>&1 \

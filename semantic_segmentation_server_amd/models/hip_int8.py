@@ -123,6 +123,12 @@ class HipDeepLabInt8:
                     lambda frames, lx, ly, x=x, OH=OH, OW=OW, c=c, tile=tile, wpk=wpk: K.stem_mfma(
                         frames, lx, ly, wpk, self.stem_b, x, H=H, W=W, OH=OH, OW=OW, Cout=c, k=k,
                         stride=st, act="relu", out_scale=S["stem"], tile=tile)]))
+            if (c, k) == (64, 7):  # one wave per 16 output channels (26 weight VGPRs, not 104)
+                for tile in ((16, 16), (16, 32), (32, 32)):
+                    stem_variants.append((f"mfmaw{tile[0]}x{tile[1]}", [
+                        lambda frames, lx, ly, x=x, OH=OH, OW=OW, c=c, tile=tile, wpk=wpk: K.stem_mfma(
+                            frames, lx, ly, wpk, self.stem_b, x, H=H, W=W, OH=OH, OW=OW, Cout=c, k=k,
+                            stride=st, act="relu", out_scale=S["stem"], tile=tile, per_wave=True)]))
         ops.append(Choice("stem", stem_variants))
         PH, PW = conv_out_hw(OH, OW, 3, 2, 1)
         y = buf("pool0", B, PH, PW, c)
@@ -182,14 +188,15 @@ class HipDeepLabInt8:
         return self._plans[key]
 
     def _autotune(self, ops, B, Hc, Wc) -> None:
-        """Time each int8 conv's kernel variants on the plan's real buffers, keep the fastest."""
-        from .hip_model import Choice
+        """Time each int8 conv's kernel variants on the plan's real buffers, keep the fastest.
+        Inputs: synthetic camera frames through the real letterbox LUTs (HipDeepLab's); with
+        all-zero LUTs every stem gather hit one cached camera pixel and the stem variants
+        were timed on a degenerate path."""
+        from .hip_model import Choice, HipDeepLab
         if torch.cuda.is_current_stream_capturing():
             return
         dev = self.device
-        frames = torch.zeros((B, Hc, Wc, 3), dtype=torch.uint8, device=dev)
-        lx = torch.zeros(self.W, dtype=torch.int32, device=dev)
-        ly = torch.zeros(self.H, dtype=torch.int32, device=dev)
+        frames, lx, ly = HipDeepLab._tune_inputs(self, B, Hc, Wc)
         for op in ops:  # populate every buffer once
             op(frames, lx, ly)
         for op in ops:

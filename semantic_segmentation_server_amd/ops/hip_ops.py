@@ -738,14 +738,18 @@ def pack_stem_mfma(w: torch.Tensor, k: int, Cout: int) -> torch.Tensor:
 
 
 def stem_mfma(frames, lut_x, lut_y, wpk, bias, out, *, H, W, OH, OW, Cout, k, stride, act,
-              out_scale=None, tile=(8, 16)):
-    """stem_conv on MFMA (TY x TX output tiles); wpk from ``pack_stem_mfma``."""
+              out_scale=None, tile=(8, 16), per_wave=False):
+    """stem_conv on MFMA (TY x TX output tiles); wpk from ``pack_stem_mfma``.
+    ``per_wave``: one wave per 16 output channels over the whole tile (7x7 / 64 channels
+    only; tiles up to 1024 pixels)."""
     B, Hc, Wc, C3 = frames.shape
     if C3 != 3 or (Cout, k) not in ((64, 7), (32, 3)):
         raise ValueError("stem_mfma: (Cout, k) must be (64, 7) or (32, 3)")
+    if per_wave and (Cout, k) != (64, 7):
+        raise ValueError("stem_mfma per_wave: (Cout, k) must be (64, 7)")
     ty, tx = tile
-    if not (ty >= 1 and 1 <= tx <= 120 and ty * tx <= 256):
-        raise ValueError("stem_mfma: tile must hold <= 256 pixels")
+    if not (ty >= 1 and tx >= 1 and ty * tx <= (1024 if per_wave else 256) and (per_wave or tx <= 120)):
+        raise ValueError("stem_mfma: tile must hold <= 256 pixels (1024 per_wave)")
     if ((ty - 1) * stride + k) * ((tx - 1) * stride + k) * 8 > 64 * 1024:
         raise ValueError("stem_mfma: tile too large")
     _chk(frames, torch.uint8, "frames")
@@ -756,7 +760,7 @@ def stem_mfma(frames, lut_x, lut_y, wpk, bias, out, *, H, W, OH, OW, Cout, k, st
     _chk(out, torch.int8 if out_scale else torch.bfloat16, "out", B * OH * OW * Cout)
     _hip_mod().stem_mfma(_ptr(frames), _ptr(lut_x), _ptr(lut_y), _ptr(wpk), _ptr(bias), _ptr(out), B,
                          Hc, Wc, H, W, OH, OW, Cout, k, stride, ACT[act],
-                         1.0 / out_scale if out_scale else 0.0, ty, tx, _stream())
+                         1.0 / out_scale if out_scale else 0.0, ty, tx, _stream(), int(per_wave))
     _dbg('stem_mfma')
     return out
 

@@ -332,21 +332,26 @@ def test_stem_fused_preprocess(cam, k, cout):
     assert _rel(_nchw(out).cpu(), ref) < 1e-2
     # MFMA stem (bf16 operands): same conv, several tile shapes, bf16 and int8 outputs
     wpk = K.pack_stem_mfma(wk, k, cout)
-    for tile in ((8, 16), (16, 16), (3, 7)):
+    # (per_wave: one wave per 16 output channels, 7x7 / 64 channels only, tiles to 32 x 32)
+    tiles = [((8, 16), False), ((16, 16), False), ((3, 7), False)]
+    if (k, cout) == (7, 64):
+        tiles += [((16, 16), True), ((16, 32), True), ((32, 32), True), ((5, 9), True)]
+    for tile, pw in tiles:
         o2 = torch.full((2, OH, OW, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
         K.stem_mfma(frames.to(DEV), torch.tensor(lx, device=DEV), torch.tensor(ly, device=DEV), wpk,
                     b.to(DEV), o2, H=H, W=W, OH=OH, OW=OW, Cout=cout, k=k, stride=2, act="relu6",
-                    tile=tile)
+                    tile=tile, per_wave=pw)
         torch.cuda.synchronize()
         assert torch.isfinite(o2.float()).all()
         assert _rel(_nchw(o2).cpu(), ref) < 2e-2, tile
-    o8 = torch.empty(2, OH, OW, cout, dtype=torch.int8, device=DEV)
-    K.stem_mfma(frames.to(DEV), torch.tensor(lx, device=DEV), torch.tensor(ly, device=DEV), wpk,
-                b.to(DEV), o8, H=H, W=W, OH=OH, OW=OW, Cout=cout, k=k, stride=2, act="relu6",
-                out_scale=0.05)
-    torch.cuda.synchronize()
     exp = torch.clamp(torch.round(ref / 0.05), -127, 127)
-    assert (_nchw(o8).cpu().float() - exp).abs().float().mean() < 0.5
+    for tile, pw in [((8, 16), False)] + ([((32, 32), True)] if (k, cout) == (7, 64) else []):
+        o8 = torch.empty(2, OH, OW, cout, dtype=torch.int8, device=DEV)
+        K.stem_mfma(frames.to(DEV), torch.tensor(lx, device=DEV), torch.tensor(ly, device=DEV), wpk,
+                    b.to(DEV), o8, H=H, W=W, OH=OH, OW=OW, Cout=cout, k=k, stride=2, act="relu6",
+                    out_scale=0.05, tile=tile, per_wave=pw)
+        torch.cuda.synchronize()
+        assert (_nchw(o8).cpu().float() - exp).abs().float().mean() < 0.5, tile
 
 
 def test_maxpool_gap_matvec():
