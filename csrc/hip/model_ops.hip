@@ -363,14 +363,16 @@ __global__ __launch_bounds__(256) void stem_mfma_ws_kernel(SMArgs a) {
   for (int m = 0; m < KG; ++m)
     wf[m] = *reinterpret_cast<const s16x4m*>(a.w + (size_t)(sub * 16 + r16) * (KG * 16) + m * 16 + kq * 4);
   const f32x4 bs = *reinterpret_cast<const f32x4*>(a.bias + sub * 16 + kq * 4);
+  // taps past K*K (the last fragment's padding) read tap 0's pixel: their weights are
+  // zero, and an unconditional read lets all KG LDS reads issue before the MFMA chain (an
+  // exec-masked read per fragment serialised read -> wait -> MFMA 13 times per group)
   int toff[KG];
 #pragma unroll
   for (int m = 0; m < KG; ++m) {
     const int tp = m * 4 + kq;
-    toff[m] = tp < a.K * a.K ? ((tp / a.K) * IWT + tp % a.K) * 4 : -1;
+    toff[m] = tp < a.K * a.K ? ((tp / a.K) * IWT + tp % a.K) * 4 : 0;
   }
   __syncthreads();
-  const s16x4m zs = {0, 0, 0, 0};
   const int Cout = 64;
   const int n = sub * 16 + kq * 4;
   const int groups = (a.TY * a.TX + 15) / 16;
@@ -381,12 +383,12 @@ __global__ __launch_bounds__(256) void stem_mfma_ws_kernel(SMArgs a) {
     const int oy = oy0 + py, ox = ox0 + px;
     const bool valid = p < a.TY * a.TX && oy < a.OH && ox < a.OW;
     const int base = valid ? (py * a.stride * IWT + px * a.stride) * 4 : 0;
+    s16x4m xf[KG];
+#pragma unroll
+    for (int m = 0; m < KG; ++m) xf[m] = *reinterpret_cast<const s16x4m*>(IN + base + toff[m]);
     f32x4 acc = bs;
 #pragma unroll
-    for (int m = 0; m < KG; ++m) {
-      const s16x4m xf = toff[m] >= 0 ? *reinterpret_cast<const s16x4m*>(IN + base + toff[m]) : zs;
-      acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wf[m], xf, acc, 0, 0, 0);
-    }
+    for (int m = 0; m < KG; ++m) acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wf[m], xf[m], acc, 0, 0, 0);
     if (!valid) continue;
     const size_t pix = ((size_t)b * a.OH + oy) * a.OW + ox;
     if (a.out_inv_scale > 0.f) {
