@@ -171,19 +171,19 @@ __global__ __launch_bounds__(64 * NW) void stem_band_kernel(StemBandArgs a) {
   const bool sin_x = sj < NSC && sxg >= 0 && sxg < a.SW;
   const int sjc = sj < NSC ? sj : 0;
   int toff[3];  // this lane's tap (m*4 + kq) as an element offset: ring-row delta, column
-  int tky[3];
+  int tky[3];   // (taps 9-11 pad the last fragment: zero weights, they read tap 0's pixel, so
+                // the three fragment reads are unconditional and issue back to back)
 #pragma unroll
   for (int m = 0; m < 3; ++m) {
     const int tp = m * 4 + kq;
-    tky[m] = tp < 9 ? tp / 3 : -1;
-    toff[m] = tp < 9 ? (2 * sjc + tp % 3) * 4 : 0;
+    tky[m] = tp < 9 ? tp / 3 : 0;
+    toff[m] = (2 * sjc + (tp < 9 ? tp % 3 : 0)) * 4;
   }
   const int xl = g * 16 + r16;                // local output column (reads stem cols xl..xl+2)
   const bool xv = xl < twv;
   const int xc = xv ? xl : 0;
   const f16x4 z4 = {0, 0, 0, 0}, s4 = {6, 6, 6, 6};
   const f16x8 h0 = {0, 0, 0, 0, 0, 0, 0, 0}, h6 = {6, 6, 6, 6, 6, 6, 6, 6};
-  const s16x4 zs = {0, 0, 0, 0};
   f16x8 D[3];
 #pragma unroll
   for (int s_ = 0; s_ < 3; ++s_) D[s_] = bdv;
@@ -209,7 +209,7 @@ __global__ __launch_bounds__(64 * NW) void stem_band_kernel(StemBandArgs a) {
         s16x4 xf[3];
 #pragma unroll
         for (int m = 0; m < 3; ++m)
-          xf[m] = tky[m] >= 0 ? *reinterpret_cast<const s16x4*>(IN + (size_t)((2 * t + tky[m]) % 6) * in_row + toff[m]) : zs;
+          xf[m] = *reinterpret_cast<const s16x4*>(IN + (size_t)((2 * t + tky[m]) % 6) * in_row + toff[m]);
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub) {
           f32x4 e4 = bst[sub];
