@@ -466,17 +466,21 @@ class DataParallelPipeline:
         now = time.time()
         ts = meta[:, 2]
         lat = (now - ts[ts > 0]) * 1e3
-        for v in lat:
-            self.frame_latency.add(float(v))
+        self.frame_latency.add_many(lat)
         if self.metrics is not None:
-            for v in lat:
-                self.metrics.observe("frame_latency_ms", float(v))
-        for fid, st in zip(meta[:, 0].astype(np.int64).tolist(), meta[:, 1].astype(np.int64).tolist()):
+            self.metrics.observe_many("frame_latency_ms", lat)
+        # vectorised per source stream (host time per step matters: ~0.17 ms of a 0.95 ms
+        # step, bench.py host_ms_per_step): an id must exceed the previous one of its stream
+        fids = meta[:, 0].astype(np.int64)
+        sts = meta[:, 1].astype(np.int64)
+        for st in np.unique(sts).tolist():
+            seq = fids[sts == st]
             last = self.stream_last_id.get(st)
-            if last is not None and fid <= last:
-                self.frame_order_errors += 1
-            self.stream_last_id[st] = fid
-            self.stream_frames[st] = self.stream_frames.get(st, 0) + 1
+            prev = np.concatenate(([last], seq[:-1])) if last is not None else seq[:-1]
+            cur = seq if last is not None else seq[1:]
+            self.frame_order_errors += int((cur <= prev).sum())
+            self.stream_last_id[st] = int(seq[-1])
+            self.stream_frames[st] = self.stream_frames.get(st, 0) + len(seq)
 
     def _collect_inner(self, pending) -> np.ndarray:
         slot, ev, fids, strm, tss = pending

@@ -26,6 +26,16 @@ class Reservoir:
         self.buf[self.n % len(self.buf)] = v
         self.n += 1
 
+    def add_many(self, vs) -> None:
+        """add() of every value of ``vs``, in order (one numpy scatter, not a Python loop)."""
+        vs = np.asarray(vs, dtype=np.float64).ravel()
+        L = len(self.buf)
+        if len(vs) > L:  # only the last L can survive
+            self.n += len(vs) - L
+            vs = vs[-L:]
+        self.buf[(self.n + np.arange(len(vs))) % L] = vs
+        self.n += len(vs)
+
     def values(self) -> np.ndarray:
         return self.buf[: min(self.n, len(self.buf))]
 
@@ -55,6 +65,13 @@ class Metrics:
             if h is None:
                 h = self.hists[name] = Reservoir()
             h.add(v)
+
+    def observe_many(self, name: str, vs) -> None:
+        with self._lock:
+            h = self.hists.get(name)
+            if h is None:
+                h = self.hists[name] = Reservoir()
+            h.add_many(vs)
 
     def timer(self, name: str):
         return _Timer(self, name)

@@ -105,3 +105,32 @@ def test_debug_sync_sets_launch_blocking_and_disables_graphs(monkeypatch):
     cfg = C.apply_debug_env(C.parse(["--debug_sync"]))
     assert cfg.debug_sync and not cfg.graph
     assert os.environ["HIP_LAUNCH_BLOCKING"] == "1"
+
+
+def test_reservoir_add_many_and_frame_order_bookkeeping():
+    """The vectorised per-step bookkeeping (Reservoir.add_many, DataParallelPipeline._observe)
+    equals the per-sample loop it replaced: same ring contents, same frame-order verdicts."""
+    import numpy as np
+    from semantic_segmentation_server_amd.parallel.dp import DataParallelPipeline
+    from semantic_segmentation_server_amd.utils.metrics import Reservoir
+    vals = np.random.default_rng(0).random(29)
+    a, b = Reservoir(8), Reservoir(8)
+    for chunk in (vals[:3], vals[3:20], vals[20:]):
+        for v in chunk:
+            a.add(float(v))
+        b.add_many(chunk)
+        assert a.n == b.n and np.array_equal(a.buf, b.buf)
+
+    class P:  # the attributes _observe touches
+        frame_latency, metrics = Reservoir(64), None
+        stream_last_id, stream_frames, frame_order_errors = {}, {}, 0
+    p = P()
+    # stream 0 in order, stream 1 with one repeat and one step back
+    fids = [0, 10, 1, 11, 2, 11, 3, 9]
+    sts = [0, 1, 0, 1, 0, 1, 0, 1]
+    meta = np.stack([np.array(fids, np.float64), np.array(sts, np.float64), np.full(8, 1.0)], 1)
+    DataParallelPipeline._observe(p, meta[:4])
+    DataParallelPipeline._observe(p, meta[4:])
+    assert p.frame_order_errors == 2
+    assert p.stream_frames == {0: 4, 1: 4} and p.stream_last_id == {0: 3, 1: 9}
+    assert p.frame_latency.n == 8
