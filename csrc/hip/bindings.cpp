@@ -78,7 +78,7 @@ PYBIND11_MODULE(_hip, m) {
         [](uintptr_t in, uintptr_t we, uintptr_t be, uintptr_t wd, uintptr_t bd, uintptr_t wp,
            uintptr_t bp, uintptr_t out, int B, int IH, int IW, int Cin, int CinP, int hidP,
            int Cout, int OH, int OW, int stride, int residual, uintptr_t stream, int dil, int TY,
-           int TX, uintptr_t wd_h, uintptr_t bd_h, uintptr_t wp_h, uintptr_t trace, int persist) {
+           int TX, uintptr_t wd_h, uintptr_t bd_h, uintptr_t wp_h, uintptr_t trace) {
           FusedIRParams p;
           p.in = P<const bf16>(in); p.we = P<const bf16>(we); p.be = P<const float>(be);
           p.wd = P<const float>(wd); p.bd = P<const float>(bd); p.wp = P<const bf16>(wp);
@@ -88,35 +88,14 @@ PYBIND11_MODULE(_hip, m) {
           p.dil = dil; p.TY = TY; p.TX = TX;
           p.wd_h = P<const void>(wd_h); p.bd_h = P<const void>(bd_h); p.wp_h = P<const void>(wp_h);
           p.trace = P<long long>(trace);
-          p.nw = persist == 2 ? 8 : 4;
-          if (persist) fused_ir_persist(p, S(stream));
-          else fused_inverted_residual(p, S(stream));
+          fused_inverted_residual(p, S(stream));
         },
         py::arg("in"), py::arg("we"), py::arg("be"), py::arg("wd"), py::arg("bd"), py::arg("wp"),
         py::arg("bp"), py::arg("out"), py::arg("B"), py::arg("IH"), py::arg("IW"), py::arg("Cin"),
         py::arg("CinP"), py::arg("hidP"), py::arg("Cout"), py::arg("OH"), py::arg("OW"),
         py::arg("stride"), py::arg("residual"), py::arg("stream"), py::arg("dil") = 1,
         py::arg("TY") = 0, py::arg("TX") = 0, py::arg("wd_h") = 0, py::arg("bd_h") = 0,
-        py::arg("wp_h") = 0, py::arg("trace") = 0, py::arg("persist") = 0);
-  m.def("fused_ir_span",
-        [](uintptr_t in, uintptr_t w, uintptr_t bp, uintptr_t table, uintptr_t out, int B, int H,
-           int W, int Cin, int hidP, int Cout, int dil, int residual, int nspan, int WR, int WCP,
-           int hstride, int npi, int xg, int xslots, uintptr_t stream, uintptr_t trace) {
-          FusedSpanParams p;
-          p.xslots = xslots;
-          p.trace = P<long long>(trace);
-          p.in = P<const bf16>(in); p.w = P<const void>(w); p.bp = P<const float>(bp);
-          p.table = P<const int>(table); p.out = P<bf16>(out);
-          p.B = B; p.H = H; p.W = W; p.Cin = Cin; p.hidP = hidP; p.Cout = Cout; p.dil = dil;
-          p.residual = residual; p.S = nspan; p.WR = WR; p.WCP = WCP; p.hstride = hstride;
-          p.npi = npi; p.xg = xg;
-          fused_ir_span(p, S(stream));
-        },
-        py::arg("in"), py::arg("w"), py::arg("bp"), py::arg("table"), py::arg("out"), py::arg("B"),
-        py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("hidP"), py::arg("Cout"), py::arg("dil"),
-        py::arg("residual"), py::arg("nspan"), py::arg("WR"), py::arg("WCP"), py::arg("hstride"),
-        py::arg("npi"), py::arg("xg"), py::arg("xslots"), py::arg("stream"), py::arg("trace") = 0);
-  m.def("fused_ir_span_lds", &fused_ir_span_lds);
+        py::arg("wp_h") = 0, py::arg("trace") = 0);
   m.def("fused_ir_stream",
         [](uintptr_t in, uintptr_t w, uintptr_t bp, uintptr_t table, uintptr_t out, int B, int H,
            int W, int Cin, int hidP, int Cout, int dil, int residual, int nspan, int WR, int WCP,
@@ -190,8 +169,6 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("blob_bytes"), py::arg("nslot"), py::arg("hs") = 1, py::arg("Cout") = 0,
         py::arg("split") = 1);
   m.def("fused_ir_tile_lds", &fused_ir_tile_lds);
-  m.def("fused_ir_persist_lds", &fused_ir_persist_lds, py::arg("CinP"), py::arg("hidP"), py::arg("Cout"),
-        py::arg("stride"), py::arg("dil"), py::arg("TY"), py::arg("TX"), py::arg("nw") = 4);
   m.def("stem_block0",
         [](uintptr_t frames, uintptr_t lx, uintptr_t ly, uintptr_t ws, uintptr_t bs, uintptr_t wd,
            uintptr_t bd, uintptr_t wp, uintptr_t bp, uintptr_t out, int B, int Hc, int Wc, int H,

@@ -5,14 +5,17 @@
 //   out = project( relu6( dw3x3_dil( relu6( expand(x) ) ) ) ) [+ x]
 //
 // The expanded tensor never leaves the CU (the reference runs the whole
-// network as one Edge TPU call, /root/reference/sem_seg_server.py:162). Same span
-// decomposition, halo table and chunk images as fused_ir_span.hip (ops/fused_span.py),
-// but a different schedule, built from that kernel's s_memtime timeline
-// (scripts/bench_span.py --trace, profiles/r3_span_trace.txt): there every 32-channel
-// step cost ~3,900 cycles against ~400 cycles of MFMA work, because each of the eight
-// waves ran all three stages back to back (LDS read -> MFMA -> LDS write chains with a
-// full lgkmcnt drain between them), staged weights through VGPRs with a vmcnt(0) drain
-// per step, and the dilation-2 / Cin-160 variants spilled (VGPRs 256 + 35..157 spilled).
+// network as one Edge TPU call, /root/reference/sem_seg_server.py:162). Span
+// decomposition, halo table and chunk images: ops/fused_span.py. The schedule replaced
+// round 2's uniform-wave span kernel (every 32-channel step ~3,900 cycles against ~400
+// cycles of MFMA work: each wave ran all three stages back to back with full lgkmcnt
+// drains, staged weights through VGPRs with a vmcnt(0) drain per step, and spilled;
+// profiles/r3_span_trace.txt).
+//
+// Both ReLU6 are a [0, 1] clamp here: the host packs the expansion / 6, the depthwise
+// bias / 6 and the projection x 6 (fused_span.pack_fused_span), so the expansion's
+// f32 -> f16 conversion and the last fma of the depthwise chain carry the clamp bit and
+// no max / min instruction is issued (the depthwise was ~30 % of the VALU stream).
 //
 // Here:
 //   * waves 0-3 ("A", one per SIMD) only EXPAND: chunk t of the hidden channels for the
@@ -100,7 +103,7 @@ template <int KS, int NQ, int NR>
 __device__ __forceinline__ void expand_chunk(const char* Wc, const char* misc, char* Eb, int PLANE,
                                              const f32x4 (&R)[NR], const int (&hpos)[kXQ],
                                              int lane, int kq) {
-  const f16x4 z4 = {0, 0, 0, 0}, s4 = {6, 6, 6, 6};
+  const f16x4 z4 = {0, 0, 0, 0}, s4 = {1, 1, 1, 1};  // folded ReLU6: v_cvt_pk_f16_f32 ... clamp
 #pragma unroll
   for (int sub = 0; sub < 2; ++sub) {
     const f32x4 be4 = *reinterpret_cast<const f32x4*>(misc + 640 + (sub * 16 + kq * 4) * 4);
@@ -125,6 +128,16 @@ __device__ __forceinline__ void expand_chunk(const char* Wc, const char* misc, c
   }
 }
 
+// ---- depthwise 3x3 of one output pixel x 8 channels: ONE fma chain per channel pair over
+// the 9 taps, starting from the (scaled) bias; the clamp of its last fma is the folded ReLU6
+__device__ __forceinline__ f16x8 dw_chain(const f16x8 (&v)[9], const f16x8 (&wt)[9], f16x8 bd) {
+  const f16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0}, o8 = {1, 1, 1, 1, 1, 1, 1, 1};
+  f16x8 r = bd;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) r = v[t] * wt[t] + r;
+  return __builtin_elementwise_min(__builtin_elementwise_max(r, z8), o8);
+}
+
 // ---- depthwise + projection of one chunk: output groups g0, g1 over all NS Cout subtiles
 // and g2 over NS3 subtiles starting at n3 (NS3 = NS / 2 for the wide blocks: the ninth
 // group of a span is split over two waves so the accumulators fit 256 VGPRs).
@@ -134,7 +147,6 @@ template <int NS, int NS3, int DIL, int WCP, int NR, bool PIPE>
 __device__ __forceinline__ void dwproj_chunk(const char* Wp, const char* misc, const char* Ek,
                                              const int (&dpos)[kGB], int n3, f32x4 (&R)[NR],
                                              int lane, int kq) {
-  const f16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0}, s8 = {6, 6, 6, 6, 6, 6, 6, 6};
   f16x8 wt[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t) wt[t] = *reinterpret_cast<const f16x8*>(misc + t * 64 + kq * 16);
@@ -144,14 +156,7 @@ __device__ __forceinline__ void dwproj_chunk(const char* Wp, const char* misc, c
     for (int t = 0; t < 9; ++t)
       v[t] = *reinterpret_cast<const f16x8*>(Ek + dpos[g] * 16 + ((t / 3 - 1) * DIL * WCP + (t % 3 - 1) * DIL) * 16);
   };
-  auto dw = [&](const f16x8 (&v)[9]) {
-    // three independent row chains, then their sum (shorter dependency chain than 9)
-    f16x8 r0 = v[0] * wt[0] + bd, r1 = v[3] * wt[3], r2 = v[6] * wt[6];
-    r0 = v[1] * wt[1] + r0; r1 = v[4] * wt[4] + r1; r2 = v[7] * wt[7] + r2;
-    r0 = v[2] * wt[2] + r0; r1 = v[5] * wt[5] + r1; r2 = v[8] * wt[8] + r2;
-    const f16x8 sum = r0 + r1 + r2;
-    return __builtin_elementwise_min(__builtin_elementwise_max(sum, z8), s8);
-  };
+  auto dw = [&](const f16x8 (&v)[9]) { return dw_chain(v, wt, bd); };
   f16x8 dv[kGB];
   if (PIPE) {
     // the next group's 9 taps are in flight while this group's depthwise runs (the
@@ -195,42 +200,68 @@ __device__ __forceinline__ void dwproj_chunk(const char* Wp, const char* misc, c
 // (indices past nlast clamp to it: duplicated work that is never stored), accumulating
 // into R[r0 + g * NN + j]. Used with group 8 moved to the expansion waves (G8A): those run
 // one group x ceil(NS/4) subtiles each, the projection waves two groups x NS.
-template <int NG, int NN, int DIL, int WCP, int NR, bool PIPE = true>
+template <int NG, int NN, int DIL, int WCP, int NR, bool PIPE = true, bool HALF = false>
 __device__ __forceinline__ void dwproj_groups(const char* Wp, const char* misc, const char* Ek,
                                               const int (&dpos)[NG], int n0, int nlast, f32x4 (&R)[NR],
                                               int r0, int lane, int kq) {
-  const f16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0}, s8 = {6, 6, 6, 6, 6, 6, 6, 6};
-  f16x8 wt[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) wt[t] = *reinterpret_cast<const f16x8*>(misc + t * 64 + kq * 16);
-  const f16x8 bd = *reinterpret_cast<const f16x8*>(misc + 576 + kq * 16);
-  auto taps = [&](int g, f16x8 (&v)[9]) {
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-      v[t] = *reinterpret_cast<const f16x8*>(Ek + dpos[g] * 16 + ((t / 3 - 1) * DIL * WCP + (t % 3 - 1) * DIL) * 16);
-  };
-  auto dw = [&](const f16x8 (&v)[9]) {
-    f16x8 r0_ = v[0] * wt[0] + bd, r1 = v[3] * wt[3], r2 = v[6] * wt[6];
-    r0_ = v[1] * wt[1] + r0_; r1 = v[4] * wt[4] + r1; r2 = v[7] * wt[7] + r2;
-    r0_ = v[2] * wt[2] + r0_; r1 = v[5] * wt[5] + r1; r2 = v[8] * wt[8] + r2;
-    const f16x8 sum = r0_ + r1 + r2;
-    return __builtin_elementwise_min(__builtin_elementwise_max(sum, z8), s8);
-  };
   f16x8 dv[NG];
-  if (NG == 2 && PIPE) {  // the second group's taps in flight while the first one's depthwise runs
-    f16x8 va[9], vb[9];
-    taps(0, va);
-    __builtin_amdgcn_sched_barrier(0);
-    taps(NG - 1, vb);
-    dv[0] = dw(va);
-    dv[NG - 1] = dw(vb);
-  } else {
+  if (HALF) {
+    // register-lean form for the kernels whose accumulators take 160 VGPRs (block 16, and
+    // the G8A variants of blocks 14-15: those spilled, and each spill reload's vmcnt(0)
+    // also waited for the next chunk's LDS-DMA): the 8 channels in two f16x4 halves, so
+    // only half the tap and weight registers are live at a time (same LDS bytes)
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    const h4 z4 = {0, 0, 0, 0}, o4 = {1, 1, 1, 1};
+    h4 lo[NG], hi[NG];
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      f16x8 v[9];
-      taps(g, v);
-      dv[g] = dw(v);
-      if (NG > 1) __builtin_amdgcn_sched_barrier(0);
+    for (int hf = 0; hf < 2; ++hf) {
+      h4 wt[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) wt[t] = *reinterpret_cast<const h4*>(misc + t * 64 + kq * 16 + hf * 8);
+      const h4 bd = *reinterpret_cast<const h4*>(misc + 576 + kq * 16 + hf * 8);
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        h4 v[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+          v[t] = *reinterpret_cast<const h4*>(Ek + dpos[g] * 16 + hf * 8 +
+                                              ((t / 3 - 1) * DIL * WCP + (t % 3 - 1) * DIL) * 16);
+        h4 r = bd;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) r = v[t] * wt[t] + r;
+        r = __builtin_elementwise_min(__builtin_elementwise_max(r, z4), o4);
+        if (hf == 0) lo[g] = r; else hi[g] = r;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int g = 0; g < NG; ++g) dv[g] = __builtin_shufflevector(lo[g], hi[g], 0, 1, 2, 3, 4, 5, 6, 7);
+  } else {
+    f16x8 wt[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wt[t] = *reinterpret_cast<const f16x8*>(misc + t * 64 + kq * 16);
+    const f16x8 bd = *reinterpret_cast<const f16x8*>(misc + 576 + kq * 16);
+    auto taps = [&](int g, f16x8 (&v)[9]) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+        v[t] = *reinterpret_cast<const f16x8*>(Ek + dpos[g] * 16 + ((t / 3 - 1) * DIL * WCP + (t % 3 - 1) * DIL) * 16);
+    };
+    auto dw = [&](const f16x8 (&v)[9]) { return dw_chain(v, wt, bd); };
+    if (NG == 2 && PIPE) {  // the second group's taps in flight while the first one's depthwise runs
+      f16x8 va[9], vb[9];
+      taps(0, va);
+      __builtin_amdgcn_sched_barrier(0);
+      taps(NG - 1, vb);
+      dv[0] = dw(va);
+      dv[NG - 1] = dw(vb);
+    } else {
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        f16x8 v[9];
+        taps(g, v);
+        dv[g] = dw(v);
+        if (NG > 1) __builtin_amdgcn_sched_barrier(0);
+      }
     }
   }
 #pragma unroll
@@ -240,6 +271,9 @@ __device__ __forceinline__ void dwproj_groups(const char* Wp, const char* misc, 
 #pragma unroll
     for (int g = 0; g < NG; ++g)
       R[r0 + g * NN + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, dv[g], R[r0 + g * NN + j], 0, 0, 0);
+    // register-lean: at most 4 projection fragments in flight (the scheduler otherwise
+    // hoists all NN fragment reads above the first MFMA: 80 VGPRs at NN = 20)
+    if (HALF && j % 4 == 3) __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -302,6 +336,8 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
   constexpr int Q8 = (NS + 3) / 4;  // G8A: group-8 subtiles per expansion wave
   constexpr int NRA = XQ * KS + (G8A ? Q8 : 0), NRB = (G8A || (MODE & 3) == 2) ? 2 * NS : 2 * NS + NS3;
   constexpr int NR = NRA > NRB ? NRA : NRB;
+  // G8A with >= 112 accumulator / X VGPRs: the register-lean depthwise (dwproj_groups HALF)
+  constexpr bool LEAN = G8A && NR >= 28;
   f32x4 R[NR];
   int hpos[kXQ];
   if (wid < 4) {
@@ -368,6 +404,36 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
     const bool more = t + LAG < NC;
     if (more) issue(t + LAG);
     if (expander) {
+      if (G8A && !(LEAN && NS > 10)) {
+        // group 8 of chunk t-1: its 9 taps, weights and bias are read FIRST, so their LDS
+        // latency runs under the expansion's MFMAs instead of after them
+        f16x8 v8[9], wt8[9], bd8 = {};
+        const int c = t - 1;
+        if (t >= 1) {
+          const char* misc = ring + (c % kNSL) * CHB + WEB + WPB;
+          const char* Ek = sE + (c & 1) * 4 * PLANE + kq * PLANE;
+#pragma unroll
+          for (int u = 0; u < 9; ++u) {
+            wt8[u] = *reinterpret_cast<const f16x8*>(misc + u * 64 + kq * 16);
+            v8[u] = *reinterpret_cast<const f16x8*>(Ek + dpos8[0] * 16 + ((u / 3 - 1) * DIL * WCP + (u % 3 - 1) * DIL) * 16);
+          }
+          bd8 = *reinterpret_cast<const f16x8*>(misc + 576 + kq * 16);
+        }
+        if (t < NC) {
+          const char* Wc = ring + (t % kNSL) * CHB;
+          expand_chunk<KS, XQ, NR>(Wc, Wc + WEB + WPB, sE + (t & 1) * 4 * PLANE, PLANE, R, hpos, lane, kq);
+        }
+        if (t >= 1) {
+          const char* Wp = ring + (c % kNSL) * CHB + WEB;
+          const f16x8 dv = dw_chain(v8, wt8, bd8);
+#pragma unroll
+          for (int j = 0; j < Q8; ++j) {
+            const int n = min(wid * Q8 + j, NS - 1);
+            const f16x8 af = *reinterpret_cast<const f16x8*>(Wp + n * 1024 + lane * 16);
+            R[XQ * KS + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, dv, R[XQ * KS + j], 0, 0, 0);
+          }
+        }
+      } else {
       if (t < NC) {
         const char* Wc = ring + (t % kNSL) * CHB;
         expand_chunk<KS, XQ, NR>(Wc, Wc + WEB + WPB, sE + (t & 1) * 4 * PLANE, PLANE, R, hpos, lane, kq);
@@ -375,8 +441,9 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
       if (G8A && t >= 1) {
         const int c = t - 1;
         const char* Wp = ring + (c % kNSL) * CHB + WEB;
-        dwproj_groups<1, Q8, DIL, WCP, NR>(Wp, Wp + WPB, sE + (c & 1) * 4 * PLANE + kq * PLANE, dpos8,
+        dwproj_groups<1, Q8, DIL, WCP, NR, true, (LEAN && NS > 10)>(Wp, Wp + WPB, sE + (c & 1) * 4 * PLANE + kq * PLANE, dpos8,
                                            wid * Q8, NS - 1, R, XQ * KS, lane, kq);
+      }
       }
     } else if (t >= 1) {
       const int c = t - 1;
@@ -389,7 +456,7 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
           dwproj_groups<1, NS, DIL, WCP, NR>(Wp, Wp + WPB, Ek, dposn, 0, NS - 1, R, NS, lane, kq);
         }
       } else if (G8A)
-        dwproj_groups<2, NS, DIL, WCP, NR, (NS <= 10)>(Wp, Wp + WPB, sE + (c & 1) * 4 * PLANE + kq * PLANE, dpos01, 0,
+        dwproj_groups<2, NS, DIL, WCP, NR, (NS <= 10 && !LEAN), (LEAN && NS > 10)>(Wp, Wp + WPB, sE + (c & 1) * 4 * PLANE + kq * PLANE, dpos01, 0,
                                            NS - 1, R, 0, lane, kq);
       else
         dwproj_chunk<NS, NS3, DIL, WCP, NR, true>(Wp, Wp + WPB, sE + (c & 1) * 4 * PLANE + kq * PLANE,

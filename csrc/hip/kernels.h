@@ -113,17 +113,13 @@ struct FusedIRParams {
   const void* bd_h = nullptr;
   const void* wp_h = nullptr;
   long long* trace = nullptr;  // debug timeline (128 slots), tile kernel only
-  int nw = 4;                  // fused_ir_persist: waves per workgroup (4 or 8)
 };
 void fused_inverted_residual(const FusedIRParams& p, hipStream_t s);
-// Persistent variant of the tile kernel (fused_ir_persist.hip): block weights staged
-// in LDS once per workgroup, next input tile prefetched; same params (TY/TX > 0).
-void fused_ir_persist(const FusedIRParams& p, hipStream_t s);
-// LDS bytes it needs (0: tile too large for the input-tile prefetch registers).
-size_t fused_ir_persist_lds(int CinP, int hidP, int Cout, int stride, int dil, int TY, int TX, int nw = 4);
-// Fused inverted residual over raster spans (fused_ir_span.hip): stride 1, dilation
-// 1-7, Cin % 32 == 0, Cout % 16 == 0. w: host-packed chunk images (hip_ops.pack_fused_span),
-// table: span/halo table (hip_ops.span_table) of S spans, hstride ints each.
+// Fused inverted residual over raster spans of the 33x33 maps (fused_ir_stream.hip):
+// stride 1, dilation 1-2, Cin % 32 == 0, Cout % 16 == 0. w: host-packed chunk images
+// (ops/fused_span.pack_fused_span, ReLU6 folded as a [0, 1] clamp: expansion / 6, depthwise
+// bias / 6, projection x 6), table: span/halo table (fused_span.span_table) of S spans,
+// hstride ints each.
 struct FusedSpanParams {
   const bf16* in = nullptr;   // [B, H, W, Cin]
   const void* w = nullptr;    // [hidP / 32][(2*Cin/32 + Cout/16 + 1) KiB]
@@ -132,8 +128,7 @@ struct FusedSpanParams {
   bf16* out = nullptr;        // [B, H, W, Cout]
   int B = 0, H = 0, W = 0, Cin = 0, hidP = 0, Cout = 0, dil = 1, residual = 0;
   int S = 8, WR = 0, WCP = 0, hstride = 0;
-  int npi = 4, xg = 2;        // pixel-group wave sets; halo groups per wave (instantiation)
-  int xslots = 0;             // halo groups beyond 16 (their X lives in LDS; xg == 3 only)
+  int npi = 0;                // fused_ir_stream variant (wave roles / ring slots)
   long long* trace = nullptr; // debug s_memtime timeline [B*S][2][64]
   int nh_max = 0;             // largest halo of the table (fused_ir_stream: <= 320)
   int hsplit = 1;             // fused_ir_stream: workgroups per span over the hidden chunks
@@ -141,10 +136,7 @@ struct FusedSpanParams {
   int* cnt = nullptr;         // hsplit > 1: per-span tickets [B*S] for the in-launch combine (null:
                               // the caller runs stream_combine)
 };
-void fused_ir_span(const FusedSpanParams& p, hipStream_t s);
-size_t fused_ir_span_lds(int Cin, int Cout, int WR, int WCP, int xslots);
-// Wave-specialised variant over the same spans / chunk images (fused_ir_stream.hip):
-// expansion waves 0-3, depthwise+projection waves 4-7, LDS-DMA chunk ring.
+// Wave-specialised: expansion waves 0-3, depthwise+projection waves 4-7, LDS-DMA chunk ring.
 void fused_ir_stream(const FusedSpanParams& p, hipStream_t s);
 size_t fused_ir_stream_lds(int Cin, int Cout, int WR, int WCP, int nsl = 0);
 // sum of the hidden-split partials + bias (+ residual) -> bf16 [M, Cout]

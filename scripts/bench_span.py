@@ -1,7 +1,8 @@
-"""Microbenchmark + s_memtime phase timeline of the fused span kernel on the 33x33
-blocks of DeepLabv3-MobileNetV2 (B = 32, random data and weights).
+"""Microbenchmark + s_memtime phase timeline of the wave-specialised fused IR kernel
+(fused_ir_stream) on the 33x33 blocks of DeepLabv3-MobileNetV2 (B = 32, random data and
+weights).
 
-  python scripts/bench_span.py [--B 32] [--trace]
+  python scripts/bench_span.py [--B 32] [--trace] [--only 16] [--variants 0,1]
 """
 import argparse
 import sys
@@ -28,7 +29,7 @@ def main():
     ap.add_argument("--trace", action="store_true")
     ap.add_argument("--only", type=int, default=0, help="run only this block index")
     ap.add_argument("--S", type=int, default=0, help="run only this span count")
-    ap.add_argument("--stream", action="store_true", help="time fused_ir_stream (wave-specialised)")
+    ap.add_argument("--variants", default="", help="comma list of stream variants (default: all)")
     a = ap.parse_args()
     dev = "cuda"
     B, H = a.B, a.H
@@ -45,14 +46,13 @@ def main():
                 tab = FS.span_table(H, H, S, dil, dev)
             except ValueError:
                 continue
-            opts = ([0, 1, 2] if cout <= 96 and dil == 1 else [0, 1]) if a.stream else FS.span_npi_options(cout)
-            if a.stream and not FS.stream_supported(cin, cout, 1, H, H, S, dil):
+            opts = ((0, 1, 2) if cout <= 96 and dil == 1 else (0, 1)) + ((4,) if cout <= 160 else ())
+            if a.variants:
+                opts = tuple(v for v in map(int, a.variants.split(",")) if v in opts)
+            if not FS.stream_supported(cin, cout, 1, H, H, S, dil):
                 continue
             for npi in opts:
-                if a.stream:
-                    run = lambda: FS.fused_ir_stream(x, packed, tab, out, B=B, residual=spec.residual, variant=npi)
-                else:
-                    run = lambda: FS.fused_ir_span(x, packed, tab, out, B=B, residual=spec.residual, npi=npi)
+                run = lambda: FS.fused_ir_stream(x, packed, tab, out, B=B, residual=spec.residual, variant=npi)
                 for _ in range(3):
                     run()
                 st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -63,10 +63,10 @@ def main():
                 en.synchronize()
                 us = st.elapsed_time(en) / a.reps * 1e3
                 print(f"block{idx:2d} {cin:3d}->{spec.hidden:3d}->{cout:3d} d{dil} S={S:2d} "
-                      f"{f'stream v{npi}' if a.stream else f'npi={npi}'}: "
+                      f"stream v{npi}: "
                       f"{us:7.1f} us  {flop / us / 1e6:7.1f} TFLOP/s  (xg={tab['xg']}, nh_max={tab['nh_max']})",
                       flush=True)
-                if a.trace and a.stream:
+                if a.trace:
                     tr = torch.zeros(B * S * 2 * 64, dtype=torch.int64, device=dev)
                     FS.fused_ir_stream(x, packed, tab, out, B=B, residual=spec.residual, trace=tr, variant=npi)
                     torch.cuda.synchronize()
@@ -84,22 +84,6 @@ def main():
                               f"step-0 {np.median(tt[:, 4] - tt[:, 1]):.0f}"
                               + (f"; epilogue {np.median(tt[:, 63] - tt[:, 62]):.0f}" if w == 1 else ""),
                               flush=True)
-                if a.trace and not a.stream:
-                    tr = torch.zeros(B * S * 2 * 64, dtype=torch.int64, device=dev)
-                    FS.fused_ir_span(x, packed, tab, out, B=B, residual=spec.residual, npi=npi, trace=tr)
-                    torch.cuda.synchronize()
-                    t = tr.view(B * S, 2, 64).cpu().numpy().astype(np.int64)
-                    NC = packed["hidP"] // 32
-                    for w in (0, 1):
-                        tt = t[:, w]
-                        pro = np.median(tt[:, 2] - tt[:, 0])
-                        steps = min(NC + 2, 12)
-                        # per step: [C], [A], [B], staging, barrier (stamps 3..7 + 5t; 2 = loop entry)
-                        ph = np.array([[np.median(tt[:, 3 + 5 * k + i] - tt[:, 2 + 5 * k + i]) for i in range(5)]
-                                       for k in range(steps)])
-                        tot = np.median(tt[:, 63] - tt[:, 0])
-                        print(f"   wave{w}: total {tot:.0f} cyc, prologue {pro:.0f}; steady step [C, A, B, stage, barrier] = "
-                              f"{np.median(ph[2:-1], axis=0).round(0).tolist()}", flush=True)
 
 
 if __name__ == "__main__":

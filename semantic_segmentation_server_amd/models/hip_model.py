@@ -674,36 +674,17 @@ class HipDeepLab:
                 variants.insert(0, (f"tile{tile[0]}x{tile[1]}", [
                     lambda *_, x=inp, out=out, h=h, w=w, OH=OH, OW=OW, tile=tile: K.fused_ir(
                         x, fp, out, B=B, IH=h, IW=w, OH=OH, OW=OW, tile=tile)]))
-            shape = (-(-s.cout // 16), fp["CinP"] // 32)
-            if fp["we"] is not None and shape in K.FUSED_PERSIST_SHAPES:
-                for tile in _TILES:
-                    for nw in (4, 8):
-                        lds = K.fused_ir_persist_lds(fp["CinP"], fp["hidP"], s.cout, s.stride,
-                                                     s.dilation, *tile, nw)
-                        covered = -(-OH // tile[0]) * tile[0] * -(-OW // tile[1]) * tile[1]
-                        if (0 < lds <= 80 * 1024 and -(-tile[0] * tile[1] // 16) <= 2 * nw
-                                and covered <= 1.25 * OH * OW):
-                            variants.insert(0, (f"persist{tile[0]}x{tile[1]}" + ("w8" if nw == 8 else ""), [
-                                lambda *_, x=inp, out=out, h=h, w=w, OH=OH, OW=OW, tile=tile, nw=nw:
-                                K.fused_ir(x, fp, out, B=B, IH=h, IW=w, OH=OH, OW=OW, tile=tile,
-                                           persist=8 if nw == 8 else True)]))
         if "fused" in blk:
             fp = blk["fused"]
             variants.insert(0, ("fused", [lambda *_, x=inp, out=out, h=h, w=w, OH=OH, OW=OW:
                                           K.fused_ir(x, fp, out, B=B, IH=h, IW=w, OH=OH, OW=OW)]))
-        if blk["expand"] is not None and s.stride == 1 and FS.span_npi_options(s.cout):
+        if blk["expand"] is not None and s.stride == 1 and (s.cin, s.cout) in FS.STREAM_SHAPES:
             # expanded tensor kept on chip: raster spans of ~h*w/S pixels per workgroup
             for S in self._span_counts(B, h, w):
-                if not FS.span_supported(s.cin, s.cout, 1, h, w, S, s.dilation):
-                    continue
-                if "span" not in blk:
-                    blk["span"] = self._pack_span(blk, s)
-                tab = self._span_table(h, w, S, s.dilation)
-                for npi in FS.span_npi_options(s.cout):
-                    variants.insert(0, (f"span{S}n{npi}", [
-                        lambda *_, x=inp, out=out, tab=tab, npi=npi, sp=blk["span"]: FS.fused_ir_span(
-                            x, sp, tab, out, B=B, residual=s.residual, npi=npi)]))
                 if FS.stream_supported(s.cin, s.cout, 1, h, w, S, s.dilation):
+                    if "span" not in blk:
+                        blk["span"] = self._pack_span(blk, s)
+                    tab = self._span_table(h, w, S, s.dilation)
                     # wave-specialised: expansion waves | depthwise+projection waves
                     # 4 / 6: the 3-slot chunk ring (72 instead of 81 KiB for blocks 7-9: two
                     # workgroups per CU)

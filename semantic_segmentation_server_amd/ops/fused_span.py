@@ -1,4 +1,4 @@
-"""Host side of the fused inverted-residual span kernel (csrc/hip/fused_ir_span.hip).
+"""Host side of the fused inverted-residual span kernel (csrc/hip/fused_ir_stream.hip).
 
 The kernel runs one MobileNetV2 inverted residual (expand 1x1 + ReLU6 -> depthwise 3x3
 dilated + ReLU6 -> project 1x1 [+ residual]) for the output-stride-16 stage with the
@@ -11,6 +11,10 @@ dilated + ReLU6 -> project 1x1 [+ residual]) for the output-stride-16 stage with
 * ``pack_fused_span``: per 32-channel hidden chunk, one contiguous "chunk image" in
   the byte layout the kernel copies into LDS: expansion MFMA fragments (bf16),
   projection fragments (fp16), depthwise weights/bias (fp16) and expansion bias (fp32).
+  Both ReLU6 are folded into a [0, 1] clamp: relu6(v) = 6 * clamp(v / 6, 0, 1), so the
+  expansion weights/bias and the depthwise bias are packed / 6 and the projection
+  weights x 6. The kernel's clamps are then the ``clamp`` bit of its last depthwise
+  ``v_pk_fma_f16`` and of the expansion's ``v_cvt_pk_f16_f32`` (no max/min instructions).
 * ``emulate_fused_span``: a numpy re-execution of the kernel's data flow from those
   packed bytes (CPU tests of the packing and table logic without a GPU).
 
@@ -27,6 +31,7 @@ import torch
 HDR = 4          # table header ints: p0, p1, wy0, nh
 MAX_GROUPS = 9   # output pixel groups per span (kSOG)
 NW = 8           # waves per workgroup
+RELU6 = 6.0      # folded ReLU6 bound (see pack_fused_span)
 
 
 def span_geometry(H: int, W: int, S: int, dil: int):
@@ -102,6 +107,8 @@ def pack_fused_span(we: torch.Tensor, be: torch.Tensor, wd: torch.Tensor, bd: to
     Bd[:hid] = bd.detach().float().cpu()
     Wp = torch.zeros(Cout, hidP, dtype=f32)
     Wp[:, :hid] = wp.detach().float().cpu().reshape(Cout, hid)
+    # ReLU6 as a [0, 1] clamp (module docstring): E' = E / 6, D' = D / 6
+    We, Be, Bd, Wp = We / RELU6, Be / RELU6, Bd / RELU6, Wp * RELU6
     # expansion fragments: [c][sub][k][lane = kq*16 + r][e] = We[c*32 + sub*16 + r][k*32 + kq*8 + e]
     fe = We.reshape(NC, 2, 16, KS, 4, 8).permute(0, 1, 3, 4, 2, 5).reshape(NC, -1)
     # projection fragments: [c][n][lane][e] = Wp[n*16 + r][c*32 + kq*8 + e]
@@ -122,37 +129,12 @@ def pack_fused_span(we: torch.Tensor, be: torch.Tensor, wd: torch.Tensor, bd: to
     return out
 
 
-def fused_ir_span(x: torch.Tensor, packed: Dict, table: Dict, out: torch.Tensor, *, B: int,
-                  residual: bool, npi: int, trace: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Launch fused_ir_span_kernel. x [B, H, W, Cin] bf16, out [B, H, W, Cout] bf16."""
-    from .hip_ops import _chk, _dbg, _hip_mod, _ptr, _stream
-    H, W = table["H"], table["W"]
-    Cin, Cout = packed["Cin"], packed["Cout"]
-    if residual and Cin != Cout:
-        raise ValueError("fused_ir_span: residual needs Cin == Cout")
-    _chk(x, torch.bfloat16, "x", B * H * W * Cin)
-    _chk(out, torch.bfloat16, "out", B * H * W * Cout)
-    _chk(packed["w"], torch.uint8, "w", (packed["hidP"] // 32) * chunk_bytes(Cin, Cout))
-    _chk(packed["bp"], torch.float32, "bp", Cout)
-    _chk(table["table"], torch.int32, "table", table["S"] * table["hstride"])
-    if trace is not None:
-        _chk(trace, torch.int64, "trace", B * table["S"] * 2 * 64)
-    _hip_mod().fused_ir_span(_ptr(x), _ptr(packed["w"]), _ptr(packed["bp"]), _ptr(table["table"]),
-                             _ptr(out), B, H, W, Cin, packed["hidP"], Cout, table["dil"],
-                             int(bool(residual)), table["S"], table["WR"], table["WCP"],
-                             table["hstride"], npi, table["xg"], table["xslots"], _stream(),
-                             0 if trace is None else _ptr(trace))
-    _dbg("fused_ir_span")
-    return out
-
-
 def fused_ir_stream(x: torch.Tensor, packed: Dict, table: Dict, out: torch.Tensor, *, B: int,
                     residual: bool, trace: Optional[torch.Tensor] = None, variant: int = 0,
                     hsplit: int = 1, part: Optional[torch.Tensor] = None,
                     cnt: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Launch fused_ir_stream_kernel (csrc/hip/fused_ir_stream.hip): the same spans and
-    chunk images as fused_ir_span, run by wave-specialised expansion / depthwise+projection
-    waves over an LDS-DMA chunk ring. x [B, H, W, Cin] bf16, out [B, H, W, Cout] bf16.
+    """Launch fused_ir_stream_kernel (csrc/hip/fused_ir_stream.hip): wave-specialised
+    expansion / depthwise+projection waves over an LDS-DMA ring of the packed chunk images. x [B, H, W, Cin] bf16, out [B, H, W, Cout] bf16.
     variant 1: the span's ninth output group runs on the expansion waves (balances the two
     roles: the depthwise+projection waves were the critical path, profiles/r3_stream_trace.txt).
     hsplit > 1: each span's hidden chunks are split over ``hsplit`` workgroups (batch 1 has
@@ -215,23 +197,6 @@ def stream_supported(Cin: int, Cout: int, stride: int, H: int, W: int, S: int, d
     return int(_hip_mod().fused_ir_stream_lds(Cin, Cout, t["WR"], t["WCP"])) <= 160 * 1024
 
 
-def span_npi_options(Cout: int):
-    """Wave splits (pixel-group sets NPI x Cout slices 8/NPI) instantiated per Cout."""
-    return {64: (2, 4), 96: (4, 8), 160: (4, 8), 320: (2,)}.get(Cout, ())
-
-
-def span_supported(Cin: int, Cout: int, stride: int, H: int, W: int, S: int, dil: int) -> bool:
-    if stride != 1 or (Cin, Cout) not in ((64, 64), (64, 96), (96, 96), (96, 160), (160, 160), (160, 320)):
-        return False
-    try:
-        t = span_table(H, W, S, dil)
-    except ValueError:
-        return False
-    from .hip_ops import _hip_mod
-    lds = int(_hip_mod().fused_ir_span_lds(Cin, Cout, t["WR"], t["WCP"], t["xslots"]))
-    return lds <= 160 * 1024
-
-
 # ----------------------------------------------------------------------------- emulation
 def _f16(a):
     return np.asarray(a, dtype=np.float16)
@@ -240,8 +205,9 @@ def _f16(a):
 def emulate_fused_span(x: np.ndarray, packed: Dict, table: Dict, *, residual: bool) -> np.ndarray:
     """Re-execute the kernel's data flow on the CPU from the packed chunk images and the
     span table. x: [B, H, W, Cin] float (bf16-representable). Returns [B, H, W, Cout] fp32
-    (before the final bf16 rounding). Mirrors fused_ir_span_kernel: fp32 expansion, fp16 E,
-    fp16 depthwise (accumulated in fp16), fp16 D, fp32 projection accumulation."""
+    (before the final bf16 rounding). Mirrors fused_ir_stream_kernel: fp32 expansion, fp16 E
+    clamped to [0, 1] (ReLU6 / 6), fp16 depthwise (one fma chain over the 9 taps from the
+    bias, the last fma clamped), fp32 projection accumulation."""
     B, H, W, Cin = x.shape
     Cout, hidP = packed["Cout"], packed["hidP"]
     KS, NS, NC = Cin // 32, Cout // 16, hidP // 32
@@ -269,14 +235,14 @@ def emulate_fused_span(x: np.ndarray, packed: Dict, table: Dict, *, residual: bo
                 ent = tab[j, HDR:HDR + nh]
                 px, pos = ent >> 12, ent & 4095
                 e = xf[b, px] @ We.T + be                            # fp32 MFMA
-                E[pos] = np.clip(_f16(e), 0, 6)
+                E[pos] = np.clip(_f16(e), 0, 1)
                 ps = np.arange(p0, p1)
                 ctr = (ps // W - wy0) * WCP + ps % W + d
                 s = np.broadcast_to(bd, (len(ps), 32)).astype(np.float16)
                 for t in range(9):
                     off = (t // 3 - 1) * d * WCP + (t % 3 - 1) * d
                     s = _f16(E[ctr + off] * wd[t] + s)
-                D = np.clip(s, 0, 6).astype(np.float32)
+                D = np.clip(s, 0, 1).astype(np.float32)
                 out[b, p0:p1] += D @ Wp.T
     out += bp
     if residual:

@@ -471,19 +471,11 @@ def tap_conv(x, wpk, bias_p, out, *, B, H, W, Cin, Cout, k=3, dil=1, ldo=None, c
     return out
 
 
-FUSED_PERSIST_SHAPES = {(2, 1), (4, 1), (4, 2), (6, 2)}  # (Cout/16, CinP/32), fused_ir_persist.hip
-
-
-def fused_ir_persist_lds(CinP, hidP, Cout, stride, dil, TY, TX, nw=4) -> int:
-    return int(_hip_mod().fused_ir_persist_lds(CinP, hidP, Cout, stride, dil, TY, TX, nw))
-
-
-def fused_ir(x, packed: dict, out, *, B, IH, IW, OH, OW, tile=None, trace=None, persist=False):
+def fused_ir(x, packed: dict, out, *, B, IH, IW, OH, OW, tile=None, trace=None):
     """Fused inverted residual. ``packed`` from ``pack_fused_ir``.
 
     ``tile=(TY, TX)`` selects the general 2-D tile kernel (any dilation, Cin <= 160,
-    Cout <= 320); ``None`` the 16-wide row-tile kernel (dilation 1, Cin <= 64).
-    ``persist`` (with a tile): the persistent kernel with LDS-resident weights."""
+    Cout <= 320); ``None`` the 16-wide row-tile kernel (dilation 1, Cin <= 64)."""
     P = packed
     TY, TX = tile if tile is not None else (0, 0)
     if tile is None and P.get("dil", 1) != 1:
@@ -501,7 +493,7 @@ def fused_ir(x, packed: dict, out, *, B, IH, IW, OH, OW, tile=None, trace=None, 
                         _ptr(P["wp"]), _ptr(P["bp"]), _ptr(out), B, IH, IW, P["Cin"], P["CinP"],
                         P["hidP"], P["Cout"], OH, OW, P["stride"], int(P["residual"]), _stream(),
                         P.get("dil", 1), TY, TX, _ptr(P["wd_h"]), _ptr(P["bd_h"]), _ptr(P["wp_h"]),
-                        _ptr(trace), (2 if persist == 8 else 1) if (persist and tile is not None) else 0)
+                        _ptr(trace))
     _dbg('fused_ir')
     return out
 

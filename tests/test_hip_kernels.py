@@ -1079,11 +1079,8 @@ def test_stem_band(cam, H, R, nbx):
     (24, 24, 1, 1, 41, (11, 11)),    # block 2 shape: residual, Cin 24 -> CinP 32
     (32, 32, 1, 1, 30, (8, 13)),     # blocks 4/5, partial edge tiles
     (32, 16, 1, 1, 37, (8, 16)),     # block 0: no expansion (t = 1)
-    (24, 24, 1, 1, 41, (16, 16)),    # 8-wave persistent tiles
-    (32, 32, 1, 1, 30, (11, 22)),
 ])
-@pytest.mark.parametrize("persist", [False, True, 8])
-def test_fused_ir_tile(cin, cout, stride, dil, H, tile, persist):
+def test_fused_ir_tile(cin, cout, stride, dil, H, tile):
     from semantic_segmentation_server_amd.models.layers import init_random
     from semantic_segmentation_server_amd.models.mobilenetv2 import InvertedResidual, IRSpec
     K = _hip()
@@ -1110,17 +1107,8 @@ def test_fused_ir_tile(cin, cout, stride, dil, H, tile, persist):
     packed = K.pack_fused_ir(ew, eb, dwf[:, 0], dbf, pwf[:, :, 0, 0], pbf, Cin=cin,
                              hid=spec.hidden, Cout=cout, stride=stride, residual=spec.residual,
                              device=DEV, dil=dil)
-    if -(-tile[0] * tile[1] // 16) > 8 and persist != 8:
-        pytest.skip("tiles over 128 pixels: 8-wave persistent kernel only")
-    if persist:
-        shape = (-(-cout // 16), packed["CinP"] // 32)
-        lds = K.fused_ir_persist_lds(packed["CinP"], packed["hidP"], cout, stride, dil, *tile,
-                                     8 if persist == 8 else 4)
-        if ew is None or shape not in K.FUSED_PERSIST_SHAPES or not 0 < lds <= 160 * 1024:
-            pytest.skip("no persistent instantiation for this block shape")
     out = torch.full((B, OH, OW, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
-    K.fused_ir(_nhwc(x).to(DEV), packed, out, B=B, IH=H, IW=W, OH=OH, OW=OW, tile=tile,
-               persist=persist)
+    K.fused_ir(_nhwc(x).to(DEV), packed, out, B=B, IH=H, IW=W, OH=OH, OW=OW, tile=tile)
     torch.cuda.synchronize()
     assert torch.isfinite(out).all()
     assert _rel(_nchw(out).cpu(), ref) < 2e-2
@@ -1323,41 +1311,6 @@ def test_stream_group_matches_single_engine(monkeypatch):
     (96, 96, 1, 33, 8),     # blocks 11-12 (residual)
     (96, 160, 1, 33, 8),    # block 13
     (160, 160, 2, 33, 8),   # blocks 14-15 (dilation 2, residual)
-    (160, 320, 2, 33, 8),   # block 16
-    (160, 160, 2, 33, 16),  # 16 spans per image
-    (96, 96, 1, 29, 7),     # odd map / span sizes
-    (160, 320, 2, 23, 4),
-])
-def test_fused_ir_span(cin, cout, dil, H, S):
-    """Fused span kernel (expanded tensor on chip) vs the fp32 torch block, and vs the
-    numpy re-execution of its own data flow from the packed operands."""
-    from semantic_segmentation_server_amd.ops import fused_span as FS
-    from test_fused_span_cpu import _block, pack_block  # tests/ is on sys.path (prepend mode)
-    blk, spec = _block(cin, cout, dil, seed=cin * 7 + cout + dil)
-    g = torch.Generator().manual_seed(21)
-    B, W = 3, H
-    x = torch.randn(B, cin, H, W, generator=g).to(torch.bfloat16)
-    with torch.no_grad():
-        ref = blk(x.float())
-    packed = pack_block(blk, spec, device=DEV)
-    table = FS.span_table(H, W, S, dil, DEV)
-    xd = _nhwc(x).to(DEV)
-    emu = FS.emulate_fused_span(_nhwc(x).float().numpy(), packed, table, residual=spec.residual)
-    for npi in FS.span_npi_options(cout):
-        out = torch.full((B, H, W, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
-        FS.fused_ir_span(xd, packed, table, out, B=B, residual=spec.residual, npi=npi)
-        torch.cuda.synchronize()
-        assert torch.isfinite(out).all(), npi
-        assert _rel(_nchw(out).cpu(), ref) < 2e-2, npi
-        assert _rel(out.cpu().float(), torch.from_numpy(emu)) < 5e-3, npi
-
-
-@pytest.mark.parametrize("cin,cout,dil,H,S", [
-    (64, 64, 1, 33, 8),     # blocks 7-9 (residual)
-    (64, 96, 1, 33, 8),     # block 10
-    (96, 96, 1, 33, 8),     # blocks 11-12 (residual)
-    (96, 160, 1, 33, 8),    # block 13
-    (160, 160, 2, 33, 8),   # blocks 14-15 (dilation 2, residual)
     (160, 160, 2, 33, 16),  # 16 spans per image
     (160, 320, 2, 33, 8),   # block 16 (3-slot ring, two epilogue passes)
     (64, 64, 1, 33, 32),    # batch-1 span counts
@@ -1365,7 +1318,7 @@ def test_fused_ir_span(cin, cout, dil, H, S):
 ])
 def test_fused_ir_stream(cin, cout, dil, H, S):
     """Wave-specialised fused IR kernel vs the fp32 torch block and vs the numpy
-    re-execution of the span kernel's data flow from the same packed chunk images."""
+    re-execution of its data flow from the packed chunk images."""
     from semantic_segmentation_server_amd.ops import fused_span as FS
     from test_fused_span_cpu import _block, pack_block  # tests/ is on sys.path (prepend mode)
     W = 33
