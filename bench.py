@@ -3,14 +3,17 @@
 
 Config (BASELINE.json): DeepLabv3-MobileNetV2, 513x513, PASCAL VOC (21 classes),
 bf16, synthetic 640x480 BGR camera frames, random-init weights. One process per
-GPU (torchrun); per-rank batch ``--batch`` (default 32) => weak scaling.
+GPU (torchrun); per-rank batch ``--batch`` (default 32) => weak scaling; ``--global_batch G``
+=> strong scaling (G / N frames per rank, BASELINE config 3 as written: 32 over 8 GPUs).
 
 One timed step, on every rank:
   H2D of the rank's next frames (pinned, copy stream, overlapped) or the rank-0
   upload + RCCL scatter (``--ingest scatter``)
   -> hipGraph replay: letterbox/normalise + DeepLabv3 + upsample/argmax + mask +
      CCL + contour statistics -> packed records
-  -> RCCL gather of records to rank 0 -> D2H -> push into the LIFO result hub.
+  -> records + frame metadata to rank 0 (pinned host memory over gloo by default, one step
+     late; ``--gather rccl``: an RCCL gather of a packed device row) -> push into the
+     LIFO result hub.
 
 After the timed region, rank 0 serves the hub over gRPC on loopback and a client
 subprocess measures GetSegmentedObjects latency while all ranks keep stepping
@@ -80,7 +83,21 @@ def main() -> int:
     p.add_argument("--serve", action="store_true",
                    help="time the real serving loop (Server / DistributedServer: feeder thread, "
                         "pinned ring, lag-1 pipeline, gRPC services up) instead of the bench loop")
+    p.add_argument("--supervise", action="store_true",
+                   help="with --serve: the CLI default -- a parent that never touches the GPU hosts "
+                        "gRPC + hub, --gpus worker processes run the pipeline and ship records "
+                        "through shared-memory rings (runtime/supervisor.py)")
+    p.add_argument("--global_batch", type=int, default=0,
+                   help="strong scaling: a fixed node-wide batch split over the ranks (per-GPU "
+                        "batch = global_batch / N; BASELINE config 3 as written: 32 over 8 GPUs)")
     a = p.parse_args()
+    a.scaling = "weak"
+    if a.global_batch:
+        nw = int(os.environ.get("WORLD_SIZE", "1")) if not a.supervise else max(1, a.gpus)
+        if a.global_batch % nw:
+            p.error(f"--global_batch {a.global_batch} is not a multiple of the {nw} ranks")
+        a.batch = a.global_batch // nw
+        a.scaling = "strong"
     if a.serve:
         return _serve_bench(a)
     # each rank's host threads and pinned staging on its GPU's NUMA node, before the first
@@ -103,6 +120,12 @@ def main() -> int:
     # SSA_SHARE_GPU=1 (rehearsal: several ranks on one GPU): RCCL refuses two ranks on one
     # device, so the auto choice is the gloo group with the host-memory gather
     share = os.environ.get("SSA_SHARE_GPU", "0") == "1"
+    if share and a.ingest == "scatter":
+        # the frame scatter is a device collective (gloo scatters CPU tensors only) and RCCL
+        # refuses two ranks on one GPU: rehearse with local ingest instead
+        print("bench: --ingest scatter needs RCCL, which SSA_SHARE_GPU=1 rules out; using local ingest",
+              file=sys.stderr)
+        a.ingest = "local"
     pg = a.pg if a.pg != "auto" else (
         "nccl" if gpu and not share and (a.ingest == "scatter" or a.gather == "rccl") else "gloo")
     ctx = D.init(pg, device="cuda" if _t.cuda.is_available() and a.backend != "cpu" else "auto")
@@ -209,7 +232,7 @@ def main() -> int:
             "warmup": a.warmup,
             "ms_per_step": round(dt / a.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": a.scaling,
             "vs_baseline": None,
             "dtype": a.dtype,
             "data": f"synthetic {a.camera} BGR frames, random-init weights",
@@ -271,7 +294,19 @@ def _serve_bench(a) -> int:
                    num_classes=21 if a.arch == "mnv2" else 19, port=0, host="127.0.0.1",
                    dataset="pascal" if a.arch == "mnv2" else "cityscapes", gpus=world)
     total = a.warmup + a.steps
-    if world > 1:
+    sup = None
+    if a.supervise:
+        from semantic_segmentation_server_amd.runtime.supervisor import SupervisedServer
+        world = max(1, a.gpus)
+        cfg.gpus = world
+        sup = srv = SupervisedServer(cfg).start()
+        steps = lambda: sum(w.steps for w in sup.workers)  # noqa: E731
+        root, port = True, srv.port
+        t_up = time.time() + 900
+        while not all(w.up for w in sup.workers) and time.time() < t_up and sup.alive:
+            time.sleep(0.05)
+        total = (a.warmup + a.steps) * world
+    elif world > 1:
         from semantic_segmentation_server_amd.parallel import dist as D
         from semantic_segmentation_server_amd.parallel.serving import DistributedServer
         srv = DistributedServer(cfg, max_steps=None)
@@ -287,15 +322,17 @@ def _serve_bench(a) -> int:
         steps = lambda: srv.producer.steps  # noqa: E731
         root, port = True, srv.port
     t_lim = time.time() + 600
-    while steps() < a.warmup and time.time() < t_lim:
+    per = world if sup is not None else 1  # steps() counts every worker's steps
+    while steps() < a.warmup * per and time.time() < t_lim:
         time.sleep(0.0005)
-    if world > 1:
+    if world > 1 and sup is None:
         port = srv.port
     s0, t0 = steps(), time.perf_counter()
-    while steps() < s0 + a.steps and time.time() < t_lim:
+    while steps() < s0 + a.steps * per and time.time() < t_lim:
         time.sleep(0.0002)
     s1, t1 = steps(), time.perf_counter()
-    fps = (s1 - s0) * a.batch * world / (t1 - t0)
+    fps = (s1 - s0) * a.batch * (world // per) / (t1 - t0)
+    s1, s0 = s0 + (s1 - s0) // per, s0
     rpc = None
     if root and a.rpc > 0 and port:
         mpctx = mp.get_context("spawn")
@@ -304,7 +341,15 @@ def _serve_bench(a) -> int:
         proc.start()
         rpc = parent.recv() if parent.poll(120) else {"error": "client timeout"}
         proc.join(10)
-    if world > 1:
+    extra = {}
+    if sup is not None:
+        snap = sup.metrics.snapshot()
+        lat = snap.get("worker_frame_latency_ms") or snap.get("worker0_frame_latency_ms") or {}
+        extra = {"p50_frame_latency_ms": lat.get("p50"), "p99_frame_latency_ms": lat.get("p99"),
+                 "ipc_drops": snap.get("ipc_drops", 0), "worker_restarts": snap.get("worker_restarts", 0),
+                 "records_pushed": int(sum(b.pushed for b in sup.hub.buffers.values()))}
+        sup.stop(0)
+    elif world > 1:
         stop_evt.set()
         th.join(60)
         srv.stop()
@@ -315,14 +360,18 @@ def _serve_bench(a) -> int:
         out = {
             "metric": _metric(a), "value": round(fps, 2), "unit": "frames/s", "n_gpus": world,
             "steps": s1 - s0, "warmup": a.warmup, "ms_per_step": round((t1 - t0) / max(1, s1 - s0) * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
+            "higher_is_better": True, "scaling": a.scaling, "vs_baseline": None, "dtype": a.dtype,
             "data": f"synthetic {a.camera} BGR frames, random-init weights",
             "config": {"model": _model_name(a), "global_batch": a.batch * world, "seq_len": a.input_size,
-                       "parallelism": f"dp{world}", "mode": "served (feeder + lagged pipeline + gRPC)",
+                       "parallelism": f"dp{world}",
+                       "mode": ("served, supervised workers (gRPC parent + per-GPU worker processes, "
+                                "shared-memory record rings)" if sup is not None else
+                                "served (feeder + lagged pipeline + gRPC)"),
                        "streams_per_gpu": a.streams},
             "p50_get_segmented_objects_ms": rpc.get("p50_ms") if rpc else None,
             "p99_get_segmented_objects_ms": rpc.get("p99_ms") if rpc else None,
         }
+        out.update(extra)
         print(json.dumps(out), flush=True)
     return 0
 

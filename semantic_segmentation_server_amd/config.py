@@ -72,7 +72,7 @@ class Config:
     debug_dump: Optional[str] = None       # directory for annotated PNG frames (reference :196-205)
     debug_every: int = 0                   # dump every N-th frame (0 = off)
     debug_sync: bool = False               # HIP_LAUNCH_BLOCKING=1, eager launches
-    supervise: bool = True                 # single-GPU CLI: GPU work in a supervised child process
+    supervise: bool = True                 # CLI: GPU work in supervised worker processes (one per GPU)
 
     @property
     def min_area(self) -> float:

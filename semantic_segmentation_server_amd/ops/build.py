@@ -95,10 +95,13 @@ def build_hip(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
         # profiles/r3_packed_f32_race.txt) -- the rare label-map mismatch of concurrent
         # plan copies (VERDICT r2 Weak #1)
         cflags += ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
+    # diagnostic builds (e.g. SSA_PACKED_F32=1 SSA_HIP_OUT=tools/bin/_hip_pk.so) go to their
+    # own object cache and output file; ops/native.py loads SSA_HIP_SO when it is set
+    out = os.environ.get("SSA_HIP_OUT", out)
     stamp = _stamp(hip_srcs + hdrs + [binding], cflags + [repr(sorted(EXTRA_FLAGS.items()))])
     if not force and _up_to_date(out, stamp):
         return out
-    bdir = os.path.join(ROOT, "build", "hip")
+    bdir = os.path.join(ROOT, "build", "hip" if out.startswith(HERE) else "hip_alt")
     os.makedirs(bdir, exist_ok=True)
     inc = [f"-I{p}" for p in _pybind_includes() + [os.path.join(CSRC, "hip")]]
 

@@ -25,6 +25,17 @@ def _load(name: str, builder):
     with _lock:
         if name in _mods:
             return _mods[name]
+        alt = os.environ.get("SSA_HIP_SO") if name == "_hip" else None
+        if alt:  # a diagnostic build of the same module (ops/build.py SSA_HIP_OUT)
+            import importlib.util
+            import sys
+            spec = importlib.util.spec_from_file_location(
+                f"semantic_segmentation_server_amd.ops.{name}", os.path.abspath(alt))
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            sys.modules[spec.name] = mod
+            _mods[name] = mod
+            return mod
         try:
             mod = importlib.import_module(f"semantic_segmentation_server_amd.ops.{name}")
         except ImportError:

@@ -91,6 +91,7 @@ def decisive_agreement(got: torch.Tensor, ref: torch.Tensor, k: float = 4.0) -> 
     mask = (top2[:, 0] - top2[:, 1]) > k * sigma
     frac = mask.float().mean().item()
     if not bool(mask.any()):
-        return 1.0, 0.0
+        # nothing decisive: no evidence either way (callers assert a minimum ``frac``)
+        return float("nan"), 0.0
     agree = (got.argmax(1) == ref.argmax(1))[mask].float().mean().item()
     return agree, frac

@@ -7,11 +7,13 @@ Every rank owns ``--streams`` frame sources (global stream id = launch rank * S 
 one engine on its GPU. Each rank's loop is the measured pipeline (``runtime/driver.py``):
 a feeder thread fills a ring of pinned batches, ``DataParallelPipeline`` (lag 1, bound
 per-slot hipGraphs, post-processing on its own stream) runs the step and gathers the
-packed records plus frame metadata to rank 0 over RCCL (``--gather host``: pinned host
-memory over gloo), which pushes them into the per-stream result hub behind the v1/v2
-services. With ``--ingest scatter`` rank 0 owns the sources for the whole node and
-scatters frames (RCCL) and their metadata (gloo) instead. The per-step heartbeat is a
-gloo all-reduce of a host flag.
+packed records plus frame metadata to rank 0 -- by default from pinned host memory over
+gloo (a latency-bound ~41 KB per rank and step that the host thread's slack absorbs;
+``--gather rccl``: one RCCL gather of a packed device row) -- which pushes them into the
+per-stream result hub behind the v1/v2 services. With ``--ingest scatter`` rank 0 owns
+the sources for the whole node and scatters frames over RCCL (xGMI) and their metadata
+over gloo instead. The per-step heartbeat is a gloo all-reduce of a host flag. (The CLI
+default for several GPUs is the supervised form, ``runtime/supervisor.py``.)
 
 Failure handling: every step starts with a tiny all-reduce carrying the
 stop flag; a source error is retried by the feeder (the rank keeps stepping). When a
@@ -70,6 +72,9 @@ class DistributedServer:
         self.gather = "host" if cfg.gather == "auto" else cfg.gather
         # SSA_SHARE_GPU=1 (several ranks on one GPU, a rehearsal): RCCL refuses that, gloo
         share = os.environ.get("SSA_SHARE_GPU", "0") == "1"
+        if share and cfg.ingest == "scatter":
+            log.warning("--ingest scatter needs RCCL, which SSA_SHARE_GPU=1 rules out: local ingest")
+            cfg.ingest = "local"
         pg = "nccl" if gpu and not share and (cfg.ingest == "scatter" or self.gather == "rccl") else "gloo"
         self.ctx = ctx or D.init(pg, timeout_s=cfg.rank_timeout,
                                  device="cuda" if torch.cuda.is_available() and cfg.device != "cpu"

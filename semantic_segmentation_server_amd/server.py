@@ -5,10 +5,12 @@ build the engine, load labels, probe the camera resolution, start the producer a
 a gRPC server on ``[::]:50051`` sharing one 10-thread pool, then block on the
 producer future.
 
-Here the producer runs on its own thread (and, with ``--gpus N`` under torchrun,
-on every rank; see ``parallel/serving.py``), the gRPC server has its own pool,
-both the v1 (reference-compatible) and v2 services are registered, and metrics are
-dumped at exit when ``--metrics_dump`` is given.
+Here the GPU pipeline runs in supervised worker processes, one per GPU (``--gpus N``;
+``runtime/supervisor.py``), while this process -- which never touches the GPU -- hosts
+the gRPC services and the result hub; ``--no_supervise`` runs it in-process (one GPU) or,
+under torchrun, as one rank per GPU with the RCCL data path (``parallel/serving.py``).
+The gRPC server has its own pool, both the v1 (reference-compatible) and v2 services are
+registered, and metrics are dumped at exit when ``--metrics_dump`` is given.
 """
 from __future__ import annotations
 
@@ -92,13 +94,16 @@ def main(argv=None) -> int:
     cfg = C.apply_debug_env(C.parse(argv))
     logging.basicConfig(level=getattr(logging, cfg.log_level.upper(), logging.INFO),
                         format="%(asctime)s %(levelname)s %(name)s: %(message)s")
-    if cfg.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 or (cfg.gpus > 1 and not cfg.supervise):
+        # torchrun launch (one process per GPU, rank 0 hosts gRPC): the RCCL data path
+        # with P-1 group re-form (parallel/serving.py)
         from .parallel.serving import serve_distributed
         return serve_distributed(cfg)
     print("Loading {} with {} labels.".format(cfg.model or f"random-init {cfg.arch}", cfg.labels))
     if cfg.supervise and not cfg.debug_dump:
-        # the GPU pipeline in a supervised child: a faulted worker is replaced by a fresh
-        # process while the parent keeps the gRPC services and the buffered results up
+        # the GPU pipeline in supervised children (one per GPU, --gpus N): a faulted or
+        # hung worker is replaced by a fresh process while the parent -- which never
+        # touches the GPU -- keeps the gRPC services and the buffered results up
         from .runtime.supervisor import SupervisedServer
         sup = SupervisedServer(cfg).start()
         stop = threading.Event()

@@ -53,6 +53,7 @@ class Metrics:
         self._lock = threading.Lock()
         self.counters: Dict[str, float] = defaultdict(float)
         self.hists: Dict[str, Reservoir] = {}
+        self.external: Dict[str, object] = {}  # entries forwarded from worker processes
         self.t_start = time.time()
 
     def inc(self, name: str, v: float = 1.0) -> None:
@@ -84,6 +85,7 @@ class Metrics:
             snap["fps"] = self.counters.get("frames", 0.0) / elapsed
             for k, h in self.hists.items():
                 snap[k] = h.summary()
+            snap.update(self.external)
         return snap
 
     def dump(self, path: str) -> None:

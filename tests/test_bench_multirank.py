@@ -25,8 +25,11 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,ingest", [(2, "local"), (3, "local"), (2, "scatter")])
-def test_bench_torchrun_cpu(world, ingest):
+@pytest.mark.parametrize("world,ingest,gb", [(2, "local", 0), (3, "local", 0), (2, "scatter", 0),
+                                              (2, "local", 4)])
+def test_bench_torchrun_cpu(world, ingest, gb):
+    """gb > 0: --global_batch (strong scaling, BASELINE config 3 as written): the node-wide
+    batch is split over the ranks."""
     steps, warmup, batch = 3, 1, 2
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1", SSA_NUMA_PIN="0",
                CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
@@ -34,7 +37,9 @@ def test_bench_torchrun_cpu(world, ingest):
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", str(steps),
            "--warmup", str(warmup), "--backend", "torch", "--input_size", "129",
-           "--batch", str(batch), "--rpc", "0", "--ingest", ingest]
+           "--rpc", "0", "--ingest", ingest] + (["--global_batch", str(gb)] if gb else ["--batch", str(batch)])
+    if gb:
+        batch = gb // world
     r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                        text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -45,6 +50,7 @@ def test_bench_torchrun_cpu(world, ingest):
     assert out["steps"] == steps and out["warmup"] == warmup
     assert out["config"]["global_batch"] == batch * world
     assert out["config"]["parallelism"] == f"dp{world}"
+    assert out["scaling"] == ("strong" if gb else "weak")
     assert out["value"] > 0 and out["ms_per_step"] > 0
     # every rank's frames reached rank 0, tagged with their own stream, ids in order
     assert out["frames_collected"] == steps * batch * world

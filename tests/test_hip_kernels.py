@@ -613,7 +613,9 @@ def test_hip_model_headline_shape_matches_torch(B):
     got = _nchw(dl.float()).cpu()
     e_hip, e_bf = _rel(got, ref_logits), _rel(bf_logits, ref_logits)
     print(f"headline shape B={B}: rel err hip={e_hip:.4f} torch-bf16={e_bf:.4f}")
-    assert e_hip < 1.5 * e_bf + 0.01, (e_hip, e_bf)
+    # no less accurate than stock PyTorch bf16 on the same GPU (the old
+    # 1.5x + 0.01 bound left 3.6x headroom), with an absolute ceiling
+    assert e_hip < 1.0 * e_bf + 0.005 and e_hip < 0.1, (e_hip, e_bf)
     ref_lab = R.upsample_argmax(ref_logits, S, S)
     hip_lab = R.upsample_argmax(got, S, S)
     bf_lab = R.upsample_argmax(bf_logits, S, S)
