@@ -184,15 +184,19 @@ PYBIND11_MODULE(_hip, m) {
   m.def("stem_band",
         [](uintptr_t frames, uintptr_t lx, uintptr_t ly, uintptr_t ws, uintptr_t bs, uintptr_t wd,
            uintptr_t bd, uintptr_t wp, uintptr_t bp, uintptr_t out, int B, int Hc, int Wc, int H,
-           int W, int SH, int SW, int R, int nbx, uintptr_t stream) {
+           int W, int SH, int SW, int R, int nbx, uintptr_t stream, int one_barrier) {
           StemBlock0Params p;
           p.frames = P<const uint8_t>(frames); p.lut_x = P<const int32_t>(lx); p.lut_y = P<const int32_t>(ly);
           p.ws = P<const bf16>(ws); p.bs = P<const float>(bs); p.wd = P<const void>(wd);
           p.bd = P<const void>(bd); p.wp = P<const void>(wp); p.bp = P<const float>(bp); p.out = P<bf16>(out);
           p.B = B; p.Hc = Hc; p.Wc = Wc; p.H = H; p.W = W; p.SH = SH; p.SW = SW; p.Cout = 16;
           p.TY = R;
-          stem_band(p, nbx, S(stream));
-        });
+          stem_band(p, nbx, S(stream), one_barrier != 0);
+        },
+        py::arg("frames"), py::arg("lx"), py::arg("ly"), py::arg("ws"), py::arg("bs"), py::arg("wd"),
+        py::arg("bd"), py::arg("wp"), py::arg("bp"), py::arg("out"), py::arg("B"), py::arg("Hc"),
+        py::arg("Wc"), py::arg("H"), py::arg("W"), py::arg("SH"), py::arg("SW"), py::arg("R"),
+        py::arg("nbx"), py::arg("stream"), py::arg("one_barrier") = 1);
   m.def("stem_band_lds", &stem_band_lds, py::arg("SW"), py::arg("nbx"), py::arg("R"));
 
   m.def("aspp_head",

@@ -176,7 +176,8 @@ struct StemBlock0Params {
 void stem_block0(const StemBlock0Params& p, hipStream_t s);
 // Row-streaming stem + block 0 (stem_band.hip): bands of p.TY output rows x ceil(SW / nbx)
 // columns; same weights as stem_block0 (p.TX unused).
-void stem_band(const StemBlock0Params& p, int nbx, hipStream_t s);
+// one_barrier: one workgroup barrier per stem row (double-buffered stem row), else two
+void stem_band(const StemBlock0Params& p, int nbx, hipStream_t s, bool one_barrier = true);
 size_t stem_band_lds(int SW, int nbx, int R);
 // LDS bytes the tile kernel needs for a (TY, TX) tile (0 if the shape is unsupported).
 size_t fused_ir_tile_lds(int CinP, int stride, int dil, int TY, int TX, int expand);

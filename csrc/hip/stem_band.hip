@@ -19,9 +19,14 @@
 //     the 3 output rows that row feeds (bias first, taps in ky-major order: the exact
 //     arithmetic of stem_block0_kernel), and a completed row goes straight from registers
 //     into the projection MFMA (lane = 8 channels of one pixel = its B fragment).
-// One step = one stem row, two barriers: [gather next rows | stem row -> S] A [depthwise,
-// projection, store] B. Weights live in VGPRs. Output: [B, 257, 257, 16] bf16 (block 1's
-// input). Reference parity: the Edge TPU model's first layers
+// One step = one stem row, ONE barrier: [gather next rows | stem row -> S[t & 1]] A
+// [depthwise, projection, store from S[t & 1]]. The stem row buffer is double-buffered, so
+// the next step's stem (other buffer) may start while a slower wave still runs this step's
+// depthwise -- the round-4 form had a second barrier per step for that (86 barriers per
+// band of 41 rows, each a full drain of a latency-bound 4-wave workgroup). Ring-row reuse
+// with one barrier: step t writes input rows 2t+3, 2t+4 and reads 2t .. 2t+2 (6-row ring);
+// the rows step t+1 overwrites (2t-1, 2t) were last read by stem t-1, before barrier t-1.
+// Weights live in VGPRs. Output: [B, 257, 257, 16] bf16 (block 1's input). Reference parity: the Edge TPU model's first layers
 // (/root/reference/sem_seg_server.py:151-162: BGR->RGB, NEAREST letterbox, quantised input).
 #include "common.h"
 #include "kernels.h"
@@ -52,7 +57,7 @@ constexpr int kSP = 80;  // stem-row entry pitch (B): 32 fp16 + 16 B pad (odd mu
 
 // NW waves = column groups of 16 stem columns (the band's TW + 2 stem columns);
 // GPX input pixels per lane per gathered row pair
-template <int NW, int GPX>
+template <int NW, int GPX, bool ONEB>
 __global__ __launch_bounds__(64 * NW) void stem_band_kernel(StemBandArgs a) {
   constexpr int NT = 64 * NW;
   constexpr int U = 3;   // step unroll: static D-slot / ring / prefetch roles
@@ -76,11 +81,12 @@ __global__ __launch_bounds__(64 * NW) void stem_band_kernel(StemBandArgs a) {
   const int n_st = y1 - y0 + 2;       // stem rows y0 - 1 .. y1
   const int n_rows = 2 * n_st + 1;    // input rows the band reads
 
-  // LDS: [IN ring 6 rows][NIC][8 B] | [S row NSC x 80 B] | [lut_y of the band's rows]
+  // LDS: [IN ring 6 rows][NIC][8 B] | [S rows 2 x NSC x 80 B] | [lut_y of the band's rows]
   bf16* IN = reinterpret_cast<bf16*>(smem);
   const int in_row = NIC * 4;  // elements per ring row
-  char* S = smem + (size_t)6 * NIC * 8;
-  int* sly = reinterpret_cast<int*>(S + (size_t)NSC * kSP);
+  char* S2 = smem + (size_t)6 * NIC * 8;
+  const int s_bytes = NSC * kSP;
+  int* sly = reinterpret_cast<int*>(S2 + (size_t)2 * s_bytes);
   for (int i = tid; i < n_rows; i += NT) {
     const int r = rbase + i;
     sly[i] = (r >= 0 && r < a.H) ? a.lut_y[r] : -2;  // -2: outside the model input (conv zero pad)
@@ -203,7 +209,8 @@ __global__ __launch_bounds__(64 * NW) void stem_band_kernel(StemBandArgs a) {
 #pragma unroll
         for (int u = 0; u < GPX; ++u) xr[sl][u] = fetch_px(2 * (t + 1 + PD) + 1 + gk[u], u);
       }
-      // ---- [stem] row s from ring rows 2t .. 2t + 2 -> S (fp16, relu6; 0 outside)
+      // ---- [stem] row s from ring rows 2t .. 2t + 2 -> S[t & 1] (fp16, relu6; 0 outside)
+      char* S = S2 + (t & 1) * s_bytes;
       const bool srow = s >= 0 && s < a.SH && t < n_st;  // uniform
       {
         s16x4 xf[3];
@@ -249,21 +256,21 @@ __global__ __launch_bounds__(64 * NW) void stem_band_kernel(StemBandArgs a) {
         }
         D[s2] = bdv;  // slot reopens as output s + 2 (bias first, as stem_block0_kernel)
       }
-      lds_barrier();  // B: S and this step's IN rows free / visible
+      if (!ONEB) lds_barrier();  // two-barrier form (round 4): B, S and IN rows free / visible
     }
   }
 }
 
-template <int NW, int GPX>
+template <int NW, int GPX, bool ONEB>
 void launch_stem_band(const StemBandArgs& a, size_t lds, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_band_kernel<NW, GPX>),
+    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_band_kernel<NW, GPX, ONEB>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
           "stem_band attr");
     attr = true;
   }
-  hipLaunchKernelGGL((stem_band_kernel<NW, GPX>), dim3(a.B * a.nby * a.nbx), dim3(64 * NW), lds, st, a);
+  hipLaunchKernelGGL((stem_band_kernel<NW, GPX, ONEB>), dim3(a.B * a.nby * a.nbx), dim3(64 * NW), lds, st, a);
   check_launch("stem_band");
 }
 
@@ -272,10 +279,10 @@ void launch_stem_band(const StemBandArgs& a, size_t lds, hipStream_t st) {
 size_t stem_band_lds(int SW, int nbx, int R) {
   const int TW = cdiv(SW, nbx);
   const int NSC = TW + 2, NIC = 2 * NSC + 1;
-  return (size_t)6 * NIC * 8 + (size_t)NSC * kSP + (size_t)(2 * (R + 2) + 1) * 4;
+  return (size_t)6 * NIC * 8 + (size_t)2 * NSC * kSP + (size_t)(2 * (R + 2) + 1) * 4;
 }
 
-void stem_band(const StemBlock0Params& p, int nbx, hipStream_t st) {
+void stem_band(const StemBlock0Params& p, int nbx, hipStream_t st, bool one_barrier) {
   if (p.Cout != 16) throw std::invalid_argument("stem_band: block 0 must project to 16 channels");
   if (p.SH != (p.H - 1) / 2 + 1 || p.SW != (p.W - 1) / 2 + 1) throw std::invalid_argument("stem_band: bad stem size");
   if (nbx < 1 || p.TY < 1) throw std::invalid_argument("stem_band: bad bands");
@@ -288,10 +295,11 @@ void stem_band(const StemBlock0Params& p, int nbx, hipStream_t st) {
   StemBandArgs a{p.frames, p.lut_x, p.lut_y, p.ws, p.bs, reinterpret_cast<const f16*>(p.wd),
                  reinterpret_cast<const f16*>(p.bd), reinterpret_cast<const f16*>(p.wp), p.bp, p.out,
                  p.B, p.Hc, p.Wc, p.H, p.W, p.SH, p.SW, p.TY, nbx, cdiv(p.SH, p.TY), TW};
-#define SB(NW_, G_)                                \
-  if (NW == NW_ && GPX == G_) {                    \
-    launch_stem_band<NW_, G_>(a, lds, st);         \
-    return;                                        \
+#define SB(NW_, G_)                                                   \
+  if (NW == NW_ && GPX == G_) {                                       \
+    if (one_barrier) launch_stem_band<NW_, G_, true>(a, lds, st);     \
+    else launch_stem_band<NW_, G_, false>(a, lds, st);                \
+    return;                                                           \
   }
   // 2 x NIC = 4 (TW + 2) + 2 <= 64 NW + 2: at most 2 gathered pixels per lane
   SB(1, 1) SB(2, 1) SB(3, 1) SB(4, 1) SB(5, 1) SB(6, 1) SB(7, 1) SB(8, 1)

@@ -346,15 +346,21 @@ class HipDeepLab:
                     # row-streaming bands: every input pixel gathered once, every stem pixel
                     # computed once (stem_band.hip); bit-identical to the tile kernel
                     SH = OH
+                    # band heights: grids of ~1-4 workgroups per CU, plus the heights whose
+                    # band count fills whole residency rounds (~3 of these 4-wave workgroups
+                    # fit a CU: a grid of 1.46 rounds pays a half-empty second round)
                     for nbx in (3, 4, 5):
-                        for target in (256, 512, 1024):
-                            R = max(2, -(-B * nbx * SH // target))
-                            tag = f"stem_band{R}x{nbx}"
-                            if any(t == tag for t, _ in fused):
-                                continue
-                            fused.insert(0, (tag, [
-                                lambda frames, lx, ly, out0=out0, R=R, nbx=nbx, sbp=sbp: K.stem_band(
-                                    frames, lx, ly, sbp, out0, H=H, W=W, R=R, nbx=nbx)]))
+                        Rs = [max(2, -(-B * nbx * SH // target)) for target in (256, 512, 1024)]
+                        Rs += [max(2, -(-SH // nby)) for nby in range(2, 13)
+                               if B * nbx * nby in range(640, 800) or B * nbx * nby in range(1400, 1560)]
+                        for R in dict.fromkeys(Rs):
+                            for oneb in (True, False):
+                                tag = f"stem_band{R}x{nbx}" + ("" if oneb else "b2")
+                                if any(t == tag for t, _ in fused):
+                                    continue
+                                fused.insert(0, (tag, [
+                                    lambda frames, lx, ly, out0=out0, R=R, nbx=nbx, sbp=sbp, oneb=oneb: K.stem_band(
+                                        frames, lx, ly, sbp, out0, H=H, W=W, R=R, nbx=nbx, one_barrier=oneb)]))
                     sep = ("separate", [ops[stem_at], ops[stem_at + 1]])
                     ops[stem_at:stem_at + 2] = [Choice("stem+block0", fused + [sep])]
         # ---- ASPP

@@ -664,9 +664,11 @@ def stem_block0(frames, lut_x, lut_y, packed: dict, out, *, H, W, tile=(8, 16)):
     return out
 
 
-def stem_band(frames, lut_x, lut_y, packed: dict, out, *, H, W, R=16, nbx=3):
+def stem_band(frames, lut_x, lut_y, packed: dict, out, *, H, W, R=16, nbx=3, one_barrier=True):
     """Row-streaming stem + block 0 (csrc/hip/stem_band.hip): bands of R output rows x
-    ceil(SW / nbx) columns; same weights and bit-identical results as ``stem_block0``."""
+    ceil(SW / nbx) columns; same weights and bit-identical results as ``stem_block0``.
+    ``one_barrier``: one workgroup barrier per stem row (double-buffered stem row; False:
+    the round-4 two-barrier step)."""
     B, Hc, Wc, _ = frames.shape
     SH, SW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
     TW = -(-SW // nbx)
@@ -682,7 +684,7 @@ def stem_band(frames, lut_x, lut_y, packed: dict, out, *, H, W, R=16, nbx=3):
     P = packed
     _hip_mod().stem_band(_ptr(frames), _ptr(lut_x), _ptr(lut_y), _ptr(P["ws"]), _ptr(P["bs"]),
                          _ptr(P["wd_h"]), _ptr(P["bd_h"]), _ptr(P["wp_h"]), _ptr(P["bp"]),
-                         _ptr(out), B, Hc, Wc, H, W, SH, SW, R, nbx, _stream())
+                         _ptr(out), B, Hc, Wc, H, W, SH, SW, R, nbx, _stream(), int(bool(one_barrier)))
     _dbg("stem_band")
     return out
 

@@ -10,7 +10,9 @@ reference path explicitly).
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
+import sys
 import threading
 
 _lock = threading.Lock()
@@ -27,8 +29,6 @@ def _load(name: str, builder):
             return _mods[name]
         alt = os.environ.get("SSA_HIP_SO") if name == "_hip" else None
         if alt:  # a diagnostic build of the same module (ops/build.py SSA_HIP_OUT)
-            import importlib.util
-            import sys
             spec = importlib.util.spec_from_file_location(
                 f"semantic_segmentation_server_amd.ops.{name}", os.path.abspath(alt))
             mod = importlib.util.module_from_spec(spec)

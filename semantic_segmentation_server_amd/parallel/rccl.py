@@ -1,0 +1,158 @@
+"""Raw RCCL communicators whose collectives run on the caller's HIP stream.
+
+Why not ``torch.distributed`` for the data path: ProcessGroupNCCL runs every collective
+on ONE internal stream per device and fences it against the issuing stream with events.
+The serving pipeline keeps three steps in flight on three slot streams (plus a result
+stream) and HIP maps a process's streams onto 4 hardware queues. Round 4 measured what
+that costs at world size 1 (profiles/r4_rccl_gather_ab.txt): the record gather -10 %,
+the frame scatter -25 %, for ~9 us of actual GPU work per step -- the collectives of all
+three slots funnel through the one internal stream (each slot's scatter waits behind the
+previous slot's gather, which waits for that slot's post-processing), and the lazily
+created internal stream lands on a hardware queue that one of the slot streams already
+uses, so it also queues behind that slot's model kernels.
+
+Here each pipeline slot owns a communicator of its own (``ncclCommInitRank`` over the
+same ranks; the unique ids travel over the gloo control group) and every collective is
+enqueued directly on the slot's stream with ``ncclScatter`` / ``ncclGather``: ordered
+after the upload and before the model on that stream, no extra stream, no cross-slot
+dependency. The library is the librccl the torch build links (one RCCL per process).
+
+Reference: the reference has no multi-device code at all; this is the
+north-star X1/X2 path over xGMI.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional
+
+import torch
+
+_lib = None
+
+_DT = {torch.float32: 7, torch.uint8: 1, torch.int32: 2, torch.float64: 8, torch.bfloat16: 9,
+       torch.float16: 6, torch.int8: 0, torch.int64: 4}
+
+
+class RcclError(RuntimeError):
+    pass
+
+
+class _UniqueId(ctypes.Structure):
+    _fields_ = [("internal", ctypes.c_char * 128)]
+
+
+def lib():
+    """The RCCL library torch itself uses (already mapped by libtorch_hip)."""
+    global _lib
+    if _lib is None:
+        cands = [os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"),
+                 "librccl.so.1", "/opt/rocm/lib/librccl.so.1"]
+        err = None
+        for c in cands:
+            try:
+                if c.startswith("/") and not os.path.exists(c):
+                    continue
+                L = ctypes.CDLL(c)
+                break
+            except OSError as e:  # pragma: no cover - image without RCCL
+                err = e
+        else:
+            raise RcclError(f"librccl not found: {err}")
+        L.ncclGetErrorString.restype = ctypes.c_char_p
+        L.ncclGetUniqueId.argtypes = [ctypes.POINTER(_UniqueId)]
+        L.ncclCommInitRank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, _UniqueId, ctypes.c_int]
+        for fn in ("ncclScatter", "ncclGather"):
+            getattr(L, fn).argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.ncclCommDestroy.argtypes = [ctypes.c_void_p]
+        L.ncclCommAbort.argtypes = [ctypes.c_void_p]
+        L.ncclCommGetAsyncError.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+        _lib = L
+    return _lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RcclError(f"{what}: {lib().ncclGetErrorString(rc).decode()} ({rc})")
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except RcclError:
+        return False
+
+
+class StreamComm:
+    """One RCCL communicator over the ranks of ``ctx``; collectives on a given stream."""
+
+    def __init__(self, ctx, tag: str = "slot"):
+        import torch.distributed as dist
+        L = lib()
+        uid = _UniqueId()
+        if ctx.rank == 0:
+            _check(L.ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
+        if ctx.world > 1:
+            obj = [bytes(uid.internal) if ctx.rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0, group=ctx.cpu_group)
+            uid.internal = obj[0]
+        self.world, self.rank = ctx.world, ctx.rank
+        self.device = ctx.device
+        self.comm = ctypes.c_void_p()
+        with torch.cuda.device(ctx.device):
+            _check(L.ncclCommInitRank(ctypes.byref(self.comm), ctx.world, uid, ctx.rank),
+                   f"ncclCommInitRank({tag})")
+        self.alive = True
+
+    @staticmethod
+    def _stream(stream: Optional[torch.cuda.Stream]) -> ctypes.c_void_p:
+        s = stream if stream is not None else torch.cuda.current_stream()
+        return ctypes.c_void_p(s.cuda_stream)
+
+    def scatter(self, recv: torch.Tensor, send: Optional[torch.Tensor], root: int = 0,
+                stream: Optional[torch.cuda.Stream] = None) -> None:
+        """recv [n] on every rank <- rows of send [world, n] on ``root`` (contiguous)."""
+        if recv.dtype not in _DT or not recv.is_contiguous():
+            raise ValueError("scatter: contiguous tensor of a supported dtype")
+        if self.rank == root and (send is None or send.numel() != recv.numel() * self.world
+                                  or send.dtype != recv.dtype or not send.is_contiguous()):
+            raise ValueError("scatter: root needs a contiguous [world, n] send buffer")
+        sp = send.data_ptr() if self.rank == root else 0
+        _check(lib().ncclScatter(ctypes.c_void_p(sp), ctypes.c_void_p(recv.data_ptr()), recv.numel(),
+                                 _DT[recv.dtype], root, self.comm, self._stream(stream)), "ncclScatter")
+
+    def gather(self, send: torch.Tensor, recv: Optional[torch.Tensor], root: int = 0,
+               stream: Optional[torch.cuda.Stream] = None) -> None:
+        """recv [world, n] on ``root`` <- send [n] of every rank (contiguous)."""
+        if send.dtype not in _DT or not send.is_contiguous():
+            raise ValueError("gather: contiguous tensor of a supported dtype")
+        if self.rank == root and (recv is None or recv.numel() != send.numel() * self.world
+                                  or recv.dtype != send.dtype or not recv.is_contiguous()):
+            raise ValueError("gather: root needs a contiguous [world, n] receive buffer")
+        rp = recv.data_ptr() if self.rank == root else 0
+        _check(lib().ncclGather(ctypes.c_void_p(send.data_ptr()), ctypes.c_void_p(rp), send.numel(),
+                                _DT[send.dtype], root, self.comm, self._stream(stream)), "ncclGather")
+
+    def async_error(self) -> int:
+        err = ctypes.c_int(0)
+        lib().ncclCommGetAsyncError(self.comm, ctypes.byref(err))
+        return int(err.value)
+
+    def abort(self) -> None:
+        """A peer is gone: free the communicator without waiting for it."""
+        if self.alive:
+            self.alive = False
+            lib().ncclCommAbort(self.comm)
+
+    def destroy(self) -> None:
+        if self.alive:
+            self.alive = False
+            lib().ncclCommDestroy(self.comm)
+
+
+def slot_comms(ctx, n: int) -> List[StreamComm]:
+    """``n`` communicators over ``ctx``'s ranks (one per pipeline slot), created in the
+    same order on every rank."""
+    return [StreamComm(ctx, f"slot{i}") for i in range(n)]

@@ -158,6 +158,11 @@ class DistributedServer:
                   self.ctx.orig_rank, err)
         self.metrics.inc("degrade_events")
         t0 = time.perf_counter()
+        if self.driver is not None:
+            try:
+                self.driver.pipe.close(abort=True)  # its RCCL communicators include the lost peer
+            except Exception:
+                log.exception("closing the old pipeline's communicators")
         new = D.reform(self.run_ctx, timeout_s=self.cfg.rank_timeout)
         log.info("re-formed the group in %.2f s", time.perf_counter() - t0)
         self.degraded = True

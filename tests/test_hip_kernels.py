@@ -1055,11 +1055,12 @@ def test_stem_band(cam, H, R, nbx):
     fd = frames.to(DEV)
     want = torch.full((2, SH, SH, 16), float("nan"), dtype=torch.bfloat16, device=DEV)
     K.stem_block0(fd, lxd, lyd, P, want, H=H, W=H, tile=(8, 16))
-    out = torch.full((2, SH, SH, 16), float("nan"), dtype=torch.bfloat16, device=DEV)
-    K.stem_band(fd, lxd, lyd, P, out, H=H, W=H, R=R, nbx=nbx)
-    torch.cuda.synchronize()
-    assert torch.isfinite(out).all()
-    assert torch.equal(out, want), (out.float() - want.float()).abs().max().item()
+    for oneb in (True, False):  # one barrier per stem row (double-buffered row) / two
+        out = torch.full((2, SH, SH, 16), float("nan"), dtype=torch.bfloat16, device=DEV)
+        K.stem_band(fd, lxd, lyd, P, out, H=H, W=H, R=R, nbx=nbx, one_barrier=oneb)
+        torch.cuda.synchronize()
+        assert torch.isfinite(out).all(), oneb
+        assert torch.equal(out, want), (oneb, (out.float() - want.float()).abs().max().item())
     if H <= 129:
         x = R_.preprocess(frames, torch.from_numpy(np.array(lx)), torch.from_numpy(np.array(ly)))
         with torch.no_grad():
