@@ -151,20 +151,20 @@ PYBIND11_MODULE(_hip, m) {
   m.def("fused_ir_slice",
         [](uintptr_t in, uintptr_t blob, uintptr_t out, int B, int IH, int IW, int Cin, int OH, int OW,
            int Cout, int hidP, int stride, int residual, int R, int o_be, int o_wd, int o_bd, int o_wp,
-           int o_bp, int nw, uintptr_t stream) {
+           int o_bp, int nw, uintptr_t stream, int one_barrier) {
           FusedBandParams p;
           p.in = P<const bf16>(in); p.blob = P<const void>(blob); p.out = P<bf16>(out);
           p.B = B; p.IH = IH; p.IW = IW; p.Cin = Cin; p.OH = OH; p.OW = OW; p.Cout = Cout;
           p.hidP = hidP; p.stride = stride; p.residual = residual; p.R = R;
           p.o_be = o_be; p.o_wd = o_wd; p.o_bd = o_bd; p.o_wp = o_wp; p.o_bp = o_bp;
-          fused_ir_slice(p, nw, S(stream));
+          fused_ir_slice(p, nw, S(stream), one_barrier != 0);
         },
         py::arg("in"), py::arg("blob"), py::arg("out"), py::arg("B"), py::arg("IH"), py::arg("IW"),
         py::arg("Cin"), py::arg("OH"), py::arg("OW"), py::arg("Cout"), py::arg("hidP"), py::arg("stride"),
         py::arg("residual"), py::arg("R"), py::arg("o_be"), py::arg("o_wd"), py::arg("o_bd"),
-        py::arg("o_wp"), py::arg("o_bp"), py::arg("nw"), py::arg("stream"));
+        py::arg("o_wp"), py::arg("o_bp"), py::arg("nw"), py::arg("stream"), py::arg("one_barrier") = 0);
   m.def("fused_ir_slice_lds", &fused_ir_slice_lds, py::arg("stride"), py::arg("hidP"), py::arg("OW"),
-        py::arg("Cout"), py::arg("nw"));
+        py::arg("Cout"), py::arg("nw"), py::arg("one_barrier") = false);
   m.def("fused_ir_band_lds", &fused_ir_band_lds, py::arg("stride"), py::arg("hidP"), py::arg("OW"),
         py::arg("blob_bytes"), py::arg("nslot"), py::arg("hs") = 1, py::arg("Cout") = 0,
         py::arg("split") = 1);

@@ -28,7 +28,10 @@
 //   [expand row t -> E] [projection of the row completed at step t-1]  | A |
 //   [depthwise of row t -> open output rows; completed row -> D-buffer] | B |
 // E and the D-buffer are single-buffered: each is written and read on opposite sides of
-// a barrier. Weight blob: pack_fused_band's (relu6 scale folded: both clamps are [0, 1]).
+// a barrier. ONEB (round 5): E and the D-buffer double-buffered by step parity and the
+// projection of a completed row deferred by two steps, so ONE barrier per input row is
+// enough (E[t&1]: written before barrier t, read after it, rewritten before barrier t+2;
+// D[t&1]: written after barrier t, projected before barrier t+2, rewritten after it). Weight blob: pack_fused_band's (relu6 scale folded: both clamps are [0, 1]).
 // Reference parity: the model executed is the reference's Edge TPU DeepLabv3-MobileNetV2
 // (/root/reference/sem_seg_server.py:238,162).
 #include "common.h"
@@ -60,7 +63,7 @@ __device__ __forceinline__ void lds_barrier() {
 
 // S: stride; NCH: hidden chunks of 32; NS: output subtiles of 16; NW: column groups;
 // PD: input rows prefetched ahead (U = the step unroll that keeps slot roles static)
-template <int S, int NCH, int NS, int NW>
+template <int S, int NCH, int NS, int NW, bool ONEB>
 __global__ __launch_bounds__(64 * NW * NCH) void fused_ir_slice_kernel(SliceArgs a) {
   constexpr int NT = 64 * NW * NCH;
   constexpr int NDS = S == 1 ? 3 : 2;     // open output rows
@@ -84,11 +87,13 @@ __global__ __launch_bounds__(64 * NW * NCH) void fused_ir_slice_kernel(SliceArgs
   const int iwv = (twv - 1) * S + 3;
   const int ixb = x0 * S - 1;
 
-  // ---- LDS: [Wp frags NS*NCH KiB][bp NS*16 f32][E row][D-buffer NW*NCH KiB]
+  // ---- LDS: [Wp frags NS*NCH KiB][bp NS*16 f32][E row(s)][D-buffer(s) NW*NCH KiB]
+  constexpr int NB = ONEB ? 2 : 1;
   char* sWp = smem;
   float* sBp = reinterpret_cast<float*>(smem + NS * NCH * 1024);
-  char* sE = smem + NS * NCH * 1024 + NS * 64;
-  char* sD = sE + a.EROW;
+  char* sE0 = smem + NS * NCH * 1024 + NS * 64;
+  char* sD0 = sE0 + NB * a.EROW;
+  constexpr int DB = NW * NCH * 1024;
   for (int i = tid; i < NS * NCH * 64; i += NT)
     *reinterpret_cast<i32x4*>(sWp + i * 16) = *reinterpret_cast<const i32x4*>(a.blob + a.o_wp + i * 16);
   for (int i = tid; i < NS * 16; i += NT) sBp[i] = reinterpret_cast<const float*>(a.blob + a.o_bp)[i];
@@ -137,7 +142,9 @@ __global__ __launch_bounds__(64 * NW * NCH) void fused_ir_slice_kernel(SliceArgs
     const int gc = ixb + i;
     if (g == 0 && (gc < 0 || gc >= a.IW)) {
       const int e = S == 1 ? i : ((i & 1) ? a.HE + (i >> 1) : (i >> 1));
-      *reinterpret_cast<i32x4*>(sE + e * a.P + (c * 32 + c8 * 8) * 2) = i32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+        *reinterpret_cast<i32x4*>(sE0 + nb * a.EROW + e * a.P + (c * 32 + c8 * 8) * 2) = i32x4{0, 0, 0, 0};
     }
   }
   __syncthreads();  // (the only full barrier: no global store is pending yet)
@@ -161,8 +168,9 @@ __global__ __launch_bounds__(64 * NW * NCH) void fused_ir_slice_kernel(SliceArgs
   const f16x8 h0 = {0, 0, 0, 0, 0, 0, 0, 0}, h1 = {1, 1, 1, 1, 1, 1, 1, 1};
   const bool task = c < NS;  // wave (g, n = c) projects output channels n*16..+15
   int pend_o = -1;           // output row waiting in the D-buffer (uniform)
+  int pend2[2] = {-1, -1};   // ONEB: output row waiting in D-buffer [parity] (uniform)
 
-  auto project = [&](int o) {  // the D-buffer holds output row o's depthwise (all chunks)
+  auto project = [&](int o, const char* sD) {  // sD holds output row o's depthwise (all chunks)
     if (!task) return;
     f32x4 acc = *reinterpret_cast<const f32x4*>(sBp + c * 16 + kq * 4);
 #pragma unroll
@@ -195,6 +203,8 @@ __global__ __launch_bounds__(64 * NW * NCH) void fused_ir_slice_kernel(SliceArgs
       const int iy = iy0 + t;
       const bool rowin = iy >= 0 && iy < a.IH;  // uniform
       const int slot = ph % PD;
+      char* sE = sE0 + (ONEB ? (t & 1) * a.EROW : 0);
+      char* sD = sD0 + (ONEB ? (t & 1) * DB : 0);
       // ---- [expand] input row iy -> E (this wave's 32 hidden channels)
       if (rowin) {
 #pragma unroll
@@ -208,9 +218,15 @@ __global__ __launch_bounds__(64 * NW * NCH) void fused_ir_slice_kernel(SliceArgs
           }
       }
       load_x(iy + PD, xq[slot]);  // in flight under the next PD steps
-      // ---- [project] the row the previous step completed (D-buffer read before barrier A)
-      if (pend_o >= 0) {
-        project(pend_o);
+      // ---- [project] the row the previous step completed (D-buffer read before barrier A);
+      // ONEB: the row completed two steps ago, in D-buffer [t & 1]
+      if (ONEB) {
+        if (pend2[t & 1] >= 0) {
+          project(pend2[t & 1], sD);
+          pend2[t & 1] = -1;
+        }
+      } else if (pend_o >= 0) {
+        project(pend_o, sD);
         pend_o = -1;
       }
       lds_barrier();  // A: E row complete; D-buffer free
@@ -253,26 +269,38 @@ __global__ __launch_bounds__(64 * NW * NCH) void fused_ir_slice_kernel(SliceArgs
           d = __builtin_elementwise_min(__builtin_elementwise_max(d, h0), h1);
           D[sc] = h0;
           *reinterpret_cast<f16x8*>(sD + ((g * NCH + c) * 64 + lane) * 16) = d;
-          pend_o = o;
+          if (ONEB) pend2[t & 1] = o;
+          else pend_o = o;
         }
       }
-      lds_barrier();  // B: depthwise reads of E done; D-buffer complete
+      if (!ONEB) lds_barrier();  // B: depthwise reads of E done; D-buffer complete
     }
   }
-  if (pend_o >= 0) project(pend_o);
+  if (ONEB) {
+    lds_barrier();  // the last steps' D-buffer rows complete
+    // in completion order: the older row first (steps n_in-2, n_in-1 by parity)
+    const int tl = (n_in + U - 1) / U * U;  // steps run (the unrolled loop rounds up)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int par = (tl + k) & 1;
+      if (pend2[par] >= 0) project(pend2[par], sD0 + par * DB);
+    }
+  } else if (pend_o >= 0) {
+    project(pend_o, sD0);
+  }
 }
 
-template <int S, int NCH, int NS, int NW>
+template <int S, int NCH, int NS, int NW, bool ONEB>
 void launch_slice(const SliceArgs& a, size_t lds, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_ir_slice_kernel<S, NCH, NS, NW>),
+    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_ir_slice_kernel<S, NCH, NS, NW, ONEB>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
           "fused_ir_slice attr");
     attr = true;
   }
-  hipLaunchKernelGGL((fused_ir_slice_kernel<S, NCH, NS, NW>), dim3(a.B * a.nby * a.nbx), dim3(64 * NW * NCH),
-                     lds, st, a);
+  hipLaunchKernelGGL((fused_ir_slice_kernel<S, NCH, NS, NW, ONEB>), dim3(a.B * a.nby * a.nbx),
+                     dim3(64 * NW * NCH), lds, st, a);
   check_launch("fused_ir_slice");
 }
 
@@ -303,30 +331,31 @@ SliceGeom slice_geom(int stride, int hidP, int OW, int nw) {
 
 }  // namespace
 
-size_t fused_ir_slice_lds(int stride, int hidP, int OW, int Cout, int nw) {
-  const int NCH = hidP / 32, NS = (Cout + 15) / 16;
+size_t fused_ir_slice_lds(int stride, int hidP, int OW, int Cout, int nw, bool one_barrier) {
+  const int NCH = hidP / 32, NS = (Cout + 15) / 16, NB = one_barrier ? 2 : 1;
   const SliceGeom g = slice_geom(stride, hidP, OW, nw);
-  return (size_t)NS * NCH * 1024 + NS * 64 + g.EROW + (size_t)nw * NCH * 1024;
+  return (size_t)NS * NCH * 1024 + NS * 64 + NB * ((size_t)g.EROW + (size_t)nw * NCH * 1024);
 }
 
-void fused_ir_slice(const FusedBandParams& p, int nw, hipStream_t st) {
+void fused_ir_slice(const FusedBandParams& p, int nw, hipStream_t st, bool one_barrier) {
   if (p.stride != 1 && p.stride != 2) throw std::invalid_argument("fused_ir_slice: stride 1 or 2");
   if (p.Cin > 32 || p.Cin % 8 || p.hidP % 32 || p.R < 1) throw std::invalid_argument("fused_ir_slice: Cin <= 32, hidP % 32");
   if (p.residual && (p.stride != 1 || p.Cin != p.Cout)) throw std::invalid_argument("fused_ir_slice: bad residual");
   if (p.OH != (p.IH - 1) / p.stride + 1 || p.OW != (p.IW - 1) / p.stride + 1)
     throw std::invalid_argument("fused_ir_slice: output size must be the pad-1 3x3 conv's");
   const SliceGeom g = slice_geom(p.stride, p.hidP, p.OW, nw);
-  const size_t lds = fused_ir_slice_lds(p.stride, p.hidP, p.OW, p.Cout, nw);
+  const size_t lds = fused_ir_slice_lds(p.stride, p.hidP, p.OW, p.Cout, nw, one_barrier);
   if (lds > 160 * 1024) throw std::invalid_argument("fused_ir_slice: LDS over 160 KiB");
   if ((g.TW - 1) * p.stride + 3 > 16 * nw * p.stride) throw std::invalid_argument("fused_ir_slice: band too wide");
   SliceArgs a{p.in, reinterpret_cast<const char*>(p.blob), p.out, p.B, p.IH, p.IW, p.Cin, p.OH, p.OW, p.Cout,
               p.residual, p.R, g.nbx, cdiv(p.OH, p.R), g.TW, g.HE, g.P, g.EROW, p.hidP,
               p.o_be, p.o_wd, p.o_bd, p.o_wp, p.o_bp};
   const int NCH = p.hidP / 32, NS = (p.Cout + 15) / 16;
-#define SLICE(S_, NCH_, NS_, NW_)                                 \
-  if (p.stride == S_ && NCH == NCH_ && NS == NS_ && nw == NW_) {  \
-    launch_slice<S_, NCH_, NS_, NW_>(a, lds, st);                 \
-    return;                                                       \
+#define SLICE(S_, NCH_, NS_, NW_)                                                  \
+  if (p.stride == S_ && NCH == NCH_ && NS == NS_ && nw == NW_) {                   \
+    if (one_barrier) launch_slice<S_, NCH_, NS_, NW_, true>(a, lds, st);           \
+    else launch_slice<S_, NCH_, NS_, NW_, false>(a, lds, st);                      \
+    return;                                                                        \
   }
   // block 1 (16 -> 96 -> 24, s2), 2 (24 -> 144 -> 24; hidden padded to 160), 3 (24 -> 144 -> 32,
   // s2), 4-5 (32 -> 192 -> 32), 6 (32 -> 192 -> 64, s2); waves = NW x NCH <= 16

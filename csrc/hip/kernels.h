@@ -161,8 +161,9 @@ int fused_ir_band_cols(int stride);
 // Hidden-sliced variant (fused_ir_slice.hip): waves = nw column groups x hidP/32 hidden
 // chunks, each wave's chunk weights in VGPRs; same blob as fused_ir_band (hs / split /
 // nslot / blob_bytes unused).
-void fused_ir_slice(const FusedBandParams& p, int nw, hipStream_t s);
-size_t fused_ir_slice_lds(int stride, int hidP, int OW, int Cout, int nw);
+// one_barrier: one workgroup barrier per input row (double-buffered E / D rows), else two
+void fused_ir_slice(const FusedBandParams& p, int nw, hipStream_t s, bool one_barrier = false);
+size_t fused_ir_slice_lds(int stride, int hidP, int OW, int Cout, int nw, bool one_barrier = false);
 // Fused stem (3x3 s2, 3 -> 32, relu6, letterbox gather) + MobileNetV2 block 0
 // (dw 3x3 on 32 ch + relu6, project 32 -> 16); weights: ws [32][32] bf16 with
 // K = (ky*3+kx)*3 + c (RGB), bs [32] f32, wd [9][32] f16, bd [32] f16, wp [16][32] f16, bp [16].

@@ -748,15 +748,16 @@ class HipDeepLab:
                 if "band" not in blk:
                     blk["band"] = self._pack_band(blk, s)
                 bp_ = blk["band"]
-                if FB.slice_lds(bp_, s.stride, OW, nw) > 160 * 1024:
-                    continue
                 twmax = 16 * nw - (2 if s.stride == 1 else 1)
                 nbx = -(-OW // twmax)
-                for R in self._slice_rows(B, OH, nbx):
-                    variants.insert(0, (f"slice{R}w{nw}", [
-                        lambda *_, x=inp, out=out, h=h, w=w, R=R, nw=nw, bp_=bp_: FB.fused_ir_slice(
-                            x, bp_, out, B=B, IH=h, IW=w, stride=s.stride, residual=s.residual,
-                            R=R, nw=nw)]))
+                for oneb in (False, True):  # "o": one barrier per input row
+                    if FB.slice_lds(bp_, s.stride, OW, nw, oneb) > 160 * 1024:
+                        continue
+                    for R in self._slice_rows(B, OH, nbx):
+                        variants.insert(0, (f"slice{R}w{nw}" + ("o" if oneb else ""), [
+                            lambda *_, x=inp, out=out, h=h, w=w, R=R, nw=nw, bp_=bp_, oneb=oneb: FB.fused_ir_slice(
+                                x, bp_, out, B=B, IH=h, IW=w, stride=s.stride, residual=s.residual,
+                                R=R, nw=nw, one_barrier=oneb)]))
         outer_ops.append(Choice(f"block{i}", variants))
         return out, OH, OW, s.cout
 

@@ -149,16 +149,19 @@ def slice_widths(cin: int, hid: int, cout: int, stride: int, dil: int) -> list:
                   reverse=True)
 
 
-def slice_lds(packed: Dict, stride: int, OW: int, nw: int) -> int:
+def slice_lds(packed: Dict, stride: int, OW: int, nw: int, one_barrier: bool = False) -> int:
     from .hip_ops import _hip_mod
-    return int(_hip_mod().fused_ir_slice_lds(stride, packed["hidP"], OW, packed["Cout"], nw))
+    return int(_hip_mod().fused_ir_slice_lds(stride, packed["hidP"], OW, packed["Cout"], nw,
+                                             bool(one_barrier)))
 
 
 def fused_ir_slice(x: torch.Tensor, packed: Dict, out: torch.Tensor, *, B: int, IH: int, IW: int,
-                   stride: int, residual: bool, R: int = 8, nw: int = 2) -> torch.Tensor:
+                   stride: int, residual: bool, R: int = 8, nw: int = 2,
+                   one_barrier: bool = False) -> torch.Tensor:
     """Launch fused_ir_slice_kernel (csrc/hip/fused_ir_slice.hip): the band kernel's row
     streaming with waves = nw column groups x hidden chunks of 32, each wave's chunk
-    weights held in VGPRs. Same blob as fused_ir_band; bit-identical results."""
+    weights held in VGPRs. Same blob as fused_ir_band; bit-identical results.
+    ``one_barrier``: one workgroup barrier per input row (E / D rows double-buffered)."""
     from .hip_ops import _chk, _dbg, _hip_mod, _ptr, _stream
     Cin, Cout = packed["Cin"], packed["Cout"]
     OH, OW = (IH - 1) // stride + 1, (IW - 1) // stride + 1
@@ -169,12 +172,12 @@ def fused_ir_slice(x: torch.Tensor, packed: Dict, out: torch.Tensor, *, B: int, 
     _chk(x, torch.bfloat16, "x", B * IH * IW * Cin)
     _chk(out, torch.bfloat16, "out", B * OH * OW * Cout)
     _chk(packed["blob"], torch.uint8, "blob", packed["blob_bytes"])
-    if slice_lds(packed, stride, OW, nw) > 160 * 1024:
+    if slice_lds(packed, stride, OW, nw, one_barrier) > 160 * 1024:
         raise ValueError("fused_ir_slice: LDS over 160 KiB")
     _hip_mod().fused_ir_slice(_ptr(x), _ptr(packed["blob"]), _ptr(out), B, IH, IW, Cin, OH, OW, Cout,
                               packed["hidP"], stride, int(bool(residual)), R, packed["o_be"],
                               packed["o_wd"], packed["o_bd"], packed["o_wp"], packed["o_bp"], nw,
-                              _stream())
+                              _stream(), int(bool(one_barrier)))
     _dbg("fused_ir_slice")
     return out
 

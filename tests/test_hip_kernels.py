@@ -1493,15 +1493,22 @@ def test_fused_ir_slice(cin, cout, stride, H, W, R):
         band = torch.full((B, OH, OW, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
         FB.fused_ir_band(xd, packed, band, B=B, IH=H, IW=W, stride=stride, residual=spec.residual,
                          R=R, nslot=2)
+    first = None
     for nw in widths:
-        out = torch.full((B, OH, OW, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
-        FB.fused_ir_slice(xd, packed, out, B=B, IH=H, IW=W, stride=stride, residual=spec.residual,
-                          R=R, nw=nw)
-        torch.cuda.synchronize()
-        assert torch.isfinite(out).all(), nw
-        assert _rel(_nchw(out).cpu(), ref) < 2e-2, nw
-        if band is not None:
-            assert torch.equal(out, band), (nw, (out.float() - band.float()).abs().max().item())
+        for oneb in (False, True):  # one barrier per input row: same arithmetic, bit-identical
+            if FB.slice_lds(packed, stride, OW, nw, oneb) > 160 * 1024:
+                continue
+            out = torch.full((B, OH, OW, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
+            FB.fused_ir_slice(xd, packed, out, B=B, IH=H, IW=W, stride=stride, residual=spec.residual,
+                              R=R, nw=nw, one_barrier=oneb)
+            torch.cuda.synchronize()
+            assert torch.isfinite(out).all(), (nw, oneb)
+            assert _rel(_nchw(out).cpu(), ref) < 2e-2, (nw, oneb)
+            if band is not None:
+                assert torch.equal(out, band), (nw, oneb, (out.float() - band.float()).abs().max().item())
+            if first is None:
+                first = out
+            assert torch.equal(out, first), (nw, oneb)
 
 
 def test_multistream_batched_step_tags_streams():
