@@ -703,7 +703,7 @@ class HipDeepLab:
                     # small batches: the hidden chunks of a span over hs workgroups (fp32
                     # partials + stream_combine), so B * S * hs workgroups share the chip
                     nc = -(-hid // 32)
-                    hs_opts = [hs for hs in (2, 3, 4, 6) if hs <= nc and B * S * hs <= 512] if B <= 8 else []
+                    hs_opts = [hs for hs in (2, 3, 4, 6) if hs <= nc and B * S * hs <= 512] if B <= 16 else []
                     if hs_opts:
                         key = f"b{i}_part"
                         if key not in bufs_part:

@@ -48,6 +48,7 @@ class Producer(threading.Thread):
         self.error: Optional[BaseException] = None
         self.steps = 0
         self.alive_ts = time.time()
+        self.on_step = None  # optional progress hook, called with the step count after each step
 
     def stop(self) -> None:
         self._stop_evt.set()
@@ -105,6 +106,8 @@ class Producer(threading.Thread):
                 drv.step(nxt)
                 self.steps += 1
                 self.alive_ts = time.time()
+                if self.on_step is not None:
+                    self.on_step(self.steps)
                 if nxt is None:
                     log.info("end of stream after %d steps", self.steps)
                     break
@@ -144,6 +147,8 @@ class Producer(threading.Thread):
                 self.metrics.inc("objects", len(recs))
                 self.steps += 1
                 self.alive_ts = time.time()
+                if self.on_step is not None:
+                    self.on_step(self.steps)
                 failures = 0
             except StopIteration:
                 log.info("end of stream after %d steps", self.steps)

@@ -212,27 +212,29 @@ def _worker_main(cfg: Config, rank: int, ring_name: str, q, stop_evt, incarnatio
                for s in range(S)]
     prod = Producer(engine, sources, _RingHub(ring), metrics, cfg.batch, max_steps=max_steps)
     fault = _fault_for(cfg.inject_fault, rank, incarnation)
+
+    def on_step(n: int) -> None:  # step progress, published by the producer thread itself
+        ring.progress(n)
+        if fault is not None and fault[0] == "hang" and n >= fault[1]:
+            # a hung GPU: the producer thread blocks (as in a synchronize that never
+            # returns) while the process and its other threads live on
+            while not stop_evt.is_set():
+                time.sleep(0.05)
+
+    prod.on_step = on_step
     q.put(("up", rank, incarnation, f"{engine.backend} {engine.device}"))
     prod.start()
     last_snap = 0.0
     while prod.is_alive():
         if stop_evt.is_set():
             prod.stop()
-        steps = prod.steps
-        if fault is not None and steps >= fault[1]:
-            if fault[0] == "crash":
-                os._exit(70)  # a crashed worker: no cleanup, no goodbye
-            # a hung GPU: the process lives on but no step completes any more
-            while not stop_evt.is_set():
-                time.sleep(0.05)
-            os._exit(0)
-        if steps != ring.steps:
-            ring.progress(steps)
+        if fault is not None and fault[0] == "crash" and prod.steps >= fault[1]:
+            os._exit(70)  # a crashed worker: no cleanup, no goodbye
         now = time.time()
         if now - last_snap > 0.5:
             q.put(("snap", rank, metrics.snapshot()))
             last_snap = now
-        prod.join(timeout=0.05)
+        prod.join(timeout=0.02)
     ring.progress(prod.steps)
     for s in sources:
         s.close()
