@@ -30,6 +30,7 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace ssa {
@@ -38,53 +39,65 @@ namespace {
 struct FrameWS {
   int32_t* L;          // [N + 1] union-find labels (index 0 = outside)
   uint8_t* mask;       // [N] 1 = foreground
-  int32_t* slot;       // [N] per root index: record slot or -1
-  int32_t* t00;        // [N] per root index: subtree 2*area
-  long long* t10;      // [N] subtree 6 * int x
-  long long* t01;      // [N] subtree 6 * int y
-  int32_t* th;         // [N][bins] per root index: class histogram of the contour's fill
-  int32_t* nslot;      // [0] selected, [1] contours dropped (> K passed), [2] cross-tile edges, [3] roots
+  int32_t* nslot;      // [0] selected, [1] contours dropped (> K passed), [2] cross-tile edges,
+                       // [3] component roots listed (zeroed by k_ccl_local)
   int32_t* slot_node;  // [K]
-  int32_t* cidx;       // [N] per tile-local root pixel: its index among the tile's roots,
-                       //     after k_ccl_merge its final label
-  int32_t* rootpix;    // [ntiles][kTileRoots] raster index of each tile-local root
-  int32_t* ntroot;     // [ntiles] tile-local roots per tile
-  int32_t* flag;       // [4]: [0] = 1 -> frame took the global union-find fallback
-  int32_t* edges;      // [kEdgeCap][2] cross-tile unions (tile-local root pairs, -1 = outside)
-  int32_t* rpar;       // [N] per root index: border-tree parent (component label, 0 = frame)
-  int32_t* rlist;      // [N] raster indices of the component roots (nslot[3] of them, any order)
-  int fb;              // (kernels after k_ccl_merge) flag[0]: L holds final labels
+  int32_t* cidx;       // [N] per tile-local root pixel: its compact index (k_ccl_local), after
+                       //     k_ccl_merge its final label; per component root (fallback): its label
+  int32_t* rootpix;    // [kMergeCap] raster index of each compact tile-local root
+  int32_t* flag;       // [8]: [0] = 1 -> global union-find fallback, [1] = 1 -> root pool exhausted
+                       //      (no records), [2] tile-local roots (k_ccl_local -> k_ccl_merge, which
+                       //      re-zeroes it), [3] the frame's first pool entry
+  int32_t* edges;      // [kEdgeCap][2] cross-tile unions (compact root pairs as raster, -1 = outside)
+  // root pool, shared by the batch and indexed by component label - 1 (labels are pool
+  // entries: a frame's components take one contiguous run of it)
+  int32_t* pool;       // [0] entries taken this call (zeroed by k_ccl_local)
+  int32_t* t00;        // [P] subtree 2*area
+  long long* t10;      // [P] subtree 6 * int x
+  long long* t01;      // [P] subtree 6 * int y
+  int32_t* th;         // [P][bins] class histogram of the contour's fill
+  int32_t* rpar;       // [P] border-tree parent (label, 0 = frame; fallback frames: raster root + 1)
+  int32_t* rlist;      // [P] raster index of the component's root (first) pixel
+  int fb;              // (kernels after k_ccl_merge) flag[0]
 };
 
 #ifndef SSA_CCL_TH
 #define SSA_CCL_TH 32
 #endif
 constexpr int TW = 32, TH = SSA_CCL_TH;  // local CCL tile
-constexpr int kTileRoots = TW * TH;  // worst case roots per tile
-constexpr int kMergeCap = 12288;     // compact nodes the per-frame LDS merge handles
-constexpr int kEdgeCap = 1 << 16;    // cross-tile union pairs per frame
+constexpr int kMergeCap = 12288;     // tile-local roots the per-frame LDS merge handles
+constexpr int kEdgeCap = 1 << 15;    // cross-tile union pairs per frame
+constexpr int kPoolPerFrame = 8192;  // root pool entries per frame of the batch (floor: N + 1)
 
-// Workspace layout: per frame, fixed stride; counters first (zeroed by k_ccl_local).
-// The per-root arrays are indexed by the root's raster index (no cap on the number of
-// components); only roots' entries are ever written or read, and k_ccl_merge zeroes them.
+// Workspace layout (round 5): per frame only what is per pixel (labels, mask,
+// compact index) plus the bounded merge inputs; everything per component lives in ONE pool
+// for the batch, indexed by label, of max(B * kPoolPerFrame, N + 1) entries. A frame's
+// components take a contiguous run of it (k_ccl_merge: one atomicAdd of its component count;
+// fallback frames reserve their tile-local root count, an upper bound). The floor of N + 1
+// entries keeps any single frame exact (a frame has fewer components than pixels); a batch
+// whose components overflow the pool flags the frames that did not fit (flag[1]: no records,
+// count NaN; never on segmentation maps -- the bench frames have ~200 components each).
+// Round 4 indexed every per-root array by raster index: 46 MB per 513^2 frame.
 struct Layout {
-  size_t N, K, bins, ntiles;
+  size_t N, K, bins, P;
   size_t small_bytes;  // nslot(16) + slot_node, per frame (zeroed every call)
   size_t big_bytes;    // per frame
-  size_t total(int B) const { return (small_bytes + big_bytes) * (size_t)B; }
+  size_t pool_bytes;   // per batch
+  size_t total(int B) const { return (small_bytes + big_bytes) * (size_t)B + 256 + pool_bytes; }
 };
 
 __host__ __device__ inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
-Layout layout(int H, int W, int K, int bins) {
+Layout layout(int B, int H, int W, int K, int bins) {
   Layout l;
   l.N = (size_t)H * W;
   l.K = K;
   l.bins = bins;
-  l.ntiles = (size_t)((W + TW - 1) / TW) * ((H + TH - 1) / TH);
+  l.P = std::max((size_t)B * kPoolPerFrame, l.N + 1);
   l.small_bytes = al(16 + (size_t)K * 4);
-  l.big_bytes = al((l.N + 1) * 4) + al(l.N) + 2 * al(l.N * 4) + 2 * al(l.N * 8) + al(l.N * bins * 4) +
-                al(l.N * 4) + al(l.ntiles * kTileRoots * 4) + al(l.ntiles * 4) + al(16) + al((size_t)kEdgeCap * 8) + 2 * al(l.N * 4);
+  l.big_bytes = al((l.N + 1) * 4) + al(l.N) + al(l.N * 4) + al((size_t)kMergeCap * 4) + al(32) +
+                al((size_t)kEdgeCap * 8);
+  l.pool_bytes = 2 * al(l.P * 8) + 3 * al(l.P * 4) + al(l.P * bins * 4);
   return l;
 }
 
@@ -93,21 +106,22 @@ __host__ __device__ inline FrameWS frame_ws(char* ws, const Layout& l, int B, in
   char* s = ws + (size_t)b * l.small_bytes;
   f.nslot = reinterpret_cast<int32_t*>(s);
   f.slot_node = reinterpret_cast<int32_t*>(s + 16);
-  char* p = ws + (size_t)B * l.small_bytes + (size_t)b * l.big_bytes;
+  char* hdr = ws + (size_t)B * l.small_bytes;
+  f.pool = reinterpret_cast<int32_t*>(hdr);
+  char* p = hdr + 256 + (size_t)b * l.big_bytes;
   f.L = reinterpret_cast<int32_t*>(p); p += al((l.N + 1) * 4);
   f.mask = reinterpret_cast<uint8_t*>(p); p += al(l.N);
-  f.slot = reinterpret_cast<int32_t*>(p); p += al(l.N * 4);
-  f.t00 = reinterpret_cast<int32_t*>(p); p += al(l.N * 4);
-  f.t10 = reinterpret_cast<long long*>(p); p += al(l.N * 8);
-  f.t01 = reinterpret_cast<long long*>(p); p += al(l.N * 8);
-  f.th = reinterpret_cast<int32_t*>(p); p += al(l.N * l.bins * 4);
   f.cidx = reinterpret_cast<int32_t*>(p); p += al(l.N * 4);
-  f.rootpix = reinterpret_cast<int32_t*>(p); p += al(l.ntiles * kTileRoots * 4);
-  f.ntroot = reinterpret_cast<int32_t*>(p); p += al(l.ntiles * 4);
-  f.flag = reinterpret_cast<int32_t*>(p); p += al(16);
-  f.edges = reinterpret_cast<int32_t*>(p); p += al((size_t)kEdgeCap * 8);
-  f.rpar = reinterpret_cast<int32_t*>(p); p += al(l.N * 4);
-  f.rlist = reinterpret_cast<int32_t*>(p); p += al(l.N * 4);
+  f.rootpix = reinterpret_cast<int32_t*>(p); p += al((size_t)kMergeCap * 4);
+  f.flag = reinterpret_cast<int32_t*>(p); p += al(32);
+  f.edges = reinterpret_cast<int32_t*>(p);
+  char* q = hdr + 256 + (size_t)B * l.big_bytes;
+  f.t10 = reinterpret_cast<long long*>(q); q += al(l.P * 8);
+  f.t01 = reinterpret_cast<long long*>(q); q += al(l.P * 8);
+  f.t00 = reinterpret_cast<int32_t*>(q); q += al(l.P * 4);
+  f.rpar = reinterpret_cast<int32_t*>(q); q += al(l.P * 4);
+  f.rlist = reinterpret_cast<int32_t*>(q); q += al(l.P * 4);
+  f.th = reinterpret_cast<int32_t*>(q);
   f.fb = 0;
   return f;
 }
@@ -237,17 +251,18 @@ __global__ __launch_bounds__(kCclThreads) void k_ccl_local(KArgs a, const int32_
   __shared__ int hs[HH2 * TW];  // packed horizontal 3-sums
   __shared__ int lbl[TW * TH];
   __shared__ unsigned fgrow[TH], bgrow[TH];
-  __shared__ int s_nroot;
   const int tid = threadIdx.x;
   for (int i = tid; i < 256; i += kCclThreads)
     spal[i] = (pal[3 * i] & 255) | (pal[3 * i + 1] & 255) << 10 | (pal[3 * i + 2] & 255) << 20;
-  if (tid == 0) s_nroot = 0;
   const int b = blockIdx.z;
   const int x0 = blockIdx.x * TW, y0 = blockIdx.y * TH;
   const int tx = tid % TW, ty0 = tid / TW;
   const int x = x0 + tx;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
-  if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) f.L[0] = 0;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) {
+    f.L[0] = 0;
+    if (b == 0) *f.pool = 0;  // read first by k_ccl_merge
+  }
   {  // the frame's tiles zero its counters (round 2 spent a k_zero launch on this)
     uint4* z = reinterpret_cast<uint4*>(a.ws + (size_t)b * a.lay.small_bytes);
     const int words = (int)(a.lay.small_bytes / 16), nt = gridDim.x * gridDim.y;
@@ -327,22 +342,32 @@ __global__ __launch_bounds__(kCclThreads) void k_ccl_local(KArgs a, const int32_
     }
   }
   __syncthreads();
-  const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+  const int lane = tid & 63;
 #pragma unroll
   for (int k = 0; k < RPT; ++k) {
     const int ty = ty0 + k * RS, y = y0 + ty, me = ty * TW + tx;
-    if (!in[k]) continue;
-    const int r = lfind(lbl, start[k]);
-    const int rx = x0 + r % TW, ry = y0 + r / TW;
-    f.L[y * a.cw + x + 1] = ry * a.cw + rx + 1;
-    if (r == me) {  // tile-local root: number it for the compact merge
-      const int c = atomicAdd(&s_nroot, 1);
-      f.cidx[y * a.cw + x] = c;
-      f.rootpix[(size_t)tile * kTileRoots + c] = y * a.cw + x;
+    bool root = false;
+    if (in[k]) {
+      const int r = lfind(lbl, start[k]);
+      const int rx = x0 + r % TW, ry = y0 + r / TW;
+      f.L[y * a.cw + x + 1] = ry * a.cw + rx + 1;
+      root = r == me;
+    }
+    // tile-local roots get frame-wide compact indices for the merge: one atomic per wave
+    // (flag[2] is zeroed again by k_ccl_merge, its reader)
+    const unsigned long long rb = __ballot(root);
+    if (rb) {
+      const int leader = __ffsll((long long)rb) - 1;
+      int base = 0;
+      if (lane == leader) base = atomicAdd(f.flag + 2, __popcll(rb));
+      base = __shfl(base, leader, 64);
+      if (root) {
+        const int c = base + __popcll(rb & ((1ull << lane) - 1));
+        f.cidx[y * a.cw + x] = c;
+        if (c < kMergeCap) f.rootpix[c] = y * a.cw + x;
+      }
     }
   }
-  __syncthreads();
-  if (tid == 0) f.ntroot[tile] = s_nroot;
 }
 
 // ---------------------------------------------------------------- compact merge
@@ -481,103 +506,91 @@ __global__ __launch_bounds__(kEdgeThreads) void k_ccl_edges(KArgs a) {
 
 __device__ __forceinline__ void ccl_boundary_pixel(KArgs& a, FrameWS& f, int p);
 
-__device__ __forceinline__ void add_root(FrameWS& f, int bins, int p, int* s_nr) {
-  f.slot[p] = -1;
-  f.t00[p] = 0;
-  f.t10[p] = 0;
-  f.t01[p] = 0;
-  int* h = f.th + (size_t)p * bins;
+// A component root takes pool entry n (label n + 1): its accumulators zeroed, listed
+__device__ __forceinline__ void new_root(FrameWS& f, int bins, int n, int p) {
+  f.t00[n] = 0;
+  f.t10[n] = 0;
+  f.t01[n] = 0;
+  int* h = f.th + (size_t)n * bins;
   for (int c = 0; c < bins; ++c) h[c] = 0;
-  f.rlist[atomicAdd(s_nr, 1)] = p;
+  f.rlist[n] = p;
 }
 
 __global__ __launch_bounds__(1024) void k_ccl_merge(KArgs a) {
   extern __shared__ int sm[];
   const int b = blockIdx.x;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
-  const int cw = a.cw, ch = a.ch;
-  const int tx_n = (cw + TW - 1) / TW, ty_n = (ch + TH - 1) / TH;
-  const int nt = tx_n * ty_n;
+  const int cw = a.cw;
   const int tid = threadIdx.x;
-  int* toff = sm;                   // [nt + 1]
-  int* part = sm + nt + 1;          // [1024] scan partials
-  int* par = part + 1024;           // [kMergeCap + 1] (last = outside)
-  int* minr = par + kMergeCap + 1;  // [kMergeCap + 1]
-  int* s_nr = minr + kMergeCap + 1; // [1] roots listed
-  if (tid == 0) *s_nr = 0;
-  // exclusive scan of the per-tile root counts
-  const int per = (nt + 1023) / 1024;
-  const int t0 = tid * per, t1 = min(nt, t0 + per);
-  int sum = 0;
-  for (int t = t0; t < t1; ++t) sum += f.ntroot[t];
-  part[tid] = sum;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const int v = tid >= o ? part[tid - o] : 0;
-    __syncthreads();
-    part[tid] += v;
-    __syncthreads();
-  }
-  int acc = part[tid] - sum;
-  for (int t = t0; t < t1; ++t) {
-    toff[t] = acc;
-    acc += f.ntroot[t];
-  }
-  if (tid == 1023) toff[nt] = part[1023];
-  __syncthreads();
-  const int R = toff[nt];
+  int* par = sm;                    // [kMergeCap + 1] (last = outside)
+  int* minr = par + kMergeCap + 1;  // [kMergeCap + 1] set minimum pixel, then the set's label
+  int* s_c = minr + kMergeCap + 1;  // [0] components, [1] listed, [2] pool base (-1: exhausted)
+  const int R = f.flag[2];
   const int E = f.nslot[2];
-  const int N = ch * cw;
-  if (tid == 0) f.flag[0] = (R > kMergeCap || E > kEdgeCap) ? 1 : 0;
-  if (R > kMergeCap || E > kEdgeCap) return;  // k_fb_unite / k_fb_relabel take the frame
+  if (tid == 0) { s_c[0] = 0; s_c[1] = 0; }
+  if (R > kMergeCap || E > kEdgeCap) {  // k_fb_unite / k_fb_relabel take the frame
+    if (tid == 0) {
+      // reserve the tile-local root count (>= its components) from the pool
+      const int base = atomicAdd(f.pool, R);
+      f.flag[0] = 1;
+      f.flag[1] = (size_t)base + R > a.lay.P ? 1 : 0;
+      f.flag[2] = 0;
+      f.flag[3] = base;
+    }
+    return;
+  }
   const int OUT = R;
   for (int i = tid; i <= R; i += 1024) {
     par[i] = i;
     minr[i] = 0x7fffffff;
   }
   __syncthreads();
-  auto compact = [&](int r) {
-    const int ly = r / cw, lx = r - ly * cw;
-    return toff[(ly / TH) * tx_n + lx / TW] + f.cidx[r];
-  };
   for (int e = tid; e < E; e += 1024) {
     const int ra = f.edges[2 * e], rb = f.edges[2 * e + 1];
-    lunite(par, compact(ra), rb < 0 ? OUT : compact(rb));
+    lunite(par, f.cidx[ra], rb < 0 ? OUT : f.cidx[rb]);
   }
   __syncthreads();
-  // per compact node (not per tile: a tile's roots were one thread's serial chain of
-  // global loads): its tile by binary search over the tile offsets
-  auto tile_of = [&](int i) {  // last tile t with toff[t] <= i (empty tiles share offsets)
-    int lo = 0, hi = nt - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (toff[mid] <= i) lo = mid; else hi = mid - 1;
-    }
-    return lo;
-  };
-  for (int i = tid; i < R; i += 1024) {
-    const int t = tile_of(i);
-    atomicMin(&minr[lfind(par, i)], f.rootpix[(size_t)t * kTileRoots + (i - toff[t])]);
-  }
+  for (int i = tid; i < R; i += 1024) atomicMin(&minr[lfind(par, i)], f.rootpix[i]);
   __syncthreads();
   const int outroot = lfind(par, OUT);
-  // every set but the outside one is a component: its minimum pixel is the root
+  // every set but the outside one is a component: count, take a run of the pool, list
   for (int i = tid; i < R; i += 1024)
-    if (i != outroot && lds_ld(par + i) == i) add_root(f, a.bins, minr[i], s_nr);
-  // final label of every tile-local root, over its cidx entry (compact() is done)
+    if (i != outroot && par[i] == i) atomicAdd(s_c, 1);
+  __syncthreads();
+  if (tid == 0) {
+    const int nr = s_c[0];
+    const int base = atomicAdd(f.pool, nr);
+    const bool ex = (size_t)base + nr > a.lay.P;
+    s_c[2] = ex ? -1 : base;
+    f.flag[0] = 0;
+    f.flag[1] = ex ? 1 : 0;
+    f.flag[2] = 0;
+    f.flag[3] = base;
+    f.nslot[3] = nr;
+  }
+  __syncthreads();
+  const int base = s_c[2];
+  if (base < 0) return;
   for (int i = tid; i < R; i += 1024) {
-    const int t = tile_of(i);
+    if (i != outroot && par[i] == i) {
+      const int n = base + atomicAdd(s_c + 1, 1);
+      new_root(f, a.bins, n, minr[i]);  // the root: the component's minimum pixel
+      minr[i] = n + 1;
+    }
+  }
+  __syncthreads();
+  // final label of every tile-local root, over its cidx entry (the compact indices are done)
+  for (int i = tid; i < R; i += 1024) {
     const int r = lfind(par, i);
-    f.cidx[f.rootpix[(size_t)t * kTileRoots + (i - toff[t])]] = r == outroot ? 0 : minr[r] + 1;
+    f.cidx[f.rootpix[i]] = r == outroot ? 0 : minr[r];
   }
   __syncthreads();
   // border-tree parent of every root: the final label of the pixel left of it
-  const int nr = *s_nr;
-  for (int i = tid; i < nr; i += 1024) {
-    const int p = f.rlist[i];
-    f.rpar[p] = p % cw > 0 ? f.cidx[f.L[p] - 1] : 0;
+  const int nr = s_c[0];
+  for (int j = tid; j < nr; j += 1024) {
+    const int p = f.rlist[base + j];
+    f.rpar[base + j] = p % cw > 0 ? f.cidx[f.L[p] - 1] : 0;
   }
-  if (tid == 0) f.nslot[3] = nr;
 }
 
 // Cross-tile merges (and image-border background -> outside node 0) of the fallback
@@ -641,31 +654,46 @@ __device__ __forceinline__ void ccl_boundary_pixel(KArgs& a, FrameWS& f, int p) 
 // then the relabel (every pixel's root, read-only traversal: concurrent stores only ever
 // write roots), the roots' accumulators zeroed and listed, and each root's border-tree
 // parent (the final label of the pixel left of it, resolved by the same traversal).
-constexpr int kFbBlocks = 96;  // blocks per frame (grid-stride over the frame's pixels)
+constexpr int kFbBlocks = 256;  // blocks (grid-stride over each flagged frame's pixels in turn)
+
+// The flagged frames of the batch, as a bitmask per 64 frames (every wave of the block
+// computes the same mask from the same flags; one load per lane, not a chain of B loads).
+__device__ __forceinline__ unsigned long long fb_frames(const KArgs& a, int b0) {
+  const int b = b0 + (int)(threadIdx.x & 63);
+  bool need = false;
+  if (b < a.B) {
+    const FrameWS g = frame_ws(a.ws, a.lay, a.B, b);
+    need = g.flag[0] != 0 && g.flag[1] == 0;
+  }
+  return __ballot(need);
+}
 
 __global__ __launch_bounds__(256) void k_fb_unite(KArgs a) {
-  FrameWS f = frame_ws(a.ws, a.lay, a.B, blockIdx.y);
-  if (__builtin_amdgcn_readfirstlane(f.flag[0]) == 0) return;
   const int N = a.ch * a.cw;
-  for (int p = blockIdx.x * 256 + threadIdx.x; p < N; p += gridDim.x * 256) ccl_boundary_pixel(a, f, p);
+  for (int b0 = 0; b0 < a.B; b0 += 64) {
+    for (unsigned long long m = fb_frames(a, b0); m; m &= m - 1) {
+      FrameWS f = frame_ws(a.ws, a.lay, a.B, b0 + __ffsll((long long)m) - 1);
+      for (int p = blockIdx.x * 256 + threadIdx.x; p < N; p += gridDim.x * 256) ccl_boundary_pixel(a, f, p);
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void k_fb_relabel(KArgs a) {
-  FrameWS f = frame_ws(a.ws, a.lay, a.B, blockIdx.y);
-  if (__builtin_amdgcn_readfirstlane(f.flag[0]) == 0) return;
   const int N = a.ch * a.cw;
-  for (int p = blockIdx.x * 256 + threadIdx.x; p < N; p += gridDim.x * 256) {
-    const int r = find_root(f.L, p + 1);
-    __hip_atomic_store(f.L + p + 1, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (r == p + 1) {
-      f.slot[p] = -1;
-      f.t00[p] = 0;
-      f.t10[p] = 0;
-      f.t01[p] = 0;
-      int* h = f.th + (size_t)p * a.bins;
-      for (int c = 0; c < a.bins; ++c) h[c] = 0;
-      f.rpar[p] = p % a.cw > 0 ? find_root(f.L, p) : 0;
-      f.rlist[atomicAdd(f.nslot + 3, 1)] = p;  // nslot[3] zeroed by k_ccl_local
+  for (int b0 = 0; b0 < a.B; b0 += 64) {
+    for (unsigned long long m = fb_frames(a, b0); m; m &= m - 1) {
+      FrameWS f = frame_ws(a.ws, a.lay, a.B, b0 + __ffsll((long long)m) - 1);
+      const int base = f.flag[3];
+      for (int p = blockIdx.x * 256 + threadIdx.x; p < N; p += gridDim.x * 256) {
+        const int r = find_root(f.L, p + 1);
+        __hip_atomic_store(f.L + p + 1, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (r == p + 1) {
+          const int n = base + atomicAdd(f.nslot + 3, 1);  // nslot[3] zeroed by k_ccl_local
+          new_root(f, a.bins, n, p);
+          f.rpar[n] = p % a.cw > 0 ? find_root(f.L, p) : 0;  // raster root + 1: parent_of maps it
+          f.cidx[p] = n + 1;
+        }
+      }
     }
   }
 }
@@ -674,13 +702,16 @@ __global__ __launch_bounds__(256) void k_fb_relabel(KArgs a) {
 // first pixel (0 = the frame at the image border), a pure function of the final labels,
 // tabulated per root by k_ccl_merge (one load instead of the L -> cidx chain).
 // Final component label of pixel q (root raster index + 1, 0 = outside).
+// (L holds the tile-local root, or after the fallback the component root / 0 = outside;
+// cidx of either is the label.)
 __device__ __forceinline__ int fin(const FrameWS& f, int q) {
   const int l = f.L[q + 1];
-  return f.fb ? l : f.cidx[l - 1];
+  return l == 0 ? 0 : f.cidx[l - 1];
 }
 
 __device__ __forceinline__ int parent_of(const FrameWS& f, int cw, int n) {
-  return f.rpar[n - 1];
+  const int r = f.rpar[n - 1];
+  return (f.fb && r != 0) ? f.cidx[r - 1] : r;
 }
 
 // Per-block privatisation of the component sums. A real scene's mask has a few
@@ -841,6 +872,7 @@ __global__ __launch_bounds__(kAccThreads) void k_accum(KArgs a) {
   const int cw = a.cw, ch = a.ch, bins = a.bins;
   const int N = cw * ch;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
+  if (f.flag[1]) return;  // root pool exhausted: no records for this frame
   f.fb = f.flag[0];
   for (int i = threadIdx.x; i < kHash; i += kAccThreads) {
     T.q.key[i] = 0; T.q.s00[i] = 0; T.q.s10[i] = 0; T.q.s01[i] = 0;
@@ -1026,6 +1058,7 @@ __global__ __launch_bounds__(256) void k_accum_tiles(KArgs a) {
   const int cw = a.cw, ch = a.ch, bins = a.bins;
   const int x0 = blockIdx.x * kAT, y0 = blockIdx.y * kAT;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
+  if (f.flag[1]) return;  // root pool exhausted: no records for this frame
   f.fb = f.flag[0];
   const int tid = threadIdx.x;
   for (int i = tid; i < kHash; i += 256) {
@@ -1058,7 +1091,7 @@ __global__ __launch_bounds__(256) void k_accum_tiles(KArgs a) {
 #pragma unroll
     for (int k = 0; k < kAPT; ++k) {
       const int i = tid + k * 256;
-      if (i < kARN) sfin[i] = lv[k] == 0 ? 0 : (f.fb ? lv[k] : f.cidx[lv[k] - 1]);
+      if (i < kARN) sfin[i] = lv[k] == 0 ? 0 : f.cidx[lv[k] - 1];
     }
   }
   __syncthreads();
@@ -1192,10 +1225,15 @@ __global__ __launch_bounds__(256) void k_accum_tiles(KArgs a) {
 // negative record count. Frames with more than kSortCap passing contours take a
 // raster-order scan of every pixel instead. (Round 2 ran a full-frame k_select pass
 // before this kernel: 20 us per 32 frames.)
-__device__ __forceinline__ bool passes(const FrameWS& f, const KArgs& a, int p) {
-  if (fin(f, p) != p + 1) return false;
-  const int t = f.t00[p];
+__device__ __forceinline__ bool passes_n(const FrameWS& f, const KArgs& a, int n) {
+  const int t = f.t00[n - 1];
   return t != 0 && (double)t * 0.5 >= a.min_area;
+}
+
+// label of pixel p if p is its component's root (first pixel) and the contour passes, else 0
+__device__ __forceinline__ int passes_px(const FrameWS& f, const KArgs& a, int p) {
+  const int n = fin(f, p);
+  return n != 0 && f.rlist[n - 1] == p && passes_n(f, a, n) ? n : 0;
 }
 
 constexpr int kSortCap = 8192;
@@ -1209,12 +1247,11 @@ __device__ __forceinline__ void assign_frame(const KArgs& a, FrameWS& f, int* s_
   const int N = a.ch * a.cw;
   if (t == 0) s_cnt = 0;
   __syncthreads();
-  const int nroot = f.nslot[3];
+  const int nroot = f.nslot[3], base = f.flag[3];
   for (int i = t; i < nroot; i += 1024) {
-    const int p = f.rlist[i];
-    if (passes(f, a, p)) {
+    if (passes_n(f, a, base + i + 1)) {
       const int k = atomicAdd(&s_cnt, 1);
-      if (k < kSortCap) s_key[k] = p;
+      if (k < kSortCap) s_key[k] = f.rlist[base + i];  // sorted by raster root
     }
   }
   __syncthreads();
@@ -1238,17 +1275,17 @@ __device__ __forceinline__ void assign_frame(const KArgs& a, FrameWS& f, int* s_
       }
     }
     for (int i = t; i < kept; i += 1024) {
-      const int p = s_key[i];
-      f.slot[p] = i;
-      f.slot_node[i] = p + 1;
-      s_sn[i] = p + 1;
+      const int n = f.cidx[s_key[i]];  // a component root's cidx entry is its label
+      f.slot_node[i] = n;
+      s_sn[i] = n;
     }
   } else {
     const int wid = t >> 6, lane = t & 63;
     int base = 0;
     for (int c0 = 0; c0 < N && base < kept; c0 += 1024) {
       const int p = c0 + t;
-      const bool ok = p < N && passes(f, a, p);
+      const int n = p < N ? passes_px(f, a, p) : 0;
+      const bool ok = n != 0;
       const unsigned long long m = __ballot(ok);
       if (lane == 0) s_w[wid] = __popcll(m);
       __syncthreads();
@@ -1259,9 +1296,8 @@ __device__ __forceinline__ void assign_frame(const KArgs& a, FrameWS& f, int* s_
       }
       const int rank = base + wb + __popcll(m & ((1ull << lane) - 1));
       if (ok && rank < kept) {
-        f.slot[p] = rank;
-        f.slot_node[rank] = p + 1;
-        s_sn[rank] = p + 1;
+        f.slot_node[rank] = n;
+        s_sn[rank] = n;
       }
       base += tot;
       __syncthreads();
@@ -1280,7 +1316,7 @@ __device__ __forceinline__ void assign_frame(const KArgs& a, FrameWS& f, int* s_
 constexpr int kMaxDepth = 32;
 
 __device__ __forceinline__ int disc_key(const FrameWS& f, int n) {
-  const int r = n - 1;
+  const int r = f.rlist[n - 1];
   return f.mask[r] ? r : r - 1;
 }
 
@@ -1325,11 +1361,7 @@ __device__ __forceinline__ void finalize_frame(const KArgs& a, FrameWS& f, const
     // ancestor chain (top first) of discovery keys
     int chain[kMaxDepth];
     int len = 0;
-    for (int n = node; n != 0 && len < kMaxDepth; n = parent_of(f, a.cw, n)) {
-      const int r = n - 1;
-      const bool isfg = f.mask[r] != 0;
-      chain[len++] = isfg ? r : r - 1;
-    }
+    for (int n = node; n != 0 && len < kMaxDepth; n = parent_of(f, a.cw, n)) chain[len++] = disc_key(f, n);
     for (int k = 0; k < len; ++k) s_path[i][k] = chain[len - 1 - k];
     s_len[i] = len;
     if (len == kMaxDepth) {
@@ -1409,6 +1441,10 @@ __device__ __forceinline__ void finalize_frame(const KArgs& a, FrameWS& f, const
 __global__ __launch_bounds__(1024) void k_records(KArgs a) {
   __shared__ int s_sn[256], s_res[2];
   FrameWS f = frame_ws(a.ws, a.lay, a.B, blockIdx.x);
+  if (f.flag[1]) {  // root pool exhausted (adversarial batch): flagged, no records
+    if (threadIdx.x == 0) a.records[(size_t)blockIdx.x * (1 + 5 * a.K)] = __builtin_nanf("");
+    return;
+  }
   f.fb = f.flag[0];
   assign_frame(a, f, s_sn, s_res);
   finalize_frame(a, f, s_sn, s_res);
@@ -1417,15 +1453,15 @@ __global__ __launch_bounds__(1024) void k_records(KArgs a) {
 }  // namespace
 
 size_t post_workspace_bytes(int B, int H, int W, int K, int num_bins) {
-  return layout(H, W, K, num_bins).total(B);
+  return layout(B, H, W, K, num_bins).total(B);
 }
 
 void postprocess(const PostParams& p, hipStream_t s) {
   if (p.K > 256) throw std::invalid_argument("postprocess: K > 256");
   if (p.H > 65535 || p.W > 65535)  // k_accum's 32-bit wave sums of 6x + 3 pieces
     throw std::invalid_argument("postprocess: maps larger than 65535 pixels per side");
-  if (((long long)p.crop_h * p.crop_w + 1) * p.num_bins * 2 >= (1ll << 31))  // k_accum's histogram keys
-    throw std::invalid_argument("postprocess: crop * classes too large for 32-bit histogram keys");
+  if (((long long)layout(p.B, p.H, p.W, p.K, p.num_bins).P + 1) * p.num_bins * 2 >= (1ll << 31))  // histogram keys
+    throw std::invalid_argument("postprocess: root pool * classes too large for 32-bit histogram keys");
   if (p.crop_h > p.H || p.crop_w > p.W || p.crop_h <= 0 || p.crop_w <= 0)
     throw std::invalid_argument("postprocess: bad crop");
   if (p.accum < 0 || p.accum > 2) throw std::invalid_argument("postprocess: accum 0 (strips), 1 (32^2 tiles), 2 (64^2)");
@@ -1434,7 +1470,7 @@ void postprocess(const PostParams& p, hipStream_t s) {
   a.B = p.B; a.H = p.H; a.W = p.W; a.ch = p.crop_h; a.cw = p.crop_w;
   a.thr = p.thr; a.K = p.K; a.bins = p.num_bins; a.min_area = p.min_area;
   a.ws = static_cast<char*>(p.ws);
-  a.lay = layout(p.H, p.W, p.K, p.num_bins);
+  a.lay = layout(p.B, p.H, p.W, p.K, p.num_bins);
   a.records = p.records;
   a.dbg = 0;
 #ifdef SSA_POST_DEBUG
@@ -1464,13 +1500,11 @@ void postprocess(const PostParams& p, hipStream_t s) {
   if (st++ < stages) hipLaunchKernelGGL(k_ccl_local, gt, dim3(kCclThreads), 0, s, a, p.palette);
   {
     const int tx_n = cdiv(p.crop_w, TW), ty_n = cdiv(p.crop_h, TH);
-    const int nt = tx_n * ty_n;
     const int lines = (ty_n - 1) + 2 + 2 * (tx_n - 1) + 2;
     if (st++ < stages)
       hipLaunchKernelGGL(k_ccl_edges, dim3(cdiv(std::max(p.crop_w, p.crop_h), kEdgeThreads), lines, p.B),
                          dim3(kEdgeThreads), 0, s, a);
-    const size_t lds = (size_t)(nt + 1 + 1024 + 2 * (kMergeCap + 1) + 1) * 4;
-    if (lds > 160 * 1024) throw std::invalid_argument("postprocess: crop too large for the LDS merge");
+    const size_t lds = (size_t)(2 * (kMergeCap + 1) + 3) * 4;
     static bool attr = false;
     if (!attr) {
       check(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ccl_merge),
@@ -1480,7 +1514,7 @@ void postprocess(const PostParams& p, hipStream_t s) {
     }
     if (st++ < stages) hipLaunchKernelGGL(k_ccl_merge, dim3(p.B), dim3(1024), lds, s, a);
     if (st++ < stages) {  // no-ops unless k_ccl_merge flagged the frame (caps exceeded)
-      const dim3 gfb(std::min(kFbBlocks, cdiv(N, 256)), p.B);
+      const dim3 gfb(std::min(kFbBlocks, cdiv(N, 256)));
       hipLaunchKernelGGL(k_fb_unite, gfb, dim3(256), 0, s, a);
       hipLaunchKernelGGL(k_fb_relabel, gfb, dim3(256), 0, s, a);
     }

@@ -122,13 +122,29 @@ int main(int argc, char** argv) {
     p.palette = dpal; p.thr = 127; p.min_area = 0.002 * H * W; p.num_bins = bins; p.K = K;
     p.ws = ws; p.records = drec;
     p.accum = getenv("SSA_POST_ACCUM") ? atoi(getenv("SSA_POST_ACCUM")) : 1;
-    for (int i = 0; i < 3; ++i) postprocess(p, s);
-    chk(hipEventRecord(e0, s), "rec");
-    for (int i = 0; i < reps; ++i) postprocess(p, s);
-    chk(hipEventRecord(e1, s), "rec");
-    chk(hipEventSynchronize(e1), "sync");
-    float ms = 0;
-    chk(hipEventElapsedTime(&ms, e0, e1), "elapsed");
+    auto timed = [&]() {
+      for (int i = 0; i < 3; ++i) postprocess(p, s);
+      chk(hipEventRecord(e0, s), "rec");
+      for (int i = 0; i < reps; ++i) postprocess(p, s);
+      chk(hipEventRecord(e1, s), "rec");
+      chk(hipEventSynchronize(e1), "sync");
+      float ms = 0;
+      chk(hipEventElapsedTime(&ms, e0, e1), "elapsed");
+      return ms;
+    };
+    if (getenv("SSA_POST_STAGEWISE")) {  // debug builds: cumulative time of the first n launches
+      float prev = 0;
+      for (int n = 1; n <= 6; ++n) {
+        char v[8];
+        snprintf(v, sizeof v, "%d", n);
+        setenv("SSA_POST_STAGES", v, 1);
+        const float t = timed() * 1e3f / reps;
+        printf("  %-8s stages<=%d %8.1f us/call (+%.1f)\n", names[kind], n, t, t - prev);
+        prev = t;
+      }
+      unsetenv("SSA_POST_STAGES");
+    }
+    const float ms = timed();
     chk(hipMemcpy(rec.data(), drec, rec.size() * 4, hipMemcpyDeviceToHost), "rec");
     double nrec = 0, chks = 0;
     for (int b = 0; b < B; ++b) {

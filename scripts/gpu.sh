@@ -22,6 +22,8 @@
 #   share8 / share:N  the dpN bench path with N ranks sharing this one GPU (SSA_SHARE_GPU=1, gloo;
 #                completes end to end -- its throughput is not a scaling number)
 #   postab       post-processing harness (tools/bin/post_bench), strips vs 32^2 / 64^2 tile accumulation
+#   postvar      every tools/bin/pb_* variant (scripts/post_variants.sh) on the bench model's own label
+#                maps + the synthetic kinds (POST_DBG_LIST: SSA_POST_DBG values; STAGEWISE=1: per launch)
 #   posttrace    post_bench (4 map kinds incl. the fallback-path lattice) under a kernel trace
 #   repro        packed-f32 co-residence reproducer, both builds (csrc/tools/packed_f32_repro.hip)
 #   retune:LIST  re-time the named choices (comma list) at B = ${TUNE_B:-32} on top of the committed
@@ -98,6 +100,12 @@ for step in "$@"; do
              cut -c1-600 $O/share$n.json ;;
     postab)  for m in 0 1 2; do SSA_POST_ACCUM=$m timeout -k 10 120 tools/bin/post_bench 50 > $O/post_accum$m.txt 2>&1 \
                || { tail -5 $O/post_accum$m.txt; exit 7; }; echo "accum=$m"; cat $O/post_accum$m.txt; done ;;
+    postvar) timeout -k 10 300 python scripts/label_stats.py /tmp/ssa_maps.bin > $O/label_stats.txt 2>&1 \
+               || { tail -5 $O/label_stats.txt; exit 7; }
+             for bin in tools/bin/pb_*; do for d in ${POST_DBG_LIST:-0}; do
+               SSA_POST_DBG=$d ${STAGEWISE:+SSA_POST_STAGEWISE=1} timeout -k 10 180 $bin ${POST_REPS:-30} /tmp/ssa_maps.bin \
+                 > $O/$(basename $bin)_d$d.txt 2>&1 || { tail -5 $O/$(basename $bin)_d$d.txt; exit 7; }
+               echo "== $bin dbg=$d"; cat $O/$(basename $bin)_d$d.txt; done; done ;;
     posttrace) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats \
                -d $REPO/$O/posttrace -o run --output-format csv -- $REPO/tools/bin/post_bench 20 \
                > $REPO/$O/posttrace.log 2>&1) || { tail -5 $O/posttrace.log; exit 7; }

@@ -37,6 +37,14 @@ log = logging.getLogger(__name__)
 
 
 _overflow_frames = 0
+_pool_exhausted_frames = 0
+
+
+def pool_exhausted_frames() -> int:
+    """Frames (process lifetime) that got no records because their batch's components
+    overflowed the device root pool (max(B * 8192, H * W + 1) components per batch;
+    postprocess.hip Layout): the record count comes back NaN."""
+    return _pool_exhausted_frames
 
 
 def overflow_frames() -> int:
@@ -49,8 +57,15 @@ def overflow_frames() -> int:
 def unpack_records(packed: np.ndarray, K: int, frame_ids, ts, streams) -> np.ndarray:
     """packed: (F, 1 + 5K) float32 -> RECORD_DTYPE rows in push order. A negative count
     marks a frame with more than K passing contours (|count| == K were kept)."""
-    global _overflow_frames
+    global _overflow_frames, _pool_exhausted_frames
     raw = packed[:, 0]
+    lost = np.isnan(raw)
+    if lost.any():  # the batch's components overflowed the device root pool (postprocess.hip)
+        if _pool_exhausted_frames == 0:
+            log.warning("a batch of label maps had more components than the device root pool "
+                        "holds; %d frame(s) returned no records", int(lost.sum()))
+        _pool_exhausted_frames += int(lost.sum())
+        raw = np.where(lost, 0.0, raw)
     over = int((raw < 0).sum())
     if over:
         if _overflow_frames == 0:

@@ -174,6 +174,22 @@ def test_unpack_records_order():
     assert r["label"].tolist() == [7, 15] and r["frame"].tolist() == [5, 5]
 
 
+def test_unpack_records_pool_exhausted():
+    """A NaN count (the device root pool overflowed for that frame) gives no records and is
+    counted, the other frames unpack as usual."""
+    from semantic_segmentation_server_amd.parallel import dp
+    K = 2
+    packed = np.zeros((3, 1 + 5 * K), np.float32)
+    packed[0, 0] = np.nan
+    packed[1, 0] = 1
+    packed[1, 1:6] = [9, 1, 0.1, 0.2, 0.3]
+    packed[2, 0] = -2
+    before = dp.pool_exhausted_frames()
+    r = dp.unpack_records(packed, K, [1, 2, 3], [0.0] * 3, [0] * 3)
+    assert r["frame"].tolist() == [2, 3, 3] and r["label"][0] == 9
+    assert dp.pool_exhausted_frames() == before + 1
+
+
 def _serve_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))

@@ -103,3 +103,18 @@ def test_letterbox_crop_geometry():
     assert R.letterbox_geometry(640, 480, 513, 513) == (513, 384, 513, 384)
     assert R.letterbox_geometry(480, 640, 513, 513) == (384, 513, 384, 513)
     assert R.letterbox_geometry(640, 480, 513, 513, keep_aspect_ratio=False) == (513, 513, 513, 513)
+
+
+def test_device_post_workspace_is_compact():
+    """the device post-processing workspace keeps per component state in a
+    batch-shared root pool indexed by label, not per raster pixel: <= 4 MB per 513^2 frame
+    at the bench batch (round 4: ~46 MB), with a floor that still holds any single frame."""
+    hip_ops = pytest.importorskip("semantic_segmentation_server_amd.ops.hip_ops")
+    try:
+        per32 = hip_ops.post_workspace_bytes(32, 513, 513, 64, 21) / 32
+        one = hip_ops.post_workspace_bytes(1, 513, 513, 64, 21)
+    except Exception as e:  # pragma: no cover - extension not built
+        pytest.skip(f"HIP extension unavailable: {e}")
+    assert per32 <= 4 * 2 ** 20, per32
+    # pool floor: H * W + 1 components (more than any frame can have), ~112 B each
+    assert one >= (513 * 513 + 1) * (24 + 4 * 21)
