@@ -44,9 +44,12 @@ struct FrameWS {
   int32_t* slot_node;  // [K]
   int32_t* cidx;       // [N] per tile-local root pixel: its compact index (k_ccl_local), after
                        //     k_ccl_merge its final label; per component root (fallback): its label
-  int32_t* rootpix;    // [kMergeCap] raster index of each compact tile-local root
+  int32_t* rootpix;    // [ntiles][kTileCap] raster index of each tile-local root (tile-local index
+                       //     c < kTileCap; the rest go to rovf)
+  int32_t* ntroot;     // [ntiles] tile-local roots per tile
+  int32_t* rovf;       // [kOvfCap][2] (tile * kTileRoots + c, raster index) of roots past kTileCap
   int32_t* flag;       // [8]: [0] = 1 -> global union-find fallback, [1] = 1 -> root pool exhausted
-                       //      (no records), [2] tile-local roots (k_ccl_local -> k_ccl_merge, which
+                       //      (no records), [2] rovf entries (k_ccl_local -> k_ccl_merge, which
                        //      re-zeroes it), [3] the frame's first pool entry
   int32_t* edges;      // [kEdgeCap][2] cross-tile unions (compact root pairs as raster, -1 = outside)
   // root pool, shared by the batch and indexed by component label - 1 (labels are pool
@@ -66,6 +69,9 @@ struct FrameWS {
 #endif
 constexpr int TW = 32, TH = SSA_CCL_TH;  // local CCL tile
 constexpr int kMergeCap = 12288;     // tile-local roots the per-frame LDS merge handles
+constexpr int kTileRoots = TW * TH;  // worst case roots per tile
+constexpr int kTileCap = 64;         // roots per tile with a rootpix slot (the rest: rovf)
+constexpr int kOvfCap = 4096;        // rovf entries per frame (more: the fallback path)
 constexpr int kEdgeCap = 1 << 15;    // cross-tile union pairs per frame
 constexpr int kPoolPerFrame = 8192;  // root pool entries per frame of the batch (floor: N + 1)
 
@@ -79,7 +85,7 @@ constexpr int kPoolPerFrame = 8192;  // root pool entries per frame of the batch
 // count NaN; never on segmentation maps -- the bench frames have ~200 components each).
 // Round 4 indexed every per-root array by raster index: 46 MB per 513^2 frame.
 struct Layout {
-  size_t N, K, bins, P;
+  size_t N, K, bins, P, ntiles;
   size_t small_bytes;  // nslot(16) + slot_node, per frame (zeroed every call)
   size_t big_bytes;    // per frame
   size_t pool_bytes;   // per batch
@@ -94,8 +100,10 @@ Layout layout(int B, int H, int W, int K, int bins) {
   l.K = K;
   l.bins = bins;
   l.P = std::max((size_t)B * kPoolPerFrame, l.N + 1);
+  l.ntiles = (size_t)((W + TW - 1) / TW) * ((H + TH - 1) / TH);
   l.small_bytes = al(16 + (size_t)K * 4);
-  l.big_bytes = al((l.N + 1) * 4) + al(l.N) + al(l.N * 4) + al((size_t)kMergeCap * 4) + al(32) +
+  l.big_bytes = al((l.N + 1) * 4) + al(l.N) + al(l.N * 4) + al(l.ntiles * kTileCap * 4) + al(l.ntiles * 4) +
+                al((size_t)kOvfCap * 8) + al(32) +
                 al((size_t)kEdgeCap * 8);
   l.pool_bytes = 2 * al(l.P * 8) + 3 * al(l.P * 4) + al(l.P * bins * 4);
   return l;
@@ -112,7 +120,9 @@ __host__ __device__ inline FrameWS frame_ws(char* ws, const Layout& l, int B, in
   f.L = reinterpret_cast<int32_t*>(p); p += al((l.N + 1) * 4);
   f.mask = reinterpret_cast<uint8_t*>(p); p += al(l.N);
   f.cidx = reinterpret_cast<int32_t*>(p); p += al(l.N * 4);
-  f.rootpix = reinterpret_cast<int32_t*>(p); p += al((size_t)kMergeCap * 4);
+  f.rootpix = reinterpret_cast<int32_t*>(p); p += al(l.ntiles * kTileCap * 4);
+  f.ntroot = reinterpret_cast<int32_t*>(p); p += al(l.ntiles * 4);
+  f.rovf = reinterpret_cast<int32_t*>(p); p += al((size_t)kOvfCap * 8);
   f.flag = reinterpret_cast<int32_t*>(p); p += al(32);
   f.edges = reinterpret_cast<int32_t*>(p);
   char* q = hdr + 256 + (size_t)B * l.big_bytes;
@@ -251,7 +261,9 @@ __global__ __launch_bounds__(kCclThreads) void k_ccl_local(KArgs a, const int32_
   __shared__ int hs[HH2 * TW];  // packed horizontal 3-sums
   __shared__ int lbl[TW * TH];
   __shared__ unsigned fgrow[TH], bgrow[TH];
+  __shared__ int s_nroot;
   const int tid = threadIdx.x;
+  if (tid == 0) s_nroot = 0;
   for (int i = tid; i < 256; i += kCclThreads)
     spal[i] = (pal[3 * i] & 255) | (pal[3 * i + 1] & 255) << 10 | (pal[3 * i + 2] & 255) << 20;
   const int b = blockIdx.z;
@@ -342,32 +354,30 @@ __global__ __launch_bounds__(kCclThreads) void k_ccl_local(KArgs a, const int32_
     }
   }
   __syncthreads();
-  const int lane = tid & 63;
+  const int tile = blockIdx.y * gridDim.x + blockIdx.x;
 #pragma unroll
   for (int k = 0; k < RPT; ++k) {
     const int ty = ty0 + k * RS, y = y0 + ty, me = ty * TW + tx;
-    bool root = false;
-    if (in[k]) {
-      const int r = lfind(lbl, start[k]);
-      const int rx = x0 + r % TW, ry = y0 + r / TW;
-      f.L[y * a.cw + x + 1] = ry * a.cw + rx + 1;
-      root = r == me;
-    }
-    // tile-local roots get frame-wide compact indices for the merge: one atomic per wave
-    // (flag[2] is zeroed again by k_ccl_merge, its reader)
-    const unsigned long long rb = __ballot(root);
-    if (rb) {
-      const int leader = __ffsll((long long)rb) - 1;
-      int base = 0;
-      if (lane == leader) base = atomicAdd(f.flag + 2, __popcll(rb));
-      base = __shfl(base, leader, 64);
-      if (root) {
-        const int c = base + __popcll(rb & ((1ull << lane) - 1));
-        f.cidx[y * a.cw + x] = c;
-        if (c < kMergeCap) f.rootpix[c] = y * a.cw + x;
+    if (!in[k]) continue;
+    const int r = lfind(lbl, start[k]);
+    const int rx = x0 + r % TW, ry = y0 + r / TW;
+    f.L[y * a.cw + x + 1] = ry * a.cw + rx + 1;
+    if (r == me) {  // tile-local root: numbered within the tile (k_ccl_merge scans the counts)
+      const int c = atomicAdd(&s_nroot, 1);
+      f.cidx[y * a.cw + x] = c;
+      if (c < kTileCap) {
+        f.rootpix[tile * kTileCap + c] = y * a.cw + x;
+      } else {  // a crowded tile: listed (rare; a frame past kOvfCap takes the fallback)
+        const int o = atomicAdd(f.flag + 2, 1);
+        if (o < kOvfCap) {
+          f.rovf[2 * o] = tile * kTileRoots + c;
+          f.rovf[2 * o + 1] = y * a.cw + x;
+        }
       }
     }
   }
+  __syncthreads();
+  if (tid == 0) f.ntroot[tile] = s_nroot;
 }
 
 // ---------------------------------------------------------------- compact merge
@@ -390,8 +400,9 @@ __global__ __launch_bounds__(kCclThreads) void k_ccl_local(KArgs a, const int32_
 // k_ccl_merge flags them and two grid kernels (k_fb_unite, k_fb_relabel) do the work,
 // leaving at once for unflagged frames; fin() then reads the final label straight from L.
 // (Round 3 ran the fallback inside the merge workgroup: 813 us per flagged frame.)
-__device__ __forceinline__ void emit_pairs(FrameWS& f, int n, const int (&pa)[3], const int (&pb)[3]) {
-  // wave-aggregated append of this lane's n pairs
+// wave-aggregated append of this lane's kept pairs (me, o0..o2; k0..k2 = kept)
+__device__ __forceinline__ void emit_pairs(FrameWS& f, int me, int o0, int o1, int o2, bool k0, bool k1, bool k2) {
+  const int n = (int)k0 + (int)k1 + (int)k2;
   int incl = n;
   const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -404,13 +415,17 @@ __device__ __forceinline__ void emit_pairs(FrameWS& f, int n, const int (&pa)[3]
   int base = 0;
   if (lane == 63) base = atomicAdd(f.nslot + 2, total);
   base = __shfl(base, 63, 64);
-  const int at = base + incl - n;
-  for (int k = 0; k < n; ++k) {
-    if (at + k < kEdgeCap) {
-      f.edges[2 * (at + k)] = pa[k];
-      f.edges[2 * (at + k) + 1] = pb[k];
+  int at = base + incl - n;
+  auto put = [&](int o) {
+    if (at < kEdgeCap) {
+      f.edges[2 * at] = me;
+      f.edges[2 * at + 1] = o;
     }
-  }
+    ++at;
+  };
+  if (k0) put(o0);
+  if (k1) put(o1);
+  if (k2) put(o2);
 }
 
 constexpr int kEdgeThreads = 256;
@@ -447,60 +462,43 @@ __global__ __launch_bounds__(kEdgeThreads) void k_ccl_edges(KArgs a) {
                        !(kind == 3 && fixed + 1 >= a.cw);
     const int x = horiz ? i : fixed, y = horiz ? fixed : i;
     const int p = y * a.cw + x;
-    int pa[3] = {0, 0, 0}, pb[3] = {0, 0, 0};
-    int n = 0;
+    // up to three partners of this pixel's tile-local root across the edge (-2 = none)
+    int me = -2, o0 = -2, o1 = -2, o2 = -2;
     if (valid) {
       const bool m = f.mask[p] != 0;
-      const int me = f.L[p + 1] - 1;
-      auto add = [&](int other) {  // distinct partners only
-        for (int k = 0; k < n; ++k)
-          if (pb[k] == other) return;
-        pa[n] = me;
-        pb[n] = other;
-        ++n;
-      };
+      me = f.L[p + 1] - 1;
       auto lr = [&](int q) { return f.L[q + 1] - 1; };
       if (kind == 0) {  // top row of a tile: unions with the row above
         const int up = p - a.cw;
         if (m) {
-          if (x > 0 && f.mask[up - 1]) add(lr(up - 1));
-          if (f.mask[up]) add(lr(up));
-          if (x + 1 < a.cw && f.mask[up + 1]) add(lr(up + 1));
+          if (x > 0 && f.mask[up - 1]) o0 = lr(up - 1);
+          if (f.mask[up]) o1 = lr(up);
+          if (x + 1 < a.cw && f.mask[up + 1]) o2 = lr(up + 1);
         } else if (!f.mask[up]) {
-          add(lr(up));
+          o0 = lr(up);
         }
       } else if (kind == 2) {  // left column of a tile: unions with the column to the left
         if (m) {
-          if (f.mask[p - 1]) add(lr(p - 1));
-          if (y > 0 && (y % TH) != 0 && f.mask[p - a.cw - 1]) add(lr(p - a.cw - 1));
+          if (f.mask[p - 1]) o0 = lr(p - 1);
+          if (y > 0 && (y % TH) != 0 && f.mask[p - a.cw - 1]) o1 = lr(p - a.cw - 1);
         } else if (!f.mask[p - 1]) {
-          add(lr(p - 1));
+          o0 = lr(p - 1);
         }
       } else if (kind == 3) {  // right column: up-right diagonal into the next tile
-        if (m && y > 0 && (y % TH) != 0 && f.mask[p - a.cw + 1]) add(lr(p - a.cw + 1));
+        if (m && y > 0 && (y % TH) != 0 && f.mask[p - a.cw + 1]) o0 = lr(p - a.cw + 1);
       }
-      if ((kind == 1 || kind == 4) && !m) add(-1);  // image-border background -> outside
+      if ((kind == 1 || kind == 4) && !m) o0 = -1;  // image-border background -> outside
     }
-    // drop pairs the previous lane (previous pixel along this line) also emitted
+    // distinct partners only, and drop pairs the previous lane (previous pixel along this
+    // line) also emitted
     const int lane = threadIdx.x & 63;
-    const int qa0 = __shfl_up(pa[0], 1, 64), qb0 = __shfl_up(pb[0], 1, 64);
-    const int qa1 = __shfl_up(pa[1], 1, 64), qb1 = __shfl_up(pb[1], 1, 64);
-    const int qa2 = __shfl_up(pa[2], 1, 64), qb2 = __shfl_up(pb[2], 1, 64);
-    const int qn = __shfl_up(n, 1, 64);
-    int keep = 0;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      if (k < n) {
-        bool dup = false;
-        if (lane > 0) {
-          dup |= qn > 0 && qa0 == pa[k] && qb0 == pb[k];
-          dup |= qn > 1 && qa1 == pa[k] && qb1 == pb[k];
-          dup |= qn > 2 && qa2 == pa[k] && qb2 == pb[k];
-        }
-        if (!dup) { pa[keep] = pa[k]; pb[keep] = pb[k]; ++keep; }
-      }
-    }
-    emit_pairs(f, keep, pa, pb);
+    const int pm = __shfl_up(me, 1, 64);
+    const int p0 = __shfl_up(o0, 1, 64), p1 = __shfl_up(o1, 1, 64), p2 = __shfl_up(o2, 1, 64);
+    auto seen = [&](int o) { return lane > 0 && pm == me && (o == p0 || o == p1 || o == p2); };
+    const bool k0 = o0 != -2 && !seen(o0);
+    const bool k1 = o1 != -2 && o1 != o0 && !seen(o1);
+    const bool k2 = o2 != -2 && o2 != o0 && o2 != o1 && !seen(o2);
+    emit_pairs(f, me, o0, o1, o2, k0, k1, k2);
   }
 }
 
@@ -520,15 +518,41 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(KArgs a) {
   extern __shared__ int sm[];
   const int b = blockIdx.x;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
-  const int cw = a.cw;
+  const int cw = a.cw, ch = a.ch;
+  const int tx_n = (cw + TW - 1) / TW, ty_n = (ch + TH - 1) / TH;
+  const int nt = tx_n * ty_n;
   const int tid = threadIdx.x;
   int* par = sm;                    // [kMergeCap + 1] (last = outside)
   int* minr = par + kMergeCap + 1;  // [kMergeCap + 1] set minimum pixel, then the set's label
-  int* s_c = minr + kMergeCap + 1;  // [0] components, [1] listed, [2] pool base (-1: exhausted)
-  const int R = f.flag[2];
-  const int E = f.nslot[2];
+  int* rp = minr + kMergeCap + 1;   // [kMergeCap] raster index of compact root i
+  int* toff = rp + kMergeCap;       // [nt + 1]
+  int* part = toff + nt + 1;        // [1024] scan partials
+  int* s_c = part + 1024;           // [0] components, [1] listed, [2] pool base (-1: exhausted)
   if (tid == 0) { s_c[0] = 0; s_c[1] = 0; }
-  if (R > kMergeCap || E > kEdgeCap) {  // k_fb_unite / k_fb_relabel take the frame
+  // exclusive scan of the per-tile root counts: compact index = tile offset + tile-local index
+  const int per = (nt + 1023) / 1024;
+  const int t0 = tid * per, t1 = min(nt, t0 + per);
+  int sum = 0;
+  for (int t = t0; t < t1; ++t) sum += f.ntroot[t];
+  part[tid] = sum;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int v = tid >= o ? part[tid - o] : 0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  int acc = part[tid] - sum;
+  for (int t = t0; t < t1; ++t) {
+    toff[t] = acc;
+    acc += f.ntroot[t];
+  }
+  if (tid == 1023) toff[nt] = part[1023];
+  __syncthreads();
+  const int R = toff[nt];
+  const int E = f.nslot[2];
+  const int O = f.flag[2];
+  if (R > kMergeCap || E > kEdgeCap || O > kOvfCap) {  // k_fb_unite / k_fb_relabel take the frame
     if (tid == 0) {
       // reserve the tile-local root count (>= its components) from the pool
       const int base = atomicAdd(f.pool, R);
@@ -540,17 +564,37 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(KArgs a) {
     return;
   }
   const int OUT = R;
+  auto tile_of = [&](int i) {  // last tile t with toff[t] <= i (empty tiles share offsets)
+    int lo = 0, hi = nt - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (toff[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+  };
   for (int i = tid; i <= R; i += 1024) {
     par[i] = i;
     minr[i] = 0x7fffffff;
+    if (i < R) {
+      const int t = tile_of(i), c = i - toff[t];
+      if (c < kTileCap) rp[i] = f.rootpix[t * kTileCap + c];
+    }
+  }
+  for (int o = tid; o < O; o += 1024) {
+    const int key = f.rovf[2 * o], t = key / kTileRoots;
+    rp[toff[t] + key - t * kTileRoots] = f.rovf[2 * o + 1];
   }
   __syncthreads();
+  auto compact = [&](int r) {
+    const int ly = r / cw, lx = r - ly * cw;
+    return toff[(ly / TH) * tx_n + lx / TW] + f.cidx[r];
+  };
   for (int e = tid; e < E; e += 1024) {
     const int ra = f.edges[2 * e], rb = f.edges[2 * e + 1];
-    lunite(par, f.cidx[ra], rb < 0 ? OUT : f.cidx[rb]);
+    lunite(par, compact(ra), rb < 0 ? OUT : compact(rb));
   }
   __syncthreads();
-  for (int i = tid; i < R; i += 1024) atomicMin(&minr[lfind(par, i)], f.rootpix[i]);
+  for (int i = tid; i < R; i += 1024) atomicMin(&minr[lfind(par, i)], rp[i]);
   __syncthreads();
   const int outroot = lfind(par, OUT);
   // every set but the outside one is a component: count, take a run of the pool, list
@@ -582,7 +626,7 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(KArgs a) {
   // final label of every tile-local root, over its cidx entry (the compact indices are done)
   for (int i = tid; i < R; i += 1024) {
     const int r = lfind(par, i);
-    f.cidx[f.rootpix[i]] = r == outroot ? 0 : minr[r];
+    f.cidx[rp[i]] = r == outroot ? 0 : minr[r];
   }
   __syncthreads();
   // border-tree parent of every root: the final label of the pixel left of it
@@ -1033,25 +1077,96 @@ __global__ __launch_bounds__(kAccThreads) void k_accum(KArgs a) {
   }
 }
 
-// Tile variant of k_accum (round 4): one 256-thread block per 32 x 32 CCL tile of a frame.
-// The strip kernel resolves every label it touches through the dependent global chain
-// L -> tile-local root -> cidx (fin()), per 256-pixel round, for the quad corners and again
-// in the hole-ring checks; round 3's ablations put ~60 of its ~112 us per 32 frames on those
-// loads. Here the block stages the final labels, the mask and the classes of its tile plus
-// the halo the per-pixel logic reads (2 columns left / right, 2 rows above, 1 below) in LDS
-// first -- every global load of the chain issued at once, one round trip per chain level
-// for the whole tile -- and the per-pixel logic below is k_accum's, reading LDS. Same
-// pieces, same keys, same hash-table flush: identical sums.
-// AT = 64 (accum mode 2): a quarter of the blocks, so a quarter of the per-(block, component)
-// flushes -- single-lane global atomics up the border tree, one per ancestor level -- for
-// the same per-pixel work.
+// Tile variant of k_accum (round 4; round 5 tables): one 256-thread block per AT x AT tile
+// of a frame. The strip kernel resolves every label it touches through the dependent global
+// chain L -> tile-local root -> cidx (fin()), per 256-pixel round; here the block stages the
+// final labels, the mask and the classes of its tile plus the halo the per-pixel logic reads
+// (2 columns left / right, 2 rows above, 1 below) in LDS first -- every global load of the
+// chain issued at once, one round trip per chain level for the whole tile -- and the
+// per-pixel logic below is k_accum's, reading LDS: same pieces, same sums.
+// Round 5 (ablations on the bench model's own label maps, profiles/r5n_post_ablation.txt:
+// moments 29 us, flush 19 us, class histogram 13 us, hole rings 10 us of 83 us per 32
+// frames): the block's components get SLOTS of one small table (key = label); moments are
+// wave-summed with DPP row adds + 4 readlanes (no ds_bpermute chains) and added to the slot;
+// class counts go to a dense [slot][class] LDS counter (own pixels in the low 16 bits, hole
+// rings in the high 16: no (node, class) hash probing, one single-lane atomic per distinct
+// class of a node-uniform wave); the flush walks each slot's border-tree ancestors ONCE
+// (one lane per slot, cached in LDS) and then issues only fire-and-forget atomics.
+constexpr int kTSlots = 64;      // components per block in the table (more: global atomics)
+constexpr int kDenseBins = 32;   // dense class counters per slot (bins <= 32; else k_accum)
+constexpr int kAnc = 8;          // ancestors cached per slot
+
+struct TileAcc {
+  int key[kTSlots];  // component label, 0 = free
+  int s00[kTSlots];
+  unsigned s10[kTSlots], s01[kTSlots];  // a tile's sums stay < 2^31 (<= 4096 quads x 6x+3, x < 65536)
+  int hist[kTSlots * kDenseBins];  // own count | ring count << 16 (both < 2^16 per tile)
+  int anc[kTSlots][kAnc];
+  int nanc[kTSlots], deep[kTSlots];
+};
+
+// Sum over the 64 lanes (all lanes active): quad and row butterflies in DPP, then the four
+// row sums by readlane (wave-uniform result).
+__device__ __forceinline__ int wave_sum(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xf, 0xf, false);  // row_ror:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xf, 0xf, false);  // row_ror:8
+  return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) +
+         __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
+}
+
+// slot of component `node` (inserted if new), -1 if the table's probe window is full
+__device__ __forceinline__ int tslot(TileAcc& T, int node) {
+  int h = (int)(((unsigned)node * 2654435761u) >> 26) & (kTSlots - 1);
+#pragma unroll 1
+  for (int probe = 0; probe < 16; ++probe, h = (h + 1) & (kTSlots - 1)) {
+    int k = __hip_atomic_load(&T.key[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (k == 0) k = atomicCAS(&T.key[h], 0, node);
+    if (k == 0 || k == node) return h;
+  }
+  return -1;
+}
+
+__device__ __forceinline__ void tmom(TileAcc& T, FrameWS& f, int cw, int node, int d00, int d10, int d01) {
+  const int h = tslot(T, node);
+  if (h < 0) {
+    moments_up(f, cw, node, d00, d10, d01, 65536);
+    return;
+  }
+  atomicAdd(&T.s00[h], d00);
+  atomicAdd(&T.s10[h], (unsigned)d10);
+  atomicAdd(&T.s01[h], (unsigned)d01);
+}
+
+// wave-aggregated moments piece (node 0 = none); wave-uniform control flow
+__device__ __forceinline__ void tagg(TileAcc& T, FrameWS& f, int cw, int node, int d00, int d10, int d01) {
+  const unsigned long long act = __ballot(node > 0);
+  if (act == 0) return;
+  const int leader = __ffsll((long long)act) - 1;
+  const int lnode = __builtin_amdgcn_readlane(node, leader);
+  if (__all(node <= 0 || node == lnode)) {
+    // one quad's pieces are < 2^19 (6x + 3, x < 65536): a 64-lane sum fits in 32 bits
+    const bool on = node > 0;
+    const int s00 = wave_sum(on ? d00 : 0), s10 = wave_sum(on ? d10 : 0), s01 = wave_sum(on ? d01 : 0);
+    if ((int)(threadIdx.x & 63) == leader) tmom(T, f, cw, lnode, s00, s10, s01);
+  } else if (node > 0) {
+    tmom(T, f, cw, node, d00, d10, d01);
+  }
+}
+
+// global class count (table full): own counts up the ancestors, ring counts to the node
+__device__ __forceinline__ void hist_global(FrameWS& f, int cw, int bins, int node, int c, int cnt, bool ring) {
+  hist_up(f, cw, bins, (node * bins + c) * 2 + (ring ? 1 : 0), cnt, 65536);
+}
+
 template <int AT>
 __global__ __launch_bounds__(256) void k_accum_tiles(KArgs a) {
   constexpr int kAT = AT;                            // accumulation tile (32 = the CCL tile width)
   constexpr int kARW = kAT + 4, kARH = kAT + 3;      // staged region incl. the halo
   constexpr int kARN = kARW * kARH;
   constexpr int kAPT = (kARN + 255) / 256;           // staged pixels per thread
-  __shared__ AccTable T;
+  __shared__ TileAcc T;
   __shared__ int sfin[kARN];
   __shared__ uint8_t smask[kARN], scls[kARN];
   const int b = blockIdx.z;
@@ -1060,14 +1175,11 @@ __global__ __launch_bounds__(256) void k_accum_tiles(KArgs a) {
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
   if (f.flag[1]) return;  // root pool exhausted: no records for this frame
   f.fb = f.flag[0];
-  const int tid = threadIdx.x;
-  for (int i = tid; i < kHash; i += 256) {
-    T.q.key[i] = 0; T.q.s00[i] = 0; T.q.s10[i] = 0; T.q.s01[i] = 0;
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (int i = tid; i < kTSlots; i += 256) {
+    T.key[i] = 0; T.s00[i] = 0; T.s10[i] = 0; T.s01[i] = 0;
   }
-  for (int i = tid; i < kHistHash; i += 256) {
-    T.hkey[i] = 0; T.hcnt[i] = 0;
-  }
-  if (tid == 0) T.maxd = 65536;
+  for (int i = tid; i < kTSlots * kDenseBins; i += 256) T.hist[i] = 0;
   const uint8_t* lab = a.labels + (size_t)b * a.H * a.W;
   {  // stage: all first-level loads, then all second-level (cidx) loads
     int lv[kAPT];
@@ -1101,18 +1213,16 @@ __global__ __launch_bounds__(256) void k_accum_tiles(KArgs a) {
   for (int k = 0; k < kAT * kAT / 256; ++k) {
     const int x = x0 + tx, y = y0 + ty0 + (256 / kAT) * k;
     const bool own = x < cw && y < ch;
-    int fnode = 0, f00 = 0;
-    long long f10 = 0, f01 = 0;
-    int bn[2] = {0, 0}, b00[2] = {0, 0};
-    long long b10[2] = {0, 0}, b01[2] = {0, 0};
-    int hkey = 0, rkey[4] = {0, 0, 0, 0};
+    // pieces in 32 bits: 6x + 3 < 2^19 for x < 65536
+    int fnode = 0, f00 = 0, f10 = 0, f01 = 0;
+    int bn[2] = {0, 0}, b00[2] = {0, 0}, b10[2] = {0, 0}, b01[2] = {0, 0};
+    int np = 0, c = 0, rc[4] = {-1, -1, -1, -1};
     if (own) {
       const int i0 = LI(x, y);
       const bool m0 = smask[i0] != 0;
       const int n0 = sfin[i0];
-      const int np = n0;
-      const int c = scls[i0];
-      if (np != 0) hkey = (np * bins + c) * 2;
+      np = n0;
+      c = scls[i0];
       if (x + 1 < cw && y + 1 < ch) {
         const int TX[4] = {1, 2, 1, 2}, TY[4] = {1, 1, 2, 2};
         const int node[4] = {n0, sfin[i0 + 1], sfin[i0 + kARW], sfin[i0 + kARW + 1]};
@@ -1122,7 +1232,7 @@ __global__ __launch_bounds__(256) void k_accum_tiles(KArgs a) {
         for (int q = 0; q < 4; ++q) {
           if (fg[q]) { ++nf; fnode = node[q]; } else { missing = q; }
         }
-        const long long X = x, Y = y;
+        const int X = x, Y = y;
         if (nf == 4) {
           f00 = 2; f10 = 6 * X + 3; f01 = 6 * Y + 3;
         } else if (nf == 3) {
@@ -1154,7 +1264,7 @@ __global__ __launch_bounds__(256) void k_accum_tiles(KArgs a) {
         }
       }
       // hole rings, counted from the hole side exactly as in k_accum
-      if (!m0 && np != 0) {
+      if (!m0 && np != 0 && !(a.dbg & 2)) {
         const int nx[4] = {x - 1, x + 1, x, x}, ny[4] = {y, y, y - 1, y + 1};
         const bool okn[4] = {x > 0, x + 1 < cw, y > 0, y + 1 < ch};
         bool fgn[4], any = false;
@@ -1189,27 +1299,89 @@ __global__ __launch_bounds__(256) void k_accum_tiles(KArgs a) {
               if (!smask[iq] && sfin[iq] == np) first = false;
             }
             if (sfin[ir] != par || !first) continue;
-            rkey[q] = (np * bins + scls[ir]) * 2 + 1;
+            rc[q] = scls[ir];
           }
         }
       }
     }
-    agg_add(T, f, cw, fnode, f00, f10, f01);
-    agg_add(T, f, cw, bn[0], b00[0], b10[0], b01[0]);
-    agg_add(T, f, cw, bn[1], b00[1], b10[1], b01[1]);
-    hagg(T, f, cw, bins, hkey);
+    if (!(a.dbg & 8)) {
+      tagg(T, f, cw, fnode, f00, f10, f01);
+      tagg(T, f, cw, bn[0], b00[0], b10[0], b01[0]);
+      tagg(T, f, cw, bn[1], b00[1], b10[1], b01[1]);
+    }
+    // class counts of the pixel's own component (and the rings of its hole contour)
+    const int hn = (a.dbg & 1) ? 0 : np;
+    const unsigned long long hact = __ballot(hn > 0);
+    if (hact) {
+      const int leader = __ffsll((long long)hact) - 1;
+      const int lnp = __builtin_amdgcn_readlane(hn, leader);
+      const bool uni = __all(hn <= 0 || hn == lnp);
+      const int h = hn > 0 ? tslot(T, hn) : -1;  // one probe chain (uniform waves: same address)
+      if (uni && h >= 0) {
+        // node-uniform wave: one single-lane add per distinct class
+        for (unsigned long long rem = hact; rem;) {
+          const int l = __ffsll((long long)rem) - 1;
+          const int cl = __builtin_amdgcn_readlane(c, l);
+          const unsigned long long g = __ballot(hn > 0 && c == cl) & rem;
+          if (lane == l) atomicAdd(&T.hist[h * kDenseBins + cl], __popcll(g));
+          rem &= ~g;
+        }
+      } else if (hn > 0) {
+        if (h >= 0) atomicAdd(&T.hist[h * kDenseBins + c], 1);
+        else hist_global(f, cw, bins, hn, c, 1, false);
+      }
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (__any(rkey[q] > 0)) hagg(T, f, cw, bins, rkey[q]);
+      for (int q = 0; q < 4; ++q) {
+        if (hn > 0 && rc[q] >= 0) {
+          if (h >= 0) atomicAdd(&T.hist[h * kDenseBins + rc[q]], 1 << 16);
+          else hist_global(f, cw, bins, hn, rc[q], 1, true);
+        }
+      }
+    }
   }
   __syncthreads();
-  for (int i = tid; i < kHash; i += 256) {
-    const int node = T.q.key[i];
-    if (node != 0) moments_up(f, cw, node, T.q.s00[i], (long long)T.q.s10[i], (long long)T.q.s01[i], T.maxd);
+  if (a.dbg & 16) return;
+  // flush: each slot's ancestor chain once (one lane per slot), then fire-and-forget atomics
+  if (tid < kTSlots) {
+    const int node = T.key[tid];
+    int d = 0, n = 0;
+    if (node > 0 && !(a.dbg & 4)) {
+      n = parent_of(f, cw, node);
+      while (n != 0 && d < kAnc) {
+        T.anc[tid][d++] = n;
+        n = parent_of(f, cw, n);
+      }
+    }
+    T.nanc[tid] = d;
+    T.deep[tid] = n;  // != 0: the chain goes on past kAnc
   }
-  for (int i = tid; i < kHistHash; i += 256) {
-    const int key = T.hkey[i];
-    if (key != 0) hist_up(f, cw, bins, key, T.hcnt[i], T.maxd);
+  __syncthreads();
+  if (tid < kTSlots) {
+    const int node = T.key[tid];
+    if (node > 0 && T.s00[tid] != 0) {
+      const int d00 = T.s00[tid];
+      const unsigned long long d10 = T.s10[tid], d01 = T.s01[tid];  // (zero-extended)
+      for (int k = -1; k < T.nanc[tid]; ++k) {
+        const int n = k < 0 ? node : T.anc[tid][k];
+        atomicAdd(f.t00 + n - 1, d00);
+        atomicAdd(reinterpret_cast<unsigned long long*>(f.t10 + n - 1), d10);
+        atomicAdd(reinterpret_cast<unsigned long long*>(f.t01 + n - 1), d01);
+      }
+      if (T.deep[tid] != 0) moments_up(f, cw, T.deep[tid], d00, (long long)d10, (long long)d01, 65536);
+    }
+  }
+  for (int i = tid; i < kTSlots * kDenseBins; i += 256) {
+    const int v = T.hist[i];
+    if (v == 0) continue;
+    const int sl = i / kDenseBins, cc = i - sl * kDenseBins;
+    const int node = T.key[sl];
+    const int own = v & 0xffff, ring = v >> 16;
+    if (ring) atomicAdd(f.th + (size_t)(node - 1) * bins + cc, ring);
+    if (own) {
+      for (int k = -1; k < T.nanc[sl]; ++k)
+        atomicAdd(f.th + (size_t)((k < 0 ? node : T.anc[sl][k]) - 1) * bins + cc, own);
+      if (T.deep[sl] != 0) hist_global(f, cw, bins, T.deep[sl], cc, own, false);
+    }
   }
 }
 
@@ -1314,6 +1486,7 @@ __device__ __forceinline__ void assign_frame(const KArgs& a, FrameWS& f, int* s_
 
 // ---------------------------------------------------------------- finalize
 constexpr int kMaxDepth = 32;
+constexpr int kRecCache = 4096;  // components whose tree k_records caches in LDS
 
 __device__ __forceinline__ int disc_key(const FrameWS& f, int n) {
   const int r = f.rlist[n - 1];
@@ -1341,7 +1514,8 @@ __device__ bool precedes(const FrameWS& f, int cw, int a, int da, int b, int db)
   return disc_key(f, u) > disc_key(f, v);
 }
 
-__device__ __forceinline__ void finalize_frame(const KArgs& a, FrameWS& f, const int* s_sn, const int* s_res) {
+__device__ __forceinline__ void finalize_frame(const KArgs& a, FrameWS& f, const int* s_sn, const int* s_res,
+                                               const int* c_par, const int* c_dk, int cbase) {
   const int b = blockIdx.x, NT = blockDim.x;
   float* rec = a.records + (size_t)b * (1 + 5 * a.K);
   __shared__ int s_node[256];
@@ -1361,7 +1535,11 @@ __device__ __forceinline__ void finalize_frame(const KArgs& a, FrameWS& f, const
     // ancestor chain (top first) of discovery keys
     int chain[kMaxDepth];
     int len = 0;
-    for (int n = node; n != 0 && len < kMaxDepth; n = parent_of(f, a.cw, n)) chain[len++] = disc_key(f, n);
+    if (c_par) {  // the frame's tree cached in LDS (parent index, discovery key per node)
+      for (int j = node - 1 - cbase; j >= 0 && len < kMaxDepth; j = c_par[j]) chain[len++] = c_dk[j];
+    } else {
+      for (int n = node; n != 0 && len < kMaxDepth; n = parent_of(f, a.cw, n)) chain[len++] = disc_key(f, n);
+    }
     for (int k = 0; k < len; ++k) s_path[i][k] = chain[len - 1 - k];
     s_len[i] = len;
     if (len == kMaxDepth) {
@@ -1446,9 +1624,22 @@ __global__ __launch_bounds__(1024) void k_records(KArgs a) {
     return;
   }
   f.fb = f.flag[0];
-  assign_frame(a, f, s_sn, s_res);
-  finalize_frame(a, f, s_sn, s_res);
+  // the border tree in LDS (parent index, discovery key of every component): the finalize
+  // phase's ancestor chains walk LDS instead of dependent global loads (2 per level)
+  __shared__ int c_par[kRecCache], c_dk[kRecCache];
+  const int nr = f.nslot[3], cbase = f.flag[3];
+  const bool cached = nr <= kRecCache;
+  if (cached) {
+    for (int j = threadIdx.x; j < nr; j += blockDim.x) {
+      const int pl = parent_of(f, a.cw, cbase + j + 1);
+      c_par[j] = pl == 0 ? -1 : pl - 1 - cbase;
+      c_dk[j] = disc_key(f, cbase + j + 1);
+    }
+  }
+  assign_frame(a, f, s_sn, s_res);  // (its barriers order the cache writes before the reads)
+  finalize_frame(a, f, s_sn, s_res, cached ? c_par : nullptr, c_dk, cbase);
 }
+
 
 }  // namespace
 
@@ -1465,6 +1656,7 @@ void postprocess(const PostParams& p, hipStream_t s) {
   if (p.crop_h > p.H || p.crop_w > p.W || p.crop_h <= 0 || p.crop_w <= 0)
     throw std::invalid_argument("postprocess: bad crop");
   if (p.accum < 0 || p.accum > 2) throw std::invalid_argument("postprocess: accum 0 (strips), 1 (32^2 tiles), 2 (64^2)");
+  const int accum = p.num_bins > kDenseBins ? 0 : p.accum;  // the tile tables count <= 32 classes
   KArgs a;
   a.labels = p.labels;
   a.B = p.B; a.H = p.H; a.W = p.W; a.ch = p.crop_h; a.cw = p.crop_w;
@@ -1500,11 +1692,13 @@ void postprocess(const PostParams& p, hipStream_t s) {
   if (st++ < stages) hipLaunchKernelGGL(k_ccl_local, gt, dim3(kCclThreads), 0, s, a, p.palette);
   {
     const int tx_n = cdiv(p.crop_w, TW), ty_n = cdiv(p.crop_h, TH);
+    const int nt = tx_n * ty_n;
     const int lines = (ty_n - 1) + 2 + 2 * (tx_n - 1) + 2;
     if (st++ < stages)
       hipLaunchKernelGGL(k_ccl_edges, dim3(cdiv(std::max(p.crop_w, p.crop_h), kEdgeThreads), lines, p.B),
                          dim3(kEdgeThreads), 0, s, a);
-    const size_t lds = (size_t)(2 * (kMergeCap + 1) + 3) * 4;
+    const size_t lds = (size_t)(2 * (kMergeCap + 1) + kMergeCap + nt + 1 + 1024 + 3) * 4;
+    if (lds > 160 * 1024) throw std::invalid_argument("postprocess: crop too large for the LDS merge (> ~1800^2 pixels)");
     static bool attr = false;
     if (!attr) {
       check(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ccl_merge),
@@ -1533,9 +1727,9 @@ void postprocess(const PostParams& p, hipStream_t s) {
   const int rounds = std::max(1, N / (256 * qtarget));
   const int qblocks = cdiv(N, 256 * rounds) * (256 / kAccThreads);
   if (st++ < stages) {
-    if (p.accum == 1)
+    if (accum == 1)
       hipLaunchKernelGGL(k_accum_tiles<32>, dim3(cdiv(p.crop_w, 32), cdiv(p.crop_h, 32), p.B), dim3(256), 0, s, a);
-    else if (p.accum == 2)
+    else if (accum == 2)
       hipLaunchKernelGGL(k_accum_tiles<64>, dim3(cdiv(p.crop_w, 64), cdiv(p.crop_h, 64), p.B), dim3(256), 0, s, a);
     else
       hipLaunchKernelGGL(k_accum, dim3(qblocks, p.B), dim3(kAccThreads), 0, s, a);

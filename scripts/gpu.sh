@@ -24,6 +24,7 @@
 #   postab       post-processing harness (tools/bin/post_bench), strips vs 32^2 / 64^2 tile accumulation
 #   postvar      every tools/bin/pb_* variant (scripts/post_variants.sh) on the bench model's own label
 #                maps + the synthetic kinds (POST_DBG_LIST: SSA_POST_DBG values; STAGEWISE=1: per launch)
+#   postpmc      3 SQ counter passes over tools/bin/pb_prod on the bench model's label maps -> post_pmc.txt
 #   posttrace    post_bench (4 map kinds incl. the fallback-path lattice) under a kernel trace
 #   repro        packed-f32 co-residence reproducer, both builds (csrc/tools/packed_f32_repro.hip)
 #   retune:LIST  re-time the named choices (comma list) at B = ${TUNE_B:-32} on top of the committed
@@ -100,12 +101,22 @@ for step in "$@"; do
              cut -c1-600 $O/share$n.json ;;
     postab)  for m in 0 1 2; do SSA_POST_ACCUM=$m timeout -k 10 120 tools/bin/post_bench 50 > $O/post_accum$m.txt 2>&1 \
                || { tail -5 $O/post_accum$m.txt; exit 7; }; echo "accum=$m"; cat $O/post_accum$m.txt; done ;;
-    postvar) timeout -k 10 300 python scripts/label_stats.py /tmp/ssa_maps.bin > $O/label_stats.txt 2>&1 \
+    postvar) [ -f /tmp/ssa_maps.bin ] || timeout -k 10 300 python scripts/label_stats.py /tmp/ssa_maps.bin > $O/label_stats.txt 2>&1 \
                || { tail -5 $O/label_stats.txt; exit 7; }
              for bin in tools/bin/pb_*; do for d in ${POST_DBG_LIST:-0}; do
-               SSA_POST_DBG=$d ${STAGEWISE:+SSA_POST_STAGEWISE=1} timeout -k 10 180 $bin ${POST_REPS:-30} /tmp/ssa_maps.bin \
+               env SSA_POST_DBG=$d ${STAGEWISE:+SSA_POST_STAGEWISE=1} timeout -k 10 180 $bin ${POST_REPS:-30} /tmp/ssa_maps.bin \
                  > $O/$(basename $bin)_d$d.txt 2>&1 || { tail -5 $O/$(basename $bin)_d$d.txt; exit 7; }
                echo "== $bin dbg=$d"; cat $O/$(basename $bin)_d$d.txt; done; done ;;
+    postpmc) [ -f /tmp/ssa_maps.bin ] || timeout -k 10 300 python scripts/label_stats.py /tmp/ssa_maps.bin > $O/label_stats.txt 2>&1 \
+               || { tail -5 $O/label_stats.txt; exit 7; }
+             i=0
+             for set in "${PMC_SETS[@]}"; do
+               i=$((i+1))
+               (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $set \
+                 -d $REPO/$O/ppmc$i -o run --output-format csv -- $REPO/tools/bin/pb_prod 5 /tmp/ssa_maps.bin 1 \
+                 > $REPO/$O/ppmc$i.log 2>&1) || { echo "pmc set $i failed"; tail -5 $O/ppmc$i.log; exit 4; }
+             done
+             python3 scripts/pmc_kernels.py $O/ppmc1 $O/ppmc2 $O/ppmc3 > $O/post_pmc.txt 2>&1; cat $O/post_pmc.txt ;;
     posttrace) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats \
                -d $REPO/$O/posttrace -o run --output-format csv -- $REPO/tools/bin/post_bench 20 \
                > $REPO/$O/posttrace.log 2>&1) || { tail -5 $O/posttrace.log; exit 7; }
