@@ -698,7 +698,8 @@ __device__ __forceinline__ void ccl_boundary_pixel(KArgs& a, FrameWS& f, int p) 
 // then the relabel (every pixel's root, read-only traversal: concurrent stores only ever
 // write roots), the roots' accumulators zeroed and listed, and each root's border-tree
 // parent (the final label of the pixel left of it, resolved by the same traversal).
-constexpr int kFbBlocks = 256;  // blocks (grid-stride over each flagged frame's pixels in turn)
+constexpr int kFbBlocks = 64;  // blocks (grid-stride over each flagged frame's pixels in turn; a small
+                                // grid: the no-op launches share the GPU with the next step's kernels)
 
 // The flagged frames of the batch, as a bitmask per 64 frames (every wave of the block
 // computes the same mask from the same flags; one load per lane, not a chain of B loads).
@@ -1408,7 +1409,7 @@ __device__ __forceinline__ int passes_px(const FrameWS& f, const KArgs& a, int p
   return n != 0 && f.rlist[n - 1] == p && passes_n(f, a, n) ? n : 0;
 }
 
-constexpr int kSortCap = 8192;
+constexpr int kSortCap = 2048;  // (LDS: k_records shares CUs with the next step's model kernels)
 
 // (record slots handed out here are also kept in LDS, s_sn / s_res, for the finalize
 // phase of the same workgroup)
@@ -1485,8 +1486,7 @@ __device__ __forceinline__ void assign_frame(const KArgs& a, FrameWS& f, int* s_
 }
 
 // ---------------------------------------------------------------- finalize
-constexpr int kMaxDepth = 32;
-constexpr int kRecCache = 4096;  // components whose tree k_records caches in LDS
+constexpr int kMaxDepth = 16;
 
 __device__ __forceinline__ int disc_key(const FrameWS& f, int n) {
   const int r = f.rlist[n - 1];
@@ -1514,8 +1514,7 @@ __device__ bool precedes(const FrameWS& f, int cw, int a, int da, int b, int db)
   return disc_key(f, u) > disc_key(f, v);
 }
 
-__device__ __forceinline__ void finalize_frame(const KArgs& a, FrameWS& f, const int* s_sn, const int* s_res,
-                                               const int* c_par, const int* c_dk, int cbase) {
+__device__ __forceinline__ void finalize_frame(const KArgs& a, FrameWS& f, const int* s_sn, const int* s_res, int) {
   const int b = blockIdx.x, NT = blockDim.x;
   float* rec = a.records + (size_t)b * (1 + 5 * a.K);
   __shared__ int s_node[256];
@@ -1535,11 +1534,7 @@ __device__ __forceinline__ void finalize_frame(const KArgs& a, FrameWS& f, const
     // ancestor chain (top first) of discovery keys
     int chain[kMaxDepth];
     int len = 0;
-    if (c_par) {  // the frame's tree cached in LDS (parent index, discovery key per node)
-      for (int j = node - 1 - cbase; j >= 0 && len < kMaxDepth; j = c_par[j]) chain[len++] = c_dk[j];
-    } else {
-      for (int n = node; n != 0 && len < kMaxDepth; n = parent_of(f, a.cw, n)) chain[len++] = disc_key(f, n);
-    }
+    for (int n = node; n != 0 && len < kMaxDepth; n = parent_of(f, a.cw, n)) chain[len++] = disc_key(f, n);
     for (int k = 0; k < len; ++k) s_path[i][k] = chain[len - 1 - k];
     s_len[i] = len;
     if (len == kMaxDepth) {
@@ -1624,20 +1619,8 @@ __global__ __launch_bounds__(1024) void k_records(KArgs a) {
     return;
   }
   f.fb = f.flag[0];
-  // the border tree in LDS (parent index, discovery key of every component): the finalize
-  // phase's ancestor chains walk LDS instead of dependent global loads (2 per level)
-  __shared__ int c_par[kRecCache], c_dk[kRecCache];
-  const int nr = f.nslot[3], cbase = f.flag[3];
-  const bool cached = nr <= kRecCache;
-  if (cached) {
-    for (int j = threadIdx.x; j < nr; j += blockDim.x) {
-      const int pl = parent_of(f, a.cw, cbase + j + 1);
-      c_par[j] = pl == 0 ? -1 : pl - 1 - cbase;
-      c_dk[j] = disc_key(f, cbase + j + 1);
-    }
-  }
-  assign_frame(a, f, s_sn, s_res);  // (its barriers order the cache writes before the reads)
-  finalize_frame(a, f, s_sn, s_res, cached ? c_par : nullptr, c_dk, cbase);
+  assign_frame(a, f, s_sn, s_res);
+  finalize_frame(a, f, s_sn, s_res, 0);
 }
 
 
