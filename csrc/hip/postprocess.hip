@@ -11,13 +11,13 @@
 //   k_ccl_local  per 32x32 tile: palette -> 3x3 box blur (REFLECT_101, rounded) ->
 //                BGR2GRAY on RGB (fixed point) -> > thr, then union-find in LDS:
 //                foreground 8-connected, background 4-connected; zeroes the counters
-//   k_ccl_edges  cross-tile unions as pairs of tile-local roots
-//   k_ccl_merge  one workgroup per frame: union-find over those pairs in LDS (frames past
-//                its caps: flagged for k_fb_unite / k_fb_relabel, a global union-find
-//                across the tile edges and a relabel, grid-wide);
+//   k_ccl_edges  cross-tile unions as pairs of tile-local roots (frames past kMergeCap
+//                roots: applied to L right away, a global union-find)
+//   k_ccl_merge  one workgroup per frame: union-find over those pairs in LDS;
 //                image-border background joins the virtual "outside" node 0; final
-//                labels of the tile-local roots (component root = raster index of its
-//                first pixel + 1, 0 = outside); roots zero their accumulators
+//                labels of the tile-local roots (a label is an entry of the batch's root
+//                pool + 1, 0 = outside); roots zero their accumulators. Extra workgroups
+//                of the same grid relabel the union-find frames.
 //   k_accum      per pixel: its 2x2 quad's polygon pieces as exact integer moments
 //                (a00 = 2A, a10 = 6*int x, a01 = 6*int y) and its class into the fill
 //                histograms (component + everything it encloses; holes also get the
@@ -47,11 +47,12 @@ struct FrameWS {
   int32_t* rootpix;    // [ntiles][kTileCap] raster index of each tile-local root (tile-local index
                        //     c < kTileCap; the rest go to rovf)
   int32_t* ntroot;     // [ntiles] tile-local roots per tile
-  int32_t* rovf;       // [kOvfCap][2] (tile * kTileRoots + c, raster index) of roots past kTileCap
+  int32_t* rovf;       // [kMergeCap][2] (tile * kTileRoots + c, raster index) of roots past kTileCap
   int32_t* flag;       // [8]: [0] = 1 -> global union-find fallback, [1] = 1 -> root pool exhausted
                        //      (no records), [2] rovf entries (k_ccl_local -> k_ccl_merge, which
                        //      re-zeroes it), [3] the frame's first pool entry
-  int32_t* edges;      // [kEdgeCap][2] cross-tile unions (compact root pairs as raster, -1 = outside)
+  int32_t* edges;      // [ecap][2] cross-tile unions (tile-local roots as raster, -1 = outside); ecap =
+                       //     3 per edge-line pixel, so the list never overflows
   // root pool, shared by the batch and indexed by component label - 1 (labels are pool
   // entries: a frame's components take one contiguous run of it)
   int32_t* pool;       // [0] entries taken this call (zeroed by k_ccl_local)
@@ -71,8 +72,6 @@ constexpr int TW = 32, TH = SSA_CCL_TH;  // local CCL tile
 constexpr int kMergeCap = 12288;     // tile-local roots the per-frame LDS merge handles
 constexpr int kTileRoots = TW * TH;  // worst case roots per tile
 constexpr int kTileCap = 64;         // roots per tile with a rootpix slot (the rest: rovf)
-constexpr int kOvfCap = 4096;        // rovf entries per frame (more: the fallback path)
-constexpr int kEdgeCap = 1 << 15;    // cross-tile union pairs per frame
 constexpr int kPoolPerFrame = 8192;  // root pool entries per frame of the batch (floor: N + 1)
 
 // Workspace layout (round 5): per frame only what is per pixel (labels, mask,
@@ -85,7 +84,7 @@ constexpr int kPoolPerFrame = 8192;  // root pool entries per frame of the batch
 // count NaN; never on segmentation maps -- the bench frames have ~200 components each).
 // Round 4 indexed every per-root array by raster index: 46 MB per 513^2 frame.
 struct Layout {
-  size_t N, K, bins, P, ntiles;
+  size_t N, K, bins, P, ntiles, ecap;
   size_t small_bytes;  // nslot(16) + slot_node, per frame (zeroed every call)
   size_t big_bytes;    // per frame
   size_t pool_bytes;   // per batch
@@ -101,10 +100,13 @@ Layout layout(int B, int H, int W, int K, int bins) {
   l.bins = bins;
   l.P = std::max((size_t)B * kPoolPerFrame, l.N + 1);
   l.ntiles = (size_t)((W + TW - 1) / TW) * ((H + TH - 1) / TH);
+  // k_ccl_edges' unions at the largest crop: <= 3 per pixel of a tile top row, 2 of a tile
+  // left column, 1 of a right column or of the image border
+  const size_t txn = (W + TW - 1) / TW, tyn = (H + TH - 1) / TH;
+  l.ecap = (tyn - 1) * W * 3 + 2 * (size_t)W + (txn - 1) * H * 3 + 2 * (size_t)H;
   l.small_bytes = al(16 + (size_t)K * 4);
   l.big_bytes = al((l.N + 1) * 4) + al(l.N) + al(l.N * 4) + al(l.ntiles * kTileCap * 4) + al(l.ntiles * 4) +
-                al((size_t)kOvfCap * 8) + al(32) +
-                al((size_t)kEdgeCap * 8);
+                al((size_t)kMergeCap * 8) + al(32) + al(l.ecap * 8);
   l.pool_bytes = 2 * al(l.P * 8) + 3 * al(l.P * 4) + al(l.P * bins * 4);
   return l;
 }
@@ -122,7 +124,7 @@ __host__ __device__ inline FrameWS frame_ws(char* ws, const Layout& l, int B, in
   f.cidx = reinterpret_cast<int32_t*>(p); p += al(l.N * 4);
   f.rootpix = reinterpret_cast<int32_t*>(p); p += al(l.ntiles * kTileCap * 4);
   f.ntroot = reinterpret_cast<int32_t*>(p); p += al(l.ntiles * 4);
-  f.rovf = reinterpret_cast<int32_t*>(p); p += al((size_t)kOvfCap * 8);
+  f.rovf = reinterpret_cast<int32_t*>(p); p += al((size_t)kMergeCap * 8);
   f.flag = reinterpret_cast<int32_t*>(p); p += al(32);
   f.edges = reinterpret_cast<int32_t*>(p);
   char* q = hdr + 256 + (size_t)B * l.big_bytes;
@@ -367,9 +369,9 @@ __global__ __launch_bounds__(kCclThreads) void k_ccl_local(KArgs a, const int32_
       f.cidx[y * a.cw + x] = c;
       if (c < kTileCap) {
         f.rootpix[tile * kTileCap + c] = y * a.cw + x;
-      } else {  // a crowded tile: listed (rare; a frame past kOvfCap takes the fallback)
+      } else {  // a crowded tile: listed (rare; at most kMergeCap of them matter)
         const int o = atomicAdd(f.flag + 2, 1);
-        if (o < kOvfCap) {
+        if (o < kMergeCap) {
           f.rovf[2 * o] = tile * kTileRoots + c;
           f.rovf[2 * o + 1] = y * a.cw + x;
         }
@@ -377,7 +379,10 @@ __global__ __launch_bounds__(kCclThreads) void k_ccl_local(KArgs a, const int32_
     }
   }
   __syncthreads();
-  if (tid == 0) f.ntroot[tile] = s_nroot;
+  if (tid == 0) {
+    f.ntroot[tile] = s_nroot;
+    atomicAdd(f.flag + 4, s_nroot);  // the frame's root count (k_ccl_edges decides the path)
+  }
 }
 
 // ---------------------------------------------------------------- compact merge
@@ -395,13 +400,12 @@ __global__ __launch_bounds__(kCclThreads) void k_ccl_local(KArgs a, const int32_
 //   of every component root and lists the roots. Pixels are resolved on the fly
 //   afterwards (fin(): L -> tile-local root -> cidx): no full-frame relabelling pass
 //   (round 2's k_compress, 22 us per 32 frames).
-// Frames past kMergeCap roots or kEdgeCap pairs take the global union-find (device-
-// coherent pointer chasing) across the tile edges and a relabelling pass instead:
-// k_ccl_merge flags them and two grid kernels (k_fb_unite, k_fb_relabel) do the work,
-// leaving at once for unflagged frames; fin() then reads the final label straight from L.
-// (Round 3 ran the fallback inside the merge workgroup: 813 us per flagged frame.)
+// Frames past kMergeCap roots take the global union-find (device-coherent pointer chasing)
+// across the tile edges inside k_ccl_edges and a relabelling pass in the merge grid (see
+// fb_relabel); fin() reads the same two levels (L -> root -> cidx) for both.
 // wave-aggregated append of this lane's kept pairs (me, o0..o2; k0..k2 = kept)
-__device__ __forceinline__ void emit_pairs(FrameWS& f, int me, int o0, int o1, int o2, bool k0, bool k1, bool k2) {
+__device__ __forceinline__ void emit_pairs(FrameWS& f, size_t ecap, int me, int o0, int o1, int o2, bool k0, bool k1,
+                                           bool k2) {
   const int n = (int)k0 + (int)k1 + (int)k2;
   int incl = n;
   const int lane = threadIdx.x & 63;
@@ -417,7 +421,7 @@ __device__ __forceinline__ void emit_pairs(FrameWS& f, int me, int o0, int o1, i
   base = __shfl(base, 63, 64);
   int at = base + incl - n;
   auto put = [&](int o) {
-    if (at < kEdgeCap) {
+    if (at < (int)ecap) {  // (never false: ecap covers 3 unions per line pixel)
       f.edges[2 * at] = me;
       f.edges[2 * at + 1] = o;
     }
@@ -433,6 +437,19 @@ constexpr int kEdgeThreads = 256;
 __global__ __launch_bounds__(kEdgeThreads) void k_ccl_edges(KArgs a) {
   const int b = blockIdx.z;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
+  // frames past kMergeCap tile-local roots take the global union-find right here: the
+  // same unions, applied to L (device-coherent pointer chasing) instead of listed; one
+  // thread per frame reserves their root count (>= the components) from the pool
+  const int R = __builtin_amdgcn_readfirstlane(f.flag[4]);
+  const bool fb = R > kMergeCap;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    f.flag[0] = fb ? 1 : 0;
+    if (fb) {
+      const int base = atomicAdd(f.pool, R);
+      f.flag[1] = (size_t)base + R > a.lay.P ? 1 : 0;
+      f.flag[3] = base;
+    }
+  }
   const int tx_n = (a.cw + TW - 1) / TW, ty_n = (a.ch + TH - 1) / TH;
   // horizontal lines: tile top rows y = k*TH (k >= 1), image rows 0 and ch-1;
   // vertical lines: tile left columns x = k*TW (k >= 1), right columns x = k*TW-1
@@ -498,11 +515,15 @@ __global__ __launch_bounds__(kEdgeThreads) void k_ccl_edges(KArgs a) {
     const bool k0 = o0 != -2 && !seen(o0);
     const bool k1 = o1 != -2 && o1 != o0 && !seen(o1);
     const bool k2 = o2 != -2 && o2 != o0 && o2 != o1 && !seen(o2);
-    emit_pairs(f, me, o0, o1, o2, k0, k1, k2);
+    if (fb) {
+      if (k0) unite(f.L, me + 1, o0 + 1);  // (-1 + 1 = the outside node 0)
+      if (k1) unite(f.L, me + 1, o1 + 1);
+      if (k2) unite(f.L, me + 1, o2 + 1);
+    } else {
+      emit_pairs(f, a.lay.ecap, me, o0, o1, o2, k0, k1, k2);
+    }
   }
 }
-
-__device__ __forceinline__ void ccl_boundary_pixel(KArgs& a, FrameWS& f, int p);
 
 // A component root takes pool entry n (label n + 1): its accumulators zeroed, listed
 __device__ __forceinline__ void new_root(FrameWS& f, int bins, int n, int p) {
@@ -514,8 +535,14 @@ __device__ __forceinline__ void new_root(FrameWS& f, int bins, int n, int p) {
   f.rlist[n] = p;
 }
 
+__device__ void fb_relabel(const KArgs& a, int bi, int nb);
+
 __global__ __launch_bounds__(1024) void k_ccl_merge(KArgs a) {
   extern __shared__ int sm[];
+  if ((int)blockIdx.x >= a.B) {  // the union-find frames' relabel (idle unless one is flagged)
+    fb_relabel(a, blockIdx.x - a.B, gridDim.x - a.B);
+    return;
+  }
   const int b = blockIdx.x;
   FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
   const int cw = a.cw, ch = a.ch;
@@ -552,17 +579,13 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(KArgs a) {
   const int R = toff[nt];
   const int E = f.nslot[2];
   const int O = f.flag[2];
-  if (R > kMergeCap || E > kEdgeCap || O > kOvfCap) {  // k_fb_unite / k_fb_relabel take the frame
-    if (tid == 0) {
-      // reserve the tile-local root count (>= its components) from the pool
-      const int base = atomicAdd(f.pool, R);
-      f.flag[0] = 1;
-      f.flag[1] = (size_t)base + R > a.lay.P ? 1 : 0;
-      f.flag[2] = 0;
-      f.flag[3] = base;
-    }
-    return;
+  __syncthreads();
+  if (tid == 0) {  // k_ccl_local's counters, read (here and by k_ccl_edges) for this call
+    f.flag[2] = 0;
+    f.flag[4] = 0;
   }
+  if (R > kMergeCap) return;  // k_ccl_edges united it in L and took its pool run; the relabel
+                              // blocks of this grid label it
   const int OUT = R;
   auto tile_of = [&](int i) {  // last tile t with toff[t] <= i (empty tiles share offsets)
     int lo = 0, hi = nt - 1;
@@ -606,9 +629,7 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(KArgs a) {
     const int base = atomicAdd(f.pool, nr);
     const bool ex = (size_t)base + nr > a.lay.P;
     s_c[2] = ex ? -1 : base;
-    f.flag[0] = 0;
     f.flag[1] = ex ? 1 : 0;
-    f.flag[2] = 0;
     f.flag[3] = base;
     f.nslot[3] = nr;
   }
@@ -637,69 +658,17 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(KArgs a) {
   }
 }
 
-// Cross-tile merges (and image-border background -> outside node 0) of the fallback
-// path: only pixels on a tile's left column / top row or on the image border do work.
-__device__ __forceinline__ void ccl_boundary_pixel(KArgs& a, FrameWS& f, int p) {
-  const int y = p / a.cw, x = p - y * a.cw;
-  const bool left = x > 0 && (x % TW) == 0;
-  const bool top = y > 0 && (y % TH) == 0;
-  const bool edge = x == 0 || y == 0 || x == a.cw - 1 || y == a.ch - 1;
-  const bool rtile = (x % TW) == TW - 1 && x + 1 < a.cw && y > 0;  // up-right neighbour in next tile
-  if (!left && !top && !edge && !rtile) return;
-  const uint8_t m = f.mask[p];
-  const int me = p + 1;
-  // Skip unions already implied by the previous pixel along the same tile edge:
-  // if it has the same class, the same tile-local root and its partner across the
-  // edge has the same local root as ours, it issued the identical union. (Local
-  // roots are still in L: tile-local writes are the only writes before this pass
-  // apart from root links, which keep equal roots equal.)
-  auto lroot = [&](int q) { return f.L[q + 1]; };
-  if (m) {
-    if (left && f.mask[p - 1]) unite(f.L, me, me - 1);
-    if (y > 0) {
-      const int up = p - a.cw;
-      if (top) {
-        const bool dup = x > 0 && (x % TW) != 0 && f.mask[p - 1] && lroot(p - 1) == lroot(p);
-        if (f.mask[up] && !(dup && f.mask[up - 1] && lroot(up - 1) == lroot(up)))
-          unite(f.L, me, up + 1);
-        if (x > 0 && f.mask[up - 1]) unite(f.L, me, up);
-        if (x + 1 < a.cw && f.mask[up + 1]) unite(f.L, me, up + 2);
-      } else {
-        // same tile row: diagonals that cross a vertical tile edge
-        if (left && f.mask[up - 1]) unite(f.L, me, up);
-        if (rtile && f.mask[up + 1]) unite(f.L, me, up + 2);
-      }
-    }
-  } else {
-    if (left && !f.mask[p - 1]) {
-      const bool dup = y > 0 && (y % TH) != 0 && !f.mask[p - a.cw] && !f.mask[p - a.cw - 1] &&
-                       lroot(p - a.cw) == lroot(p) && lroot(p - a.cw - 1) == lroot(p - 1);
-      if (!dup) unite(f.L, me, me - 1);
-    }
-    if (top && !f.mask[p - a.cw]) {
-      const bool dup = x > 0 && (x % TW) != 0 && !f.mask[p - 1] && !f.mask[p - a.cw - 1] &&
-                       lroot(p - 1) == lroot(p) && lroot(p - a.cw - 1) == lroot(p - a.cw);
-      if (!dup) unite(f.L, me, me - a.cw);
-    }
-    if (edge) {
-      // one union per run of border pixels sharing a tile-local root
-      const int prev = (y == 0 || y == a.ch - 1) ? (x > 0 && (x % TW) != 0 ? p - 1 : -1)
-                                                 : ((y % TH) != 0 ? p - a.cw : -1);
-      if (prev < 0 || f.mask[prev] || lroot(prev) != lroot(p)) unite(f.L, me, 0);
-    }
-  }
-}
-
-// Fallback for frames past the LDS merge's caps (more than kMergeCap tile-local roots or
-// kEdgeCap cross-tile pairs: speckled maps). Round 3 ran it inside k_ccl_merge, one
-// workgroup per frame: 813 us for a frame of ~12k components (the lattice maps
-// of csrc/tools/post_bench.hip). Here two grid kernels that every frame's blocks leave at
-// once unless k_ccl_merge flagged the frame: the global union-find across the tile edges,
-// then the relabel (every pixel's root, read-only traversal: concurrent stores only ever
-// write roots), the roots' accumulators zeroed and listed, and each root's border-tree
-// parent (the final label of the pixel left of it, resolved by the same traversal).
-constexpr int kFbBlocks = 64;  // blocks (grid-stride over each flagged frame's pixels in turn; a small
-                                // grid: the no-op launches share the GPU with the next step's kernels)
+// Fallback for frames past the LDS merge's cap (more than kMergeCap tile-local roots:
+// speckled maps). Round 3 ran it inside one k_ccl_merge workgroup per frame: 813 us for a
+// frame of ~12k components (the lattice maps of csrc/tools/post_bench.hip).
+// Since round 5 it costs no launch of its own: k_ccl_edges applies the frame's cross-tile
+// unions to L directly (global union-find), and extra workgroups of the k_ccl_merge grid
+// relabel it (every pixel's root, read-only traversal: concurrent stores only ever write
+// roots), zero and list the roots' pool entries, and record each root's border-tree parent
+// (the root of the pixel left of it, by the same traversal). Round 4 spent two grid
+// launches (k_fb_unite, k_fb_relabel) on this: ~11 us per step of no-ops in the step trace;
+// a separate small relabel grid read 11-21 us there (profiles/r5z_layer_times.txt).
+constexpr int kFbBlocks = 64;  // relabel workgroups of the merge grid (grid-stride per frame)
 
 // The flagged frames of the batch, as a bitmask per 64 frames (every wave of the block
 // computes the same mask from the same flags; one load per lane, not a chain of B loads).
@@ -713,23 +682,13 @@ __device__ __forceinline__ unsigned long long fb_frames(const KArgs& a, int b0) 
   return __ballot(need);
 }
 
-__global__ __launch_bounds__(256) void k_fb_unite(KArgs a) {
-  const int N = a.ch * a.cw;
-  for (int b0 = 0; b0 < a.B; b0 += 64) {
-    for (unsigned long long m = fb_frames(a, b0); m; m &= m - 1) {
-      FrameWS f = frame_ws(a.ws, a.lay, a.B, b0 + __ffsll((long long)m) - 1);
-      for (int p = blockIdx.x * 256 + threadIdx.x; p < N; p += gridDim.x * 256) ccl_boundary_pixel(a, f, p);
-    }
-  }
-}
-
-__global__ __launch_bounds__(256) void k_fb_relabel(KArgs a) {
-  const int N = a.ch * a.cw;
+__device__ void fb_relabel(const KArgs& a, int bi, int nb) {
+  const int N = a.ch * a.cw, nt = blockDim.x;
   for (int b0 = 0; b0 < a.B; b0 += 64) {
     for (unsigned long long m = fb_frames(a, b0); m; m &= m - 1) {
       FrameWS f = frame_ws(a.ws, a.lay, a.B, b0 + __ffsll((long long)m) - 1);
       const int base = f.flag[3];
-      for (int p = blockIdx.x * 256 + threadIdx.x; p < N; p += gridDim.x * 256) {
+      for (int p = bi * nt + threadIdx.x; p < N; p += nb * nt) {
         const int r = find_root(f.L, p + 1);
         __hip_atomic_store(f.L + p + 1, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (r == p + 1) {
@@ -1624,6 +1583,16 @@ __global__ __launch_bounds__(1024) void k_records(KArgs a) {
 }
 
 
+#ifdef SSA_POST_DEBUG
+__global__ void k_dbg_reset(KArgs a) {
+  for (int b = threadIdx.x; b < a.B; b += 256) {
+    FrameWS f = frame_ws(a.ws, a.lay, a.B, b);
+    f.flag[2] = 0;
+    f.flag[4] = 0;
+  }
+}
+#endif
+
 }  // namespace
 
 size_t post_workspace_bytes(int B, int H, int W, int K, int num_bins) {
@@ -1689,12 +1658,9 @@ void postprocess(const PostParams& p, hipStream_t s) {
             "k_ccl_merge attr");
       attr = true;
     }
-    if (st++ < stages) hipLaunchKernelGGL(k_ccl_merge, dim3(p.B), dim3(1024), lds, s, a);
-    if (st++ < stages) {  // no-ops unless k_ccl_merge flagged the frame (caps exceeded)
-      const dim3 gfb(std::min(kFbBlocks, cdiv(N, 256)));
-      hipLaunchKernelGGL(k_fb_unite, gfb, dim3(256), 0, s, a);
-      hipLaunchKernelGGL(k_fb_relabel, gfb, dim3(256), 0, s, a);
-    }
+    // B merge workgroups + the union-find frames' relabel workgroups (idle unless flagged)
+    if (st++ < stages)
+      hipLaunchKernelGGL(k_ccl_merge, dim3(p.B + std::min(kFbBlocks, cdiv(N, 1024))), dim3(1024), lds, s, a);
   }
   // strip-privatised pass: kQuadBlocks strips per frame (SSA_QUAD_BLOCKS overrides, tuning)
   // rounds of 256 pixels per block chosen first, so no block ends with a near-empty round
@@ -1718,6 +1684,9 @@ void postprocess(const PostParams& p, hipStream_t s) {
       hipLaunchKernelGGL(k_accum, dim3(qblocks, p.B), dim3(kAccThreads), 0, s, a);
   }
   if (st++ < stages) hipLaunchKernelGGL(k_records, dim3(p.B), dim3(1024), 0, s, a);
+#ifdef SSA_POST_DEBUG
+  if (stages < 3) hipLaunchKernelGGL(k_dbg_reset, dim3(1), dim3(256), 0, s, a);  // k_ccl_merge's resets
+#endif
   check_launch("postprocess");
 }
 

@@ -134,7 +134,7 @@ int main(int argc, char** argv) {
     };
     if (getenv("SSA_POST_STAGEWISE")) {  // debug builds: cumulative time of the first n launches
       float prev = 0;
-      for (int n = 1; n <= 6; ++n) {
+      for (int n = 1; n <= 5; ++n) {
         char v[8];
         snprintf(v, sizeof v, "%d", n);
         setenv("SSA_POST_STAGES", v, 1);
