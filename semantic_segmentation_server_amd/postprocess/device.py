@@ -31,14 +31,14 @@ class DevicePostprocess:
         self.accum = int(env) if env is not None else None
 
     def accum_for(self, B: int) -> int:
-        """The accumulation pass for a batch of B frames: the strips at batch <= 2 (a
-        frame is 221 tiles for 256 CUs there: 19.7 us strips vs 26.9 us tiles at batch 1,
-        profiles/r3h_b1_layer_times.txt, r4_b1_layer_times.txt), the 32 x 32 tiles above
-        (94.5 vs 124.6 us at batch 32, r4a_layer_times.txt vs r3_v7_layer_times.txt)."""
+        """The accumulation pass for a batch of B frames: the LDS-staged 32 x 32 tiles at every
+        batch size since round 5's slot tables (batch 1: 18.6 vs 20.5 us for round 3's strips,
+        5678 vs 5456 frames/s, p50 0.625 vs 0.638 ms, profiles/r6b_b1_accum_ab.txt; batch 32:
+        64.8 vs 219 us per 32 bench frames, r5t). More than 32 classes use the strips (the
+        tile kernel's dense class counters hold 32)."""
         if self.accum is not None:
             return self.accum
-        return 0 if B <= 2 else 1
-
+        return 1
     def _buffers(self, B: int):
         if B not in self._bufs:
             nbytes = hip_ops.post_workspace_bytes(B, self.H, self.W, self.K, self.bins)
