@@ -22,7 +22,7 @@ sets = [load(d) for d in sys.argv[1:]]
 # last step: from the last stem_kernel dispatch on
 def last_step(ds):
     # one steady-state step: after the second-to-last post-processing finalize
-    idx = [i for i, d in enumerate(ds) if "k_finalize" in d["name"]]
+    idx = [i for i, d in enumerate(ds) if "k_finalize" in d["name"] or "k_records" in d["name"]]
     return ds[idx[-2] + 1: idx[-1] + 1] if len(idx) >= 2 else ds
 
 
