@@ -29,6 +29,50 @@ struct I8Args {
 
 __device__ __forceinline__ i32x4v ld16(const int8_t* p) { return *reinterpret_cast<const i32x4v*>(p); }
 
+// int8 requantisation of 16 consecutive channels (n..n+15) of pixel m, folded into the
+// affine terms: z = acc * (scale * ios) + (bias * ios + 128) + u * (res_scale * ios), u =
+// residual byte + 128 (v_cvt_f32_ubyte on the XOR-ed word, the -128 folded into the bias);
+// the activation and the int8 range are one med3 on the +128 offset grid, v_cvt_pk_u8_f32
+// rounds (nearest even) and packs, XOR 0x80 gives the signed bytes. ~8 VALU per value
+// instead of ~13 for the float chain, and within one rounding step of it (round 5).
+__device__ __forceinline__ i32x4v i8_requant16(const I8Args& a, const i32x4v (&v)[4], int m, int n) {
+  const float ios = a.inv_out_scale;
+  const float rs = a.res ? a.res_scale * ios : 0.f;
+  const float lo = a.act == ACT_NONE ? 1.f : 128.f;
+  const float hi = a.act == ACT_RELU6 ? fminf(255.f, 128.f + 6.f * ios) : 255.f;
+  unsigned ur[4] = {0, 0, 0, 0};
+  if (a.res) {
+    const i32x4v rv = *reinterpret_cast<const i32x4v*>(a.res + (size_t)m * a.Cout + n);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) ur[c] = (unsigned)rv[c] ^ 0x80808080u;
+  }
+  i32x4v pk;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const float4 sc = *reinterpret_cast<const float4*>(a.scale + n + c * 4);
+    const float4 bi = *reinterpret_cast<const float4*>(a.bias + n + c * 4);
+    const float s4[4] = {sc.x * ios, sc.y * ios, sc.z * ios, sc.w * ios};
+    float b4[4] = {fmaf(bi.x, ios, 128.f - 128.f * rs), fmaf(bi.y, ios, 128.f - 128.f * rs),
+                   fmaf(bi.z, ios, 128.f - 128.f * rs), fmaf(bi.w, ios, 128.f - 128.f * rs)};
+    if (a.img_bias) {
+      const int b = m / (a.OH * a.OW);
+      const float4 ib = *reinterpret_cast<const float4*>(a.img_bias + (size_t)b * a.Cout + n + c * 4);
+      b4[0] = fmaf(ib.x, ios, b4[0]); b4[1] = fmaf(ib.y, ios, b4[1]);
+      b4[2] = fmaf(ib.z, ios, b4[2]); b4[3] = fmaf(ib.w, ios, b4[3]);
+    }
+    unsigned w = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float z = fmaf((float)v[c][q], s4[q], b4[q]);
+      if (a.res) z = fmaf((float)((ur[c] >> (8 * q)) & 0xffu), rs, z);
+      z = __builtin_amdgcn_fmed3f(z, lo, hi);
+      w = __builtin_amdgcn_cvt_pk_u8_f32(z, q, w);
+    }
+    pk[c] = (int)(w ^ 0x80808080u);
+  }
+  return pk;
+}
+
 // Transposing epilogue (NT == 4: a wave's 64 output channels): the MFMA C layout
 // gives a lane 4 channels of one pixel per 16-channel subtile, so a direct store is
 // 4 bytes per lane at a Cout stride and the int8 residual is read byte by byte.
@@ -64,7 +108,10 @@ __device__ __forceinline__ void i8_epilogue_lds(const I8Args& a, const i32x4v (&
     for (int c = 0; c < 4; ++c)
 #pragma unroll
       for (int q = 0; q < 4; ++q) f[c * 4 + q] = (float)v[c][q];
-    if (n + 16 <= a.Cout && (a.Cout & 15) == 0) {
+    if (n + 16 <= a.Cout && (a.Cout & 15) == 0 && a.out_mode == 0 && ((a.ldo | a.co_off) & 15) == 0) {
+      *reinterpret_cast<i32x4v*>(static_cast<int8_t*>(a.out) + (size_t)m * a.ldo + a.co_off + n) =
+          i8_requant16(a, v, m, n);
+    } else if (n + 16 <= a.Cout && (a.Cout & 15) == 0) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const float4 sc = *reinterpret_cast<const float4*>(a.scale + n + c * 4);
@@ -455,6 +502,164 @@ __global__ void gap_i8_reduce(const float* __restrict__ part, float* __restrict_
 
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// Streaming 1x1 / stride-1 variant for the memory-bound bottleneck convs (ResNet-50
+// layers 1-3 at 1025^2: K = 64..256, 2-27 MAC per byte moved). The register-fed kernel
+// above runs one short-lived 32x32..32x64 tile per wave with the weights reloaded from
+// L2 by every wave and a 4-byte-per-lane epilogue (r4_config4_roofline.txt: L1's 1x1 convs
+// at 12-31 % of HBM bandwidth). Here a workgroup owns one block of NB = 16 NS output
+// channels for its whole life: the block's weight fragments are loaded into VGPRs once,
+// then the workgroup walks pixel tiles of 64 (one 16-pixel subtile per wave), prefetching
+// the next tile's input fragments while the MFMAs of the current one run, and stages the
+// int32 accumulators through LDS so the epilogue reads 16 consecutive channels of one
+// pixel per lane (16-byte residual loads and stores). Exact int32 accumulation; the int8
+// epilogue folds the requantisation into the affine terms (see below: within one rounding
+// step of the other variants), the bf16 one is theirs.
+template <int CF, int NS, int PD>
+__global__ __launch_bounds__(256) void conv_i8_1x1_kernel(I8Args a, int nblk) {
+  constexpr int NB = 16 * NS;           // output channels per workgroup
+  constexpr int EPP = NB + 4;           // staged row pitch (ints): 16 distinct bank groups
+  __shared__ __attribute__((aligned(16))) int ep_all[4 * 16 * EPP];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r = lane & 15, kq = lane >> 4;
+  const int M = a.B * a.OH * a.OW;
+  const int nb = blockIdx.x % nblk;     // this workgroup's channel block
+  const int tstep = gridDim.x / nblk;   // (the grid is a multiple of nblk)
+  const int ch0 = nb * NB;
+  // weights: A fragments (rows = out channels, 16 K bytes per lane), resident
+  i32x4v wf[NS][CF];
+#pragma unroll
+  for (int j = 0; j < NS; ++j)
+#pragma unroll
+    for (int f = 0; f < CF; ++f)
+      wf[j][f] = ld16(a.w + (size_t)(ch0 + j * 16 + r) * a.Cin + f * 64 + kq * 16);
+  int* ep = ep_all + wid * 16 * EPP;
+  const int ntile = (M + 63) / 64;
+  int t = blockIdx.x / nblk;
+  i32x4v xf[PD][CF];  // PD tiles of input fragments in flight
+  auto load_x = [&](int tile, i32x4v (&dst)[CF]) {
+    const int m = min(tile * 64 + wid * 16 + r, M - 1);  // clamped: tail pixels are not stored
+#pragma unroll
+    for (int f = 0; f < CF; ++f) dst[f] = ld16(a.in + (size_t)m * a.Cin + f * 64 + kq * 16);
+  };
+  const int px = lane >> 2, cq = lane & 3;  // epilogue: 16 pixels x 4 lanes of 16 channels
+  // one tile: MFMAs on xb, staged transpose, epilogue
+  auto tile_work = [&](int tile, const i32x4v (&xb)[CF]) {
+    i32x4v acc[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      acc[j] = i32x4v{0, 0, 0, 0};
+#pragma unroll
+      for (int f = 0; f < CF; ++f) acc[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wf[j][f], xb[f], acc[j], 0, 0, 0);
+    }
+    // stage [16 px][NB ch]: lane (r = pixel, kq) holds channels j*16 + kq*4 .. +3
+#pragma unroll
+    for (int j = 0; j < NS; ++j) *reinterpret_cast<i32x4v*>(ep + r * EPP + j * 16 + kq * 4) = acc[j];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int m = tile * 64 + wid * 16 + px;
+#pragma unroll 1
+    for (int g = cq; g < NS; g += 4) {  // this lane's 16-channel groups of pixel px
+      i32x4v v[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = *reinterpret_cast<const i32x4v*>(ep + px * EPP + g * 16 + c * 4);
+      if (m >= M) continue;
+      const int n = ch0 + g * 16;
+      const size_t o = (size_t)m * a.ldo + a.co_off + n;
+      if (a.out_mode == 0) {  // int8 out: the folded requantisation
+        *reinterpret_cast<i32x4v*>(static_cast<int8_t*>(a.out) + o) = i8_requant16(a, v, m, n);
+        continue;
+      }
+      float f[16];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float4 sc = *reinterpret_cast<const float4*>(a.scale + n + c * 4);
+        const float4 bi = *reinterpret_cast<const float4*>(a.bias + n + c * 4);
+        f[c * 4 + 0] = (float)v[c][0] * sc.x + bi.x; f[c * 4 + 1] = (float)v[c][1] * sc.y + bi.y;
+        f[c * 4 + 2] = (float)v[c][2] * sc.z + bi.z; f[c * 4 + 3] = (float)v[c][3] * sc.w + bi.w;
+        if (a.img_bias) {
+          const int b = m / (a.OH * a.OW);
+          const float4 ib = *reinterpret_cast<const float4*>(a.img_bias + (size_t)b * a.Cout + n + c * 4);
+          f[c * 4 + 0] += ib.x; f[c * 4 + 1] += ib.y; f[c * 4 + 2] += ib.z; f[c * 4 + 3] += ib.w;
+        }
+      }
+      if (a.res) {
+        const i32x4v rv = *reinterpret_cast<const i32x4v*>(a.res + (size_t)m * a.Cout + n);
+        const signed char* rb = reinterpret_cast<const signed char*>(&rv);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) f[q] += (float)rb[q] * a.res_scale;
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) f[q] = apply_act(f[q], a.act);
+      bf16* op = static_cast<bf16*>(a.out) + o;
+      bf16x8 o0, o1;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) { o0[q] = (bf16)f[q]; o1[q] = (bf16)f[q + 8]; }
+      *reinterpret_cast<bf16x8*>(op) = o0;
+      *reinterpret_cast<bf16x8*>(op + 8) = o1;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the next tile rewrites ep
+  };
+  // PD tiles per iteration, so the prefetch buffers stay statically indexed
+#pragma unroll
+  for (int i = 0; i < PD - 1; ++i)
+    if (t + i * tstep < ntile) load_x(t + i * tstep, xf[i]);
+#pragma unroll 1
+  for (; t < ntile; t += PD * tstep) {
+#pragma unroll
+    for (int i = 0; i < PD; ++i) {
+      const int tt = t + i * tstep;
+      if (tt >= ntile) break;
+      const int tp = tt + (PD - 1) * tstep;
+      if (tp < ntile) load_x(tp, xf[(i + PD - 1) % PD]);
+      tile_work(tt, xf[i]);
+    }
+  }
+}
+
+template <int CF, int NS>
+void launch_i8_1x1(const I8Args& a, hipStream_t s) {
+  const int M = a.B * a.OH * a.OW;
+  const int nblk = a.Cout / (16 * NS);
+  const int ntile = cdiv(M, 64);
+  // ~4 resident workgroups per CU, each channel block's tiles spread over the same count
+  const int per = std::max(1, std::min(ntile, 1024 / nblk));
+  // prefetch depth: input tiles in flight per wave (CF * 4 VGPRs each)
+  constexpr int PD = CF <= 2 ? 4 : (CF <= 4 ? 3 : 2);
+  hipLaunchKernelGGL((conv_i8_1x1_kernel<CF, NS, PD>), dim3(per * nblk), dim3(256), 0, s, a, nblk);
+  check_launch("conv_i8_1x1");
+}
+
+// (CF, NS): K fragments of 64 per pixel, 16-channel subtiles per workgroup; NS * CF <= 16
+// keeps the weight fragments at <= 64 VGPRs. First match wins (widest channel block).
+constexpr int kI8x1Inst[][2] = {{1, 16}, {1, 8}, {1, 4}, {2, 8}, {2, 4}, {4, 4}, {4, 2}, {8, 2}, {8, 1}, {16, 1}};
+
+void launch_i8_1x1_any(const I8Args& a, hipStream_t s, bool narrow) {
+  const int CF = a.Cin / 64, nsub = a.Cout / 16;
+  // the fitting instantiations of this CF, widest first; narrow (variant 6) takes the second
+  // when there is one -- half the accumulators and LDS, the input read once more (from L2)
+  int fit[4], nf = 0;
+  for (const auto& cn : kI8x1Inst)
+    if (cn[0] == CF && nsub % cn[1] == 0 && nf < 4) fit[nf++] = cn[1];
+  if (nf == 0) throw std::invalid_argument("conv_i8: no 1x1 streaming instantiation for this Cin / Cout");
+  const int ns = fit[narrow && nf > 1 ? 1 : 0];
+#define I8_1X1(CF_, NS_)                                    \
+  if (CF == CF_ && ns == NS_) { launch_i8_1x1<CF_, NS_>(a, s); return; }
+  I8_1X1(1, 16) I8_1X1(1, 8) I8_1X1(1, 4) I8_1X1(2, 8) I8_1X1(2, 4) I8_1X1(4, 4) I8_1X1(4, 2)
+  I8_1X1(8, 2) I8_1X1(8, 1) I8_1X1(16, 1)
+#undef I8_1X1
+  throw std::invalid_argument("conv_i8: no 1x1 streaming instantiation for this Cin / Cout");
+}
+
+bool conv_i8_1x1_ok(const ConvI8Params& p) {
+  const int CF = p.Cin / 64, nsub = p.Cout / 16;
+  bool inst = false;
+  for (const auto& cn : kI8x1Inst)
+    if (CF == cn[0] && nsub % cn[1] == 0) inst = true;
+  const int vec = p.out_mode == 0 ? 16 : 8;  // 16-byte stores
+  return p.KH == 1 && p.KW == 1 && p.stride == 1 && p.IH == p.OH && p.IW == p.OW && p.Cin % 64 == 0 &&
+         p.Cout % 16 == 0 && (p.ldo % vec) == 0 && (p.co_off % vec) == 0 && inst;
+}
+
 void conv_i8(const ConvI8Params& p, hipStream_t s) {
   if (p.Cin % 16) throw std::invalid_argument("conv_i8: Cin must be a multiple of 16");
   if (p.ldo < p.co_off + p.Cout) throw std::invalid_argument("conv_i8: bad ldo/co_off");
@@ -463,11 +668,17 @@ void conv_i8(const ConvI8Params& p, hipStream_t s) {
            p.ldo, p.co_off, p.act};
   const long long M = (long long)p.B * p.OH * p.OW;
   // variant: 0 auto, 1 register-fed, 2 LDS-DMA 128 x 128 (4 waves), 3 LDS-DMA
-  // 128 x 256 (8 waves), 4 LDS-DMA 256 x 128 (8 waves)
+  // 128 x 256 (8 waves), 4 LDS-DMA 256 x 128 (8 waves), 5 / 6 streaming 1x1 (stride 1,
+  // Cin % 64 == 0, Cout % 16 == 0, 16-byte aligned output; 6: the next narrower channel block)
   const bool glds_ok = p.KH * p.KW <= 16 && (long long)p.B * p.IH * p.IW * p.Cin < (1LL << 40);
   int v = p.variant;
   if (v == 0) v = (glds_ok && p.Cout >= 64 && M >= 8192) ? (p.Cout >= 256 ? 3 : 2) : 1;
-  if (v >= 2 && !glds_ok) throw std::invalid_argument("conv_i8: LDS-DMA variants need <= 16 taps");
+  if (v >= 2 && v <= 4 && !glds_ok) throw std::invalid_argument("conv_i8: LDS-DMA variants need <= 16 taps");
+  if (v == 5 || v == 6) {
+    if (!conv_i8_1x1_ok(p)) throw std::invalid_argument("conv_i8: streaming 1x1 variant does not fit this conv");
+    launch_i8_1x1_any(a, s, v == 6);
+    return;
+  }
   switch (v) {
     case 2: launch_i8_glds<4, 4, 2, 2>(a, s); return;
     case 3: launch_i8_glds<4, 4, 2, 4>(a, s); return;

@@ -27,14 +27,19 @@ from .quant import calibrate, pack_int8
 
 
 _I8_VARIANTS = (1, 2, 3, 4)  # register-fed, LDS-DMA 128x128 / 128x256 / 256x128
+# + 5 / 6: streaming 1x1 (weights resident per channel block, prefetched pixel tiles; 6 with
+# a narrower channel block) where it fits
 
 
 def I8(*args, **kw):
     """One int8 conv step as an autotuned Choice over the conv_i8 kernel variants."""
     from .hip_model import Choice
     I8.n = getattr(I8, "n", 0) + 1
+    variants = list(_I8_VARIANTS)
+    if K.conv_i8_1x1_ok(int8_out=kw.get("out_scale") is not None, **kw):
+        variants += [5, 6]
     c = Choice(f"i8conv{I8.n}", [(f"v{v}", [lambda *_, v=v: K.conv_i8(*args, variant=v, **kw)])
-                                 for v in _I8_VARIANTS])
+                                 for v in variants])
     c.desc = (f"M={kw['B'] * kw['OH'] * kw['OW']} Cin={kw['Cin']} Cout={kw['Cout']} "
               f"k={kw.get('k', 1)} s={kw.get('stride', 1)} d={kw.get('dil', 1)}")
     return c

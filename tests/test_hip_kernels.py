@@ -1267,6 +1267,42 @@ def test_conv_i8(Cin, Cout, k, stride, dil, res, mode, variant):
         assert _rel(_nchw(out).cpu(), ref) < 5e-3
 
 
+@pytest.mark.parametrize("Cin,Cout,res,img,mode,M", [
+    (64, 64, False, False, "i8", 2 * 33 * 33), (64, 256, True, False, "i8", 2 * 33 * 33 + 0),
+    (256, 64, False, True, "i8", 3 * 17 * 19), (128, 512, True, False, "i8", 2 * 17 * 17),
+    (256, 1024, True, False, "i8", 2 * 17 * 17), (512, 128, False, False, "bf16", 2 * 9 * 9),
+    (1024, 256, False, False, "i8", 1000), (64, 128, False, True, "i8", 3 * 77)])
+def test_conv_i8_1x1_stream_exact(Cin, Cout, res, img, mode, M):
+    """The streaming 1x1 variants (5, 6) against the register-fed one (1): same int32 sums;
+    bf16 outputs bit-identical, int8 outputs within one rounding step of the float epilogue
+    (pixel tails, residual, per-image bias)."""
+    K = _hip()
+    g = torch.Generator().manual_seed(31)
+    B = 3 if M % 3 == 0 else 1
+    H, W = 1, M // B
+    x8 = torch.randint(-127, 128, (B, H, W, Cin), generator=g, dtype=torch.int32).to(torch.int8).to(DEV)
+    w8 = torch.randint(-127, 128, (Cout, Cin), generator=g, dtype=torch.int32).to(torch.int8).to(DEV)
+    sc = (torch.rand(Cout, generator=g) * 1e-4).to(DEV)
+    bi = torch.randn(Cout, generator=g).to(DEV)
+    r8 = (torch.randint(-127, 128, (B, H, W, Cout), generator=g, dtype=torch.int32).to(torch.int8).to(DEV)
+          if res else None)
+    ib = torch.randn(B, Cout, generator=g).to(DEV) if img else None
+    outs = []
+    for v in (1, 5, 6):
+        dt = torch.int8 if mode == "i8" else torch.bfloat16
+        out = torch.zeros(B, H, W, Cout, dtype=dt, device=DEV)
+        K.conv_i8(x8, w8, sc, bi, out, B=B, IH=H, IW=W, Cin=Cin, OH=H, OW=W, Cout=Cout, act="relu",
+                  res=r8, res_scale=0.02, img_bias=ib, out_scale=0.05 if mode == "i8" else None, variant=v)
+        outs.append(out)
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        if mode == "bf16":  # the float epilogue, shared
+            assert torch.equal(outs[0].cpu(), o.cpu())
+        else:  # folded requantisation: at most one rounding step, rarely
+            d = (outs[0].cpu().int() - o.cpu().int()).abs()
+            assert d.max() <= 1 and (d > 0).float().mean() < 2e-3, (d.max(), (d > 0).float().mean())
+
+
 def test_int8_resnet50_matches_fake_quant():
     from semantic_segmentation_server_amd.models.deeplab import build_model
     from semantic_segmentation_server_amd.models.hip_int8 import HipDeepLabInt8
