@@ -534,6 +534,17 @@ __global__ __launch_bounds__(256) void conv_i8_1x1_kernel(I8Args a, int nblk) {
     for (int f = 0; f < CF; ++f)
       wf[j][f] = ld16(a.w + (size_t)(ch0 + j * 16 + r) * a.Cin + f * 64 + kq * 16);
   int* ep = ep_all + wid * 16 * EPP;
+  // the block's requantisation constants in LDS (int8 out: folded as in i8_requant16)
+  __shared__ __attribute__((aligned(16))) float s_sc[NB], s_bi[NB];
+  const float ios = a.inv_out_scale;
+  const float rs = a.res ? a.res_scale * ios : 0.f;
+  for (int i = threadIdx.x; i < NB; i += 256) {
+    s_sc[i] = a.scale[ch0 + i] * ios;
+    s_bi[i] = fmaf(a.bias[ch0 + i], ios, 128.f - 128.f * rs);
+  }
+  __syncthreads();
+  const float lo = a.act == ACT_NONE ? 1.f : 128.f;
+  const float hi = a.act == ACT_RELU6 ? fminf(255.f, 128.f + 6.f * ios) : 255.f;
   const int ntile = (M + 63) / 64;
   int t = blockIdx.x / nblk;
   i32x4v xf[PD][CF];  // PD tiles of input fragments in flight
@@ -544,7 +555,19 @@ __global__ __launch_bounds__(256) void conv_i8_1x1_kernel(I8Args a, int nblk) {
   };
   const int px = lane >> 2, cq = lane & 3;  // epilogue: 16 pixels x 4 lanes of 16 channels
   // one tile: MFMAs on xb, staged transpose, epilogue
+  constexpr int NG = (NS + 3) / 4;  // 16-channel groups per epilogue lane
   auto tile_work = [&](int tile, const i32x4v (&xb)[CF]) {
+    // this lane's residual bytes for the epilogue, in flight under the MFMAs
+    const int me = tile * 64 + wid * 16 + px;
+    i32x4v rq[NG];
+    if (a.res && a.out_mode == 0) {
+#pragma unroll
+      for (int i = 0; i < NG; ++i) {
+        const int g = cq + 4 * i;
+        rq[i] = (g < NS && me < M) ? *reinterpret_cast<const i32x4v*>(a.res + (size_t)me * a.Cout + ch0 + g * 16)
+                                   : i32x4v{0, 0, 0, 0};
+      }
+    }
     i32x4v acc[NS];
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
@@ -557,15 +580,40 @@ __global__ __launch_bounds__(256) void conv_i8_1x1_kernel(I8Args a, int nblk) {
     for (int j = 0; j < NS; ++j) *reinterpret_cast<i32x4v*>(ep + r * EPP + j * 16 + kq * 4) = acc[j];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const int m = tile * 64 + wid * 16 + px;
-#pragma unroll 1
-    for (int g = cq; g < NS; g += 4) {  // this lane's 16-channel groups of pixel px
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {  // this lane's 16-channel groups of pixel px
+      const int g = cq + 4 * gi;
+      if (g >= NS) break;
       i32x4v v[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) v[c] = *reinterpret_cast<const i32x4v*>(ep + px * EPP + g * 16 + c * 4);
       if (m >= M) continue;
       const int n = ch0 + g * 16;
       const size_t o = (size_t)m * a.ldo + a.co_off + n;
-      if (a.out_mode == 0) {  // int8 out: the folded requantisation
+      if (a.out_mode == 0 && !a.img_bias) {
+        // int8 out: the folded requantisation (i8_requant16) with the block's constants from
+        // LDS and the residual prefetched above
+        i32x4v pk;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float4 sc = *reinterpret_cast<const float4*>(s_sc + g * 16 + c * 4);
+          const float4 bi = *reinterpret_cast<const float4*>(s_bi + g * 16 + c * 4);
+          const float s4[4] = {sc.x, sc.y, sc.z, sc.w}, b4[4] = {bi.x, bi.y, bi.z, bi.w};
+          const unsigned ur = a.res ? ((unsigned)rq[gi][c] ^ 0x80808080u) : 0u;
+          unsigned w = 0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float z = fmaf((float)v[c][q], s4[q], b4[q]);
+            if (a.res) z = fmaf((float)((ur >> (8 * q)) & 0xffu), rs, z);
+            z = __builtin_amdgcn_fmed3f(z, lo, hi);
+            w = __builtin_amdgcn_cvt_pk_u8_f32(z, q, w);
+          }
+          pk[c] = (int)(w ^ 0x80808080u);
+        }
+        *reinterpret_cast<i32x4v*>(static_cast<int8_t*>(a.out) + o) = pk;
+        continue;
+      }
+      if (a.out_mode == 0) {  // int8 out with a per-image bias
         *reinterpret_cast<i32x4v*>(static_cast<int8_t*>(a.out) + o) = i8_requant16(a, v, m, n);
         continue;
       }
