@@ -672,28 +672,31 @@ void launch_i8_1x1(const I8Args& a, hipStream_t s) {
   // ~4 resident workgroups per CU, each channel block's tiles spread over the same count
   const int per = std::max(1, std::min(ntile, 1024 / nblk));
   // prefetch depth: input tiles in flight per wave (CF * 4 VGPRs each)
-  constexpr int PD = CF <= 2 ? 4 : (CF <= 4 ? 3 : 2);
+  constexpr int PD = CF * NS > 32 ? 2 : (CF <= 2 ? 4 : (CF <= 4 ? 3 : 2));
   hipLaunchKernelGGL((conv_i8_1x1_kernel<CF, NS, PD>), dim3(per * nblk), dim3(256), 0, s, a, nblk);
   check_launch("conv_i8_1x1");
 }
 
 // (CF, NS): K fragments of 64 per pixel, 16-channel subtiles per workgroup; NS * CF <= 16
 // keeps the weight fragments at <= 64 VGPRs. First match wins (widest channel block).
-constexpr int kI8x1Inst[][2] = {{1, 16}, {1, 8}, {1, 4}, {2, 8}, {2, 4}, {4, 4}, {4, 2}, {8, 2}, {8, 1}, {16, 1}};
+constexpr int kI8x1Inst[][2] = {{1, 16}, {1, 8}, {1, 4}, {2, 16}, {2, 8}, {2, 4}, {4, 16}, {4, 8}, {4, 4}, {4, 2},
+                                 {8, 8}, {8, 4}, {8, 2}, {8, 1}, {16, 4}, {16, 2}, {16, 1}};
 
-void launch_i8_1x1_any(const I8Args& a, hipStream_t s, bool narrow) {
+void launch_i8_1x1_any(const I8Args& a, hipStream_t s, int which) {
   const int CF = a.Cin / 64, nsub = a.Cout / 16;
-  // the fitting instantiations of this CF, widest first; narrow (variant 6) takes the second
-  // when there is one -- half the accumulators and LDS, the input read once more (from L2)
-  int fit[4], nf = 0;
+  // the fitting instantiations of this CF, widest channel block first; `which` (variants
+  // 5, 6, 10, 11 -> 0..3) picks one: narrower blocks hold fewer weight / accumulator VGPRs
+  // and read the input once more per extra block (from L2)
+  int fit[8], nf = 0;
   for (const auto& cn : kI8x1Inst)
-    if (cn[0] == CF && nsub % cn[1] == 0 && nf < 4) fit[nf++] = cn[1];
+    if (cn[0] == CF && nsub % cn[1] == 0 && nf < 8) fit[nf++] = cn[1];
   if (nf == 0) throw std::invalid_argument("conv_i8: no 1x1 streaming instantiation for this Cin / Cout");
-  const int ns = fit[narrow && nf > 1 ? 1 : 0];
+  const int ns = fit[std::min(which, nf - 1)];
 #define I8_1X1(CF_, NS_)                                    \
   if (CF == CF_ && ns == NS_) { launch_i8_1x1<CF_, NS_>(a, s); return; }
-  I8_1X1(1, 16) I8_1X1(1, 8) I8_1X1(1, 4) I8_1X1(2, 8) I8_1X1(2, 4) I8_1X1(4, 4) I8_1X1(4, 2)
-  I8_1X1(8, 2) I8_1X1(8, 1) I8_1X1(16, 1)
+  I8_1X1(1, 16) I8_1X1(1, 8) I8_1X1(1, 4) I8_1X1(2, 16) I8_1X1(2, 8) I8_1X1(2, 4) I8_1X1(4, 16)
+  I8_1X1(4, 8) I8_1X1(4, 4) I8_1X1(4, 2) I8_1X1(8, 8) I8_1X1(8, 4) I8_1X1(8, 2) I8_1X1(8, 1)
+  I8_1X1(16, 4) I8_1X1(16, 2) I8_1X1(16, 1)
 #undef I8_1X1
   throw std::invalid_argument("conv_i8: no 1x1 streaming instantiation for this Cin / Cout");
 }
@@ -716,15 +719,16 @@ void conv_i8(const ConvI8Params& p, hipStream_t s) {
            p.ldo, p.co_off, p.act};
   const long long M = (long long)p.B * p.OH * p.OW;
   // variant: 0 auto, 1 register-fed, 2 LDS-DMA 128 x 128 (4 waves), 3 LDS-DMA
-  // 128 x 256 (8 waves), 4 LDS-DMA 256 x 128 (8 waves), 5 / 6 streaming 1x1 (stride 1,
-  // Cin % 64 == 0, Cout % 16 == 0, 16-byte aligned output; 6: the next narrower channel block)
+  // 128 x 256 (8 waves), 4 LDS-DMA 256 x 128 (8 waves), 5 / 6 / 10 / 11 streaming 1x1 (stride 1,
+  // Cin % 64 == 0, Cout % 16 == 0, 16-byte aligned output; the widest fitting channel block,
+  // then the next narrower ones)
   const bool glds_ok = p.KH * p.KW <= 16 && (long long)p.B * p.IH * p.IW * p.Cin < (1LL << 40);
   int v = p.variant;
   if (v == 0) v = (glds_ok && p.Cout >= 64 && M >= 8192) ? (p.Cout >= 256 ? 3 : 2) : 1;
   if (v >= 2 && v <= 4 && !glds_ok) throw std::invalid_argument("conv_i8: LDS-DMA variants need <= 16 taps");
-  if (v == 5 || v == 6) {
+  if (v == 5 || v == 6 || v == 10 || v == 11) {
     if (!conv_i8_1x1_ok(p)) throw std::invalid_argument("conv_i8: streaming 1x1 variant does not fit this conv");
-    launch_i8_1x1_any(a, s, v == 6);
+    launch_i8_1x1_any(a, s, v == 5 ? 0 : v == 6 ? 1 : v == 10 ? 2 : 3);
     return;
   }
   switch (v) {

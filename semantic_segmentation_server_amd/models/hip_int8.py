@@ -37,7 +37,7 @@ def I8(*args, **kw):
     I8.n = getattr(I8, "n", 0) + 1
     variants = list(_I8_VARIANTS)
     if K.conv_i8_1x1_ok(int8_out=kw.get("out_scale") is not None, **kw):
-        variants += [5, 6]
+        variants += [5, 6, 10, 11]
     c = Choice(f"i8conv{I8.n}", [(f"v{v}", [lambda *_, v=v: K.conv_i8(*args, variant=v, **kw)])
                                  for v in variants])
     c.desc = (f"M={kw['B'] * kw['OH'] * kw['OW']} Cin={kw['Cin']} Cout={kw['Cout']} "

@@ -760,7 +760,8 @@ def stem_mfma(frames, lut_x, lut_y, wpk, bias, out, *, H, W, OH, OW, Cout, k, st
 
 
 # (K fragments of 64, 16-channel subtiles) instantiated by conv_i8.hip's streaming 1x1 kernel
-_I8_1X1_INST = ((1, 16), (1, 8), (1, 4), (2, 8), (2, 4), (4, 4), (4, 2), (8, 2), (8, 1), (16, 1))
+_I8_1X1_INST = ((1, 16), (1, 8), (1, 4), (2, 16), (2, 8), (2, 4), (4, 16), (4, 8), (4, 4), (4, 2),
+                (8, 8), (8, 4), (8, 2), (8, 1), (16, 4), (16, 2), (16, 1))
 
 
 def conv_i8_1x1_ok(*, Cin, Cout, k=1, stride=1, ldo=None, co_off=0, int8_out=True, **_) -> bool:
@@ -776,10 +777,11 @@ def conv_i8(x, w8, scale, bias, out, *, B, IH, IW, Cin, OH, OW, Cout, k=1, strid
             out_scale=None, variant=0) -> torch.Tensor:
     """int8 NHWC conv. out int8 (out_scale given: v / out_scale rounded) or bf16.
     variant: 0 auto, 1 register-fed, 2/3/4 LDS-DMA 128x128 / 128x256 / 256x128 tiles,
-    5 / 6 streaming 1x1 (stride 1; conv_i8_1x1_ok; 6: a narrower channel block)."""
-    if variant not in (0, 1, 2, 3, 4, 5, 6) or (2 <= variant <= 4 and k * k > 16):
+    5 / 6 / 10 / 11 streaming 1x1 (stride 1; conv_i8_1x1_ok; the widest fitting channel block,
+    then narrower ones)."""
+    if variant not in (0, 1, 2, 3, 4, 5, 6, 10, 11) or (2 <= variant <= 4 and k * k > 16):
         raise ValueError("conv_i8: bad variant")
-    if variant in (5, 6) and not conv_i8_1x1_ok(Cin=Cin, Cout=Cout, k=k, stride=stride, ldo=ldo, co_off=co_off,
+    if variant in (5, 6, 10, 11) and not conv_i8_1x1_ok(Cin=Cin, Cout=Cout, k=k, stride=stride, ldo=ldo, co_off=co_off,
                                            int8_out=out_scale is not None):
         raise ValueError("conv_i8: the streaming 1x1 variant does not fit this conv")
     ldo = Cout if ldo is None else ldo

@@ -1288,7 +1288,7 @@ def test_conv_i8_1x1_stream_exact(Cin, Cout, res, img, mode, M):
           if res else None)
     ib = torch.randn(B, Cout, generator=g).to(DEV) if img else None
     outs = []
-    for v in (1, 5, 6):
+    for v in (1, 5, 6, 10, 11):
         dt = torch.int8 if mode == "i8" else torch.bfloat16
         out = torch.zeros(B, H, W, Cout, dtype=dt, device=DEV)
         K.conv_i8(x8, w8, sc, bi, out, B=B, IH=H, IW=W, Cin=Cin, OH=H, OW=W, Cout=Cout, act="relu",
