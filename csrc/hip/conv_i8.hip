@@ -515,8 +515,11 @@ __global__ void gap_i8_reduce(const float* __restrict__ part, float* __restrict_
 // pixel per lane (16-byte residual loads and stores). Exact int32 accumulation; the int8
 // epilogue folds the requantisation into the affine terms (see below: within one rounding
 // step of the other variants), the bf16 one is theirs.
-template <int CF, int NS, int PD>
+template <int CF, int NS, int PD, int KT>
 __global__ __launch_bounds__(256) void conv_i8_1x1_kernel(I8Args a, int nblk) {
+  // KT = 1 (1x1, stride 1) or 9 (3x3, any stride / dilation: the taps are extra K fragments
+  // read from the shifted pixels, zero outside the image)
+  constexpr int KF = KT * CF;           // K fragments of 64 per output pixel
   constexpr int NB = 16 * NS;           // output channels per workgroup
   constexpr int EPP = NB + 4;           // staged row pitch (ints): 16 distinct bank groups
   __shared__ __attribute__((aligned(16))) int ep_all[4 * 16 * EPP];
@@ -527,12 +530,12 @@ __global__ __launch_bounds__(256) void conv_i8_1x1_kernel(I8Args a, int nblk) {
   const int tstep = gridDim.x / nblk;   // (the grid is a multiple of nblk)
   const int ch0 = nb * NB;
   // weights: A fragments (rows = out channels, 16 K bytes per lane), resident
-  i32x4v wf[NS][CF];
+  i32x4v wf[NS][KF];
 #pragma unroll
   for (int j = 0; j < NS; ++j)
 #pragma unroll
-    for (int f = 0; f < CF; ++f)
-      wf[j][f] = ld16(a.w + (size_t)(ch0 + j * 16 + r) * a.Cin + f * 64 + kq * 16);
+    for (int f = 0; f < KF; ++f)  // [Cout][tap][Cin]: fragment f = tap * CF + (f % CF)
+      wf[j][f] = ld16(a.w + (size_t)(ch0 + j * 16 + r) * KT * a.Cin + (f / CF) * a.Cin + (f % CF) * 64 + kq * 16);
   int* ep = ep_all + wid * 16 * EPP;
   // the block's requantisation constants in LDS (int8 out: folded as in i8_requant16)
   __shared__ __attribute__((aligned(16))) float s_sc[NB], s_bi[NB];
@@ -547,16 +550,29 @@ __global__ __launch_bounds__(256) void conv_i8_1x1_kernel(I8Args a, int nblk) {
   const float hi = a.act == ACT_RELU6 ? fminf(255.f, 128.f + 6.f * ios) : 255.f;
   const int ntile = (M + 63) / 64;
   int t = blockIdx.x / nblk;
-  i32x4v xf[PD][CF];  // PD tiles of input fragments in flight
-  auto load_x = [&](int tile, i32x4v (&dst)[CF]) {
+  i32x4v xf[PD][KF];  // PD tiles of input fragments in flight
+  auto load_x = [&](int tile, i32x4v (&dst)[KF]) {
     const int m = min(tile * 64 + wid * 16 + r, M - 1);  // clamped: tail pixels are not stored
+    if constexpr (KT == 1) {
 #pragma unroll
-    for (int f = 0; f < CF; ++f) dst[f] = ld16(a.in + (size_t)m * a.Cin + f * 64 + kq * 16);
+      for (int f = 0; f < CF; ++f) dst[f] = ld16(a.in + (size_t)m * a.Cin + f * 64 + kq * 16);
+    } else {
+      const int b = m / (a.OH * a.OW), rem = m - b * a.OH * a.OW;
+      const int oy = rem / a.OW, ox = rem - oy * a.OW;
+#pragma unroll
+      for (int tp = 0; tp < KT; ++tp) {
+        const int iy = oy * a.stride + (tp / 3 - 1) * a.dil, ix = ox * a.stride + (tp % 3 - 1) * a.dil;
+        const bool ok = iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW;
+        const int8_t* src = a.in + (((size_t)b * a.IH + (ok ? iy : 0)) * a.IW + (ok ? ix : 0)) * a.Cin + kq * 16;
+#pragma unroll
+        for (int f = 0; f < CF; ++f) dst[tp * CF + f] = ok ? ld16(src + f * 64) : i32x4v{0, 0, 0, 0};
+      }
+    }
   };
   const int px = lane >> 2, cq = lane & 3;  // epilogue: 16 pixels x 4 lanes of 16 channels
   // one tile: MFMAs on xb, staged transpose, epilogue
   constexpr int NG = (NS + 3) / 4;  // 16-channel groups per epilogue lane
-  auto tile_work = [&](int tile, const i32x4v (&xb)[CF]) {
+  auto tile_work = [&](int tile, const i32x4v (&xb)[KF]) {
     // this lane's residual bytes for the epilogue, in flight under the MFMAs
     const int me = tile * 64 + wid * 16 + px;
     i32x4v rq[NG];
@@ -573,7 +589,7 @@ __global__ __launch_bounds__(256) void conv_i8_1x1_kernel(I8Args a, int nblk) {
     for (int j = 0; j < NS; ++j) {
       acc[j] = i32x4v{0, 0, 0, 0};
 #pragma unroll
-      for (int f = 0; f < CF; ++f) acc[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wf[j][f], xb[f], acc[j], 0, 0, 0);
+      for (int f = 0; f < KF; ++f) acc[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wf[j][f], xb[f], acc[j], 0, 0, 0);
     }
     // stage [16 px][NB ch]: lane (r = pixel, kq) holds channels j*16 + kq*4 .. +3
 #pragma unroll
@@ -664,7 +680,7 @@ __global__ __launch_bounds__(256) void conv_i8_1x1_kernel(I8Args a, int nblk) {
   }
 }
 
-template <int CF, int NS>
+template <int CF, int NS, int KT = 1>
 void launch_i8_1x1(const I8Args& a, hipStream_t s) {
   const int M = a.B * a.OH * a.OW;
   const int nblk = a.Cout / (16 * NS);
@@ -672,8 +688,9 @@ void launch_i8_1x1(const I8Args& a, hipStream_t s) {
   // ~4 resident workgroups per CU, each channel block's tiles spread over the same count
   const int per = std::max(1, std::min(ntile, 1024 / nblk));
   // prefetch depth: input tiles in flight per wave (CF * 4 VGPRs each)
-  constexpr int PD = CF * NS > 32 ? 2 : (CF <= 2 ? 4 : (CF <= 4 ? 3 : 2));
-  hipLaunchKernelGGL((conv_i8_1x1_kernel<CF, NS, PD>), dim3(per * nblk), dim3(256), 0, s, a, nblk);
+  constexpr int KF = KT * CF;
+  constexpr int PD = KT > 1 ? 2 : (KF * NS > 32 ? 2 : (KF <= 2 ? 4 : (KF <= 4 ? 3 : 2)));
+  hipLaunchKernelGGL((conv_i8_1x1_kernel<CF, NS, PD, KT>), dim3(per * nblk), dim3(256), 0, s, a, nblk);
   check_launch("conv_i8_1x1");
 }
 
@@ -681,6 +698,23 @@ void launch_i8_1x1(const I8Args& a, hipStream_t s) {
 // keeps the weight fragments at <= 64 VGPRs. First match wins (widest channel block).
 constexpr int kI8x1Inst[][2] = {{1, 16}, {1, 8}, {1, 4}, {2, 16}, {2, 8}, {2, 4}, {4, 16}, {4, 8}, {4, 4}, {4, 2},
                                  {8, 8}, {8, 4}, {8, 2}, {8, 1}, {16, 4}, {16, 2}, {16, 1}};
+
+// 3x3 (KT = 9): 9 * CF * NS <= 36 weight fragments (144 VGPRs), Cin <= 128
+constexpr int kI8x3Inst[][2] = {{1, 4}, {1, 2}, {2, 2}, {2, 1}};
+
+void launch_i8_3x3_any(const I8Args& a, hipStream_t s, int which) {
+  const int CF = a.Cin / 64, nsub = a.Cout / 16;
+  int fit[8], nf = 0;
+  for (const auto& cn : kI8x3Inst)
+    if (cn[0] == CF && nsub % cn[1] == 0 && nf < 8) fit[nf++] = cn[1];
+  if (nf == 0) throw std::invalid_argument("conv_i8: no 3x3 streaming instantiation for this Cin / Cout");
+  const int ns = fit[std::min(which, nf - 1)];
+#define I8_3X3(CF_, NS_)                                    \
+  if (CF == CF_ && ns == NS_) { launch_i8_1x1<CF_, NS_, 9>(a, s); return; }
+  I8_3X3(1, 4) I8_3X3(1, 2) I8_3X3(2, 2) I8_3X3(2, 1)
+#undef I8_3X3
+  throw std::invalid_argument("conv_i8: no 3x3 streaming instantiation for this Cin / Cout");
+}
 
 void launch_i8_1x1_any(const I8Args& a, hipStream_t s, int which) {
   const int CF = a.Cin / 64, nsub = a.Cout / 16;
@@ -703,12 +737,18 @@ void launch_i8_1x1_any(const I8Args& a, hipStream_t s, int which) {
 
 bool conv_i8_1x1_ok(const ConvI8Params& p) {
   const int CF = p.Cin / 64, nsub = p.Cout / 16;
+  const bool k3 = p.KH == 3 && p.KW == 3;
   bool inst = false;
-  for (const auto& cn : kI8x1Inst)
-    if (CF == cn[0] && nsub % cn[1] == 0) inst = true;
+  if (k3) {
+    for (const auto& cn : kI8x3Inst)
+      if (CF == cn[0] && nsub % cn[1] == 0) inst = true;
+  } else {
+    for (const auto& cn : kI8x1Inst)
+      if (CF == cn[0] && nsub % cn[1] == 0) inst = true;
+  }
   const int vec = p.out_mode == 0 ? 16 : 8;  // 16-byte stores
-  return p.KH == 1 && p.KW == 1 && p.stride == 1 && p.IH == p.OH && p.IW == p.OW && p.Cin % 64 == 0 &&
-         p.Cout % 16 == 0 && (p.ldo % vec) == 0 && (p.co_off % vec) == 0 && inst;
+  const bool geom = k3 || (p.KH == 1 && p.KW == 1 && p.stride == 1 && p.IH == p.OH && p.IW == p.OW);
+  return geom && p.Cin % 64 == 0 && p.Cout % 16 == 0 && (p.ldo % vec) == 0 && (p.co_off % vec) == 0 && inst;
 }
 
 void conv_i8(const ConvI8Params& p, hipStream_t s) {
@@ -728,7 +768,9 @@ void conv_i8(const ConvI8Params& p, hipStream_t s) {
   if (v >= 2 && v <= 4 && !glds_ok) throw std::invalid_argument("conv_i8: LDS-DMA variants need <= 16 taps");
   if (v == 5 || v == 6 || v == 10 || v == 11) {
     if (!conv_i8_1x1_ok(p)) throw std::invalid_argument("conv_i8: streaming 1x1 variant does not fit this conv");
-    launch_i8_1x1_any(a, s, v == 5 ? 0 : v == 6 ? 1 : v == 10 ? 2 : 3);
+    const int which = v == 5 ? 0 : v == 6 ? 1 : v == 10 ? 2 : 3;
+    if (p.KH == 3) launch_i8_3x3_any(a, s, which);
+    else launch_i8_1x1_any(a, s, which);
     return;
   }
   switch (v) {

@@ -764,12 +764,22 @@ _I8_1X1_INST = ((1, 16), (1, 8), (1, 4), (2, 16), (2, 8), (2, 4), (4, 16), (4, 8
                 (8, 8), (8, 4), (8, 2), (8, 1), (16, 4), (16, 2), (16, 1))
 
 
-def conv_i8_1x1_ok(*, Cin, Cout, k=1, stride=1, ldo=None, co_off=0, int8_out=True, **_) -> bool:
-    """Whether the streaming 1x1 variant (5) covers this conv (mirrors conv_i8_1x1_ok)."""
+_I8_3X3_INST = ((1, 4), (1, 2), (2, 2), (2, 1))
+
+
+def conv_i8_1x1_ok(*, Cin, Cout, k=1, stride=1, ldo=None, co_off=0, int8_out=True, IH=None, OH=None,
+                   IW=None, OW=None, **_) -> bool:
+    """Whether the streaming variants (5 / 6 / 10 / 11) cover this conv: 1x1 stride 1, or
+    3x3 with few enough weight fragments (mirrors conv_i8.hip conv_i8_1x1_ok)."""
     ldo = Cout if ldo is None else ldo
     vec = 16 if int8_out else 8
-    return (k == 1 and stride == 1 and Cin % 64 == 0 and Cout % 16 == 0 and ldo % vec == 0
-            and co_off % vec == 0 and any(Cin // 64 == cf and (Cout // 16) % ns == 0 for cf, ns in _I8_1X1_INST))
+    if k == 3:
+        table, geom = _I8_3X3_INST, True
+    else:
+        table = _I8_1X1_INST
+        geom = k == 1 and stride == 1 and (IH is None or IH == OH) and (IW is None or IW == OW)
+    return (geom and Cin % 64 == 0 and Cout % 16 == 0 and ldo % vec == 0 and co_off % vec == 0
+            and any(Cin // 64 == cf and (Cout // 16) % ns == 0 for cf, ns in table))
 
 
 def conv_i8(x, w8, scale, bias, out, *, B, IH, IW, Cin, OH, OW, Cout, k=1, stride=1, dil=1,

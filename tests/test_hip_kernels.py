@@ -1303,6 +1303,33 @@ def test_conv_i8_1x1_stream_exact(Cin, Cout, res, img, mode, M):
             assert d.max() <= 1 and (d > 0).float().mean() < 2e-3, (d.max(), (d > 0).float().mean())
 
 
+@pytest.mark.parametrize("Cin,Cout,stride,dil,res", [(64, 64, 1, 1, False), (128, 128, 1, 1, True),
+                                                    (128, 64, 2, 1, False), (64, 32, 1, 2, False)])
+def test_conv_i8_3x3_stream(Cin, Cout, stride, dil, res):
+    """The streaming kernel's 3x3 form (taps as extra K fragments from shifted pixels, zero
+    outside the image) against the register-fed variant: within one rounding step."""
+    K = _hip()
+    g = torch.Generator().manual_seed(33)
+    B, H = 2, 19
+    OH = (H - 1) // stride + 1
+    x8 = torch.randint(-127, 128, (B, H, H, Cin), generator=g, dtype=torch.int32).to(torch.int8).to(DEV)
+    w8 = torch.randint(-127, 128, (Cout, 3, 3, Cin), generator=g, dtype=torch.int32).to(torch.int8).to(DEV)
+    sc = (torch.rand(Cout, generator=g) * 1e-5).to(DEV)
+    bi = torch.randn(Cout, generator=g).to(DEV)
+    r8 = (torch.randint(-127, 128, (B, OH, OH, Cout), generator=g, dtype=torch.int32).to(torch.int8).to(DEV)
+          if res else None)
+    outs = []
+    for v in (1, 5, 6):
+        out = torch.zeros(B, OH, OH, Cout, dtype=torch.int8, device=DEV)
+        K.conv_i8(x8, w8, sc, bi, out, B=B, IH=H, IW=H, Cin=Cin, OH=OH, OW=OH, Cout=Cout, k=3, stride=stride,
+                  dil=dil, act="relu", res=r8, res_scale=0.02, out_scale=0.05, variant=v)
+        outs.append(out)
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        d = (outs[0].cpu().int() - o.cpu().int()).abs()
+        assert d.max() <= 1 and (d > 0).float().mean() < 2e-3, (d.max(), (d > 0).float().mean())
+
+
 def test_int8_resnet50_matches_fake_quant():
     from semantic_segmentation_server_amd.models.deeplab import build_model
     from semantic_segmentation_server_amd.models.hip_int8 import HipDeepLabInt8
