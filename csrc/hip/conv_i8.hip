@@ -515,8 +515,10 @@ __global__ void gap_i8_reduce(const float* __restrict__ part, float* __restrict_
 // pixel per lane (16-byte residual loads and stores). Exact int32 accumulation; the int8
 // epilogue folds the requantisation into the affine terms (see below: within one rounding
 // step of the other variants), the bf16 one is theirs.
-template <int CF, int NS, int PD, int KT>
+template <int CF, int NS, int PD, int KT, bool WL = false>
 __global__ __launch_bounds__(256) void conv_i8_1x1_kernel(I8Args a, int nblk) {
+  // WL: the weight fragments live in LDS (NS * KF KiB, one conflict-free ds_read_b128 per
+  // MFMA) instead of VGPRs -- fewer registers, more resident waves for the 3x3 form
   // KT = 1 (1x1, stride 1) or 9 (3x3, any stride / dilation: the taps are extra K fragments
   // read from the shifted pixels, zero outside the image)
   constexpr int KF = KT * CF;           // K fragments of 64 per output pixel
@@ -530,12 +532,22 @@ __global__ __launch_bounds__(256) void conv_i8_1x1_kernel(I8Args a, int nblk) {
   const int tstep = gridDim.x / nblk;   // (the grid is a multiple of nblk)
   const int ch0 = nb * NB;
   // weights: A fragments (rows = out channels, 16 K bytes per lane), resident
-  i32x4v wf[NS][KF];
+  constexpr int NWF = WL ? 1 : NS, KWF = WL ? 1 : KF;
+  i32x4v wf[NWF][KWF];
+  __shared__ __attribute__((aligned(16))) i32x4v s_w[WL ? NS * KF * 64 : 1];
+  if constexpr (WL) {
+    for (int i = threadIdx.x; i < NS * KF * 64; i += 256) {
+      const int l = i & 63, jf = i >> 6, j = jf / KF, f = jf - j * KF;
+      s_w[i] = ld16(a.w + (size_t)(ch0 + j * 16 + (l & 15)) * KT * a.Cin + (f / CF) * a.Cin + (f % CF) * 64 +
+                    (l >> 4) * 16);
+    }
+  } else {
 #pragma unroll
-  for (int j = 0; j < NS; ++j)
+    for (int j = 0; j < NS; ++j)
 #pragma unroll
-    for (int f = 0; f < KF; ++f)  // [Cout][tap][Cin]: fragment f = tap * CF + (f % CF)
-      wf[j][f] = ld16(a.w + (size_t)(ch0 + j * 16 + r) * KT * a.Cin + (f / CF) * a.Cin + (f % CF) * 64 + kq * 16);
+      for (int f = 0; f < KF; ++f)  // [Cout][tap][Cin]: fragment f = tap * CF + (f % CF)
+        wf[j][f] = ld16(a.w + (size_t)(ch0 + j * 16 + r) * KT * a.Cin + (f / CF) * a.Cin + (f % CF) * 64 + kq * 16);
+  }
   int* ep = ep_all + wid * 16 * EPP;
   // the block's requantisation constants in LDS (int8 out: folded as in i8_requant16)
   __shared__ __attribute__((aligned(16))) float s_sc[NB], s_bi[NB];
@@ -589,7 +601,10 @@ __global__ __launch_bounds__(256) void conv_i8_1x1_kernel(I8Args a, int nblk) {
     for (int j = 0; j < NS; ++j) {
       acc[j] = i32x4v{0, 0, 0, 0};
 #pragma unroll
-      for (int f = 0; f < KF; ++f) acc[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wf[j][f], xb[f], acc[j], 0, 0, 0);
+      for (int f = 0; f < KF; ++f) {
+        const i32x4v wa = WL ? s_w[(j * KF + f) * 64 + lane] : wf[WL ? 0 : j][WL ? 0 : f];
+        acc[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wa, xb[f], acc[j], 0, 0, 0);
+      }
     }
     // stage [16 px][NB ch]: lane (r = pixel, kq) holds channels j*16 + kq*4 .. +3
 #pragma unroll
@@ -680,7 +695,7 @@ __global__ __launch_bounds__(256) void conv_i8_1x1_kernel(I8Args a, int nblk) {
   }
 }
 
-template <int CF, int NS, int KT = 1>
+template <int CF, int NS, int KT = 1, bool WL = false>
 void launch_i8_1x1(const I8Args& a, hipStream_t s) {
   const int M = a.B * a.OH * a.OW;
   const int nblk = a.Cout / (16 * NS);
@@ -689,8 +704,10 @@ void launch_i8_1x1(const I8Args& a, hipStream_t s) {
   const int per = std::max(1, std::min(ntile, 1024 / nblk));
   // prefetch depth: input tiles in flight per wave (CF * 4 VGPRs each)
   constexpr int KF = KT * CF;
-  constexpr int PD = KT > 1 ? 2 : (KF * NS > 32 ? 2 : (KF <= 2 ? 4 : (KF <= 4 ? 3 : 2)));
-  hipLaunchKernelGGL((conv_i8_1x1_kernel<CF, NS, PD, KT>), dim3(per * nblk), dim3(256), 0, s, a, nblk);
+  // (the LDS-weight 3x3 form keeps no tile in flight: its 9 * CF input fragments per tile
+  // would double the registers; occupancy hides the latency instead)
+  constexpr int PD = KT > 1 ? (WL ? 1 : 2) : (KF * NS > 32 ? 2 : (KF <= 2 ? 4 : (KF <= 4 ? 3 : 2)));
+  hipLaunchKernelGGL((conv_i8_1x1_kernel<CF, NS, PD, KT, WL>), dim3(per * nblk), dim3(256), 0, s, a, nblk);
   check_launch("conv_i8_1x1");
 }
 
@@ -699,20 +716,43 @@ void launch_i8_1x1(const I8Args& a, hipStream_t s) {
 constexpr int kI8x1Inst[][2] = {{1, 16}, {1, 8}, {1, 4}, {2, 16}, {2, 8}, {2, 4}, {4, 16}, {4, 8}, {4, 4}, {4, 2},
                                  {8, 8}, {8, 4}, {8, 2}, {8, 1}, {16, 4}, {16, 2}, {16, 1}};
 
-// 3x3 (KT = 9): 9 * CF * NS <= 36 weight fragments (144 VGPRs), Cin <= 128
+// 3x3 (KT = 9), weights in VGPRs: 9 * CF * NS <= 36 fragments (144 VGPRs), Cin <= 128;
+// weights in LDS (WL): NS * 9 * CF KiB <= 72
 constexpr int kI8x3Inst[][2] = {{1, 4}, {1, 2}, {2, 2}, {2, 1}};
+constexpr int kI8x3InstL[][2] = {{1, 8}, {1, 4}, {2, 4}, {2, 2}, {4, 2}, {4, 1}};
 
 void launch_i8_3x3_any(const I8Args& a, hipStream_t s, int which) {
   const int CF = a.Cin / 64, nsub = a.Cout / 16;
-  int fit[8], nf = 0;
-  for (const auto& cn : kI8x3Inst)
-    if (cn[0] == CF && nsub % cn[1] == 0 && nf < 8) fit[nf++] = cn[1];
+  // variants 10 / 11: the LDS-weight form; either form falls back to the other when it has
+  // no instantiation for this (Cin, Cout)
+  auto collect = [&](bool l, int (&fit)[8]) {
+    int n = 0;
+    if (l) {
+      for (const auto& cn : kI8x3InstL)
+        if (cn[0] == CF && nsub % cn[1] == 0 && n < 8) fit[n++] = cn[1];
+    } else {
+      for (const auto& cn : kI8x3Inst)
+        if (cn[0] == CF && nsub % cn[1] == 0 && n < 8) fit[n++] = cn[1];
+    }
+    return n;
+  };
+  bool wl = which >= 2;
+  int fit[8];
+  int nf = collect(wl, fit);
+  if (nf == 0) {
+    wl = !wl;
+    nf = collect(wl, fit);
+  }
   if (nf == 0) throw std::invalid_argument("conv_i8: no 3x3 streaming instantiation for this Cin / Cout");
-  const int ns = fit[std::min(which, nf - 1)];
+  const int ns = fit[std::min(which & 1, nf - 1)];
 #define I8_3X3(CF_, NS_)                                    \
-  if (CF == CF_ && ns == NS_) { launch_i8_1x1<CF_, NS_, 9>(a, s); return; }
+  if (!wl && CF == CF_ && ns == NS_) { launch_i8_1x1<CF_, NS_, 9>(a, s); return; }
+#define I8_3X3L(CF_, NS_)                                   \
+  if (wl && CF == CF_ && ns == NS_) { launch_i8_1x1<CF_, NS_, 9, true>(a, s); return; }
   I8_3X3(1, 4) I8_3X3(1, 2) I8_3X3(2, 2) I8_3X3(2, 1)
+  I8_3X3L(1, 8) I8_3X3L(1, 4) I8_3X3L(2, 4) I8_3X3L(2, 2) I8_3X3L(4, 2) I8_3X3L(4, 1)
 #undef I8_3X3
+#undef I8_3X3L
   throw std::invalid_argument("conv_i8: no 3x3 streaming instantiation for this Cin / Cout");
 }
 
@@ -741,6 +781,8 @@ bool conv_i8_1x1_ok(const ConvI8Params& p) {
   bool inst = false;
   if (k3) {
     for (const auto& cn : kI8x3Inst)
+      if (CF == cn[0] && nsub % cn[1] == 0) inst = true;
+    for (const auto& cn : kI8x3InstL)
       if (CF == cn[0] && nsub % cn[1] == 0) inst = true;
   } else {
     for (const auto& cn : kI8x1Inst)

@@ -764,7 +764,8 @@ _I8_1X1_INST = ((1, 16), (1, 8), (1, 4), (2, 16), (2, 8), (2, 4), (4, 16), (4, 8
                 (8, 8), (8, 4), (8, 2), (8, 1), (16, 4), (16, 2), (16, 1))
 
 
-_I8_3X3_INST = ((1, 4), (1, 2), (2, 2), (2, 1))
+_I8_3X3_INST = ((1, 4), (1, 2), (2, 2), (2, 1),                    # weights in VGPRs (5 / 6)
+                (1, 8), (2, 4), (4, 2), (4, 1))                    # + weights in LDS (10 / 11)
 
 
 def conv_i8_1x1_ok(*, Cin, Cout, k=1, stride=1, ldo=None, co_off=0, int8_out=True, IH=None, OH=None,

@@ -1304,7 +1304,8 @@ def test_conv_i8_1x1_stream_exact(Cin, Cout, res, img, mode, M):
 
 
 @pytest.mark.parametrize("Cin,Cout,stride,dil,res", [(64, 64, 1, 1, False), (128, 128, 1, 1, True),
-                                                    (128, 64, 2, 1, False), (64, 32, 1, 2, False)])
+                                                    (128, 64, 2, 1, False), (64, 32, 1, 2, False),
+                                                    (256, 256, 1, 2, False)])
 def test_conv_i8_3x3_stream(Cin, Cout, stride, dil, res):
     """The streaming kernel's 3x3 form (taps as extra K fragments from shifted pixels, zero
     outside the image) against the register-fed variant: within one rounding step."""
@@ -1319,7 +1320,7 @@ def test_conv_i8_3x3_stream(Cin, Cout, stride, dil, res):
     r8 = (torch.randint(-127, 128, (B, OH, OH, Cout), generator=g, dtype=torch.int32).to(torch.int8).to(DEV)
           if res else None)
     outs = []
-    for v in (1, 5, 6):
+    for v in (1, 5, 6, 10, 11):
         out = torch.zeros(B, OH, OH, Cout, dtype=torch.int8, device=DEV)
         K.conv_i8(x8, w8, sc, bi, out, B=B, IH=H, IW=H, Cin=Cin, OH=OH, OW=OH, Cout=Cout, k=3, stride=stride,
                   dil=dil, act="relu", res=r8, res_scale=0.02, out_scale=0.05, variant=v)
