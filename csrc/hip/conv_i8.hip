@@ -503,7 +503,7 @@ __global__ void gap_i8_reduce(const float* __restrict__ part, float* __restrict_
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// Streaming 1x1 / stride-1 variant for the memory-bound bottleneck convs (ResNet-50
+// Streaming 1x1 variant (any stride; 3x3 form below) for the memory-bound bottleneck convs (ResNet-50
 // layers 1-3 at 1025^2: K = 64..256, 2-27 MAC per byte moved). The register-fed kernel
 // above runs one short-lived 32x32..32x64 tile per wave with the weights reloaded from
 // L2 by every wave and a 4-byte-per-lane epilogue (r4_config4_roofline.txt: L1's 1x1 convs
@@ -566,8 +566,14 @@ __global__ __launch_bounds__(256) void conv_i8_1x1_kernel(I8Args a, int nblk) {
   auto load_x = [&](int tile, i32x4v (&dst)[KF]) {
     const int m = min(tile * 64 + wid * 16 + r, M - 1);  // clamped: tail pixels are not stored
     if constexpr (KT == 1) {
+      size_t pix = (size_t)m;
+      if (a.stride != 1) {  // strided 1x1 (the projection shortcuts): the sampled input pixel
+        const int b = m / (a.OH * a.OW), rem = m - b * a.OH * a.OW;
+        const int oy = rem / a.OW, ox = rem - oy * a.OW;
+        pix = ((size_t)b * a.IH + oy * a.stride) * a.IW + ox * a.stride;
+      }
 #pragma unroll
-      for (int f = 0; f < CF; ++f) dst[f] = ld16(a.in + (size_t)m * a.Cin + f * 64 + kq * 16);
+      for (int f = 0; f < CF; ++f) dst[f] = ld16(a.in + pix * a.Cin + f * 64 + kq * 16);
     } else {
       const int b = m / (a.OH * a.OW), rem = m - b * a.OH * a.OW;
       const int oy = rem / a.OW, ox = rem - oy * a.OW;
@@ -789,7 +795,8 @@ bool conv_i8_1x1_ok(const ConvI8Params& p) {
       if (CF == cn[0] && nsub % cn[1] == 0) inst = true;
   }
   const int vec = p.out_mode == 0 ? 16 : 8;  // 16-byte stores
-  const bool geom = k3 || (p.KH == 1 && p.KW == 1 && p.stride == 1 && p.IH == p.OH && p.IW == p.OW);
+  const bool geom = k3 || (p.KH == 1 && p.KW == 1 && p.OH == (p.IH - 1) / p.stride + 1 &&
+                           p.OW == (p.IW - 1) / p.stride + 1);
   return geom && p.Cin % 64 == 0 && p.Cout % 16 == 0 && (p.ldo % vec) == 0 && (p.co_off % vec) == 0 && inst;
 }
 

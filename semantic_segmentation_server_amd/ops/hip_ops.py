@@ -778,7 +778,7 @@ def conv_i8_1x1_ok(*, Cin, Cout, k=1, stride=1, ldo=None, co_off=0, int8_out=Tru
         table, geom = _I8_3X3_INST, True
     else:
         table = _I8_1X1_INST
-        geom = k == 1 and stride == 1 and (IH is None or IH == OH) and (IW is None or IW == OW)
+        geom = k == 1 and (IH is None or OH == (IH - 1) // stride + 1) and (IW is None or OW == (IW - 1) // stride + 1)
     return (geom and Cin % 64 == 0 and Cout % 16 == 0 and ldo % vec == 0 and co_off % vec == 0
             and any(Cin // 64 == cf and (Cout // 16) % ns == 0 for cf, ns in table))
 

@@ -1303,6 +1303,29 @@ def test_conv_i8_1x1_stream_exact(Cin, Cout, res, img, mode, M):
             assert d.max() <= 1 and (d > 0).float().mean() < 2e-3, (d.max(), (d > 0).float().mean())
 
 
+def test_conv_i8_1x1_stride2_stream():
+    """The streaming 1x1 variants on a strided projection shortcut (256 -> 512, stride 2)
+    against the register-fed one: within one rounding step."""
+    K = _hip()
+    g = torch.Generator().manual_seed(35)
+    B, H, Cin, Cout = 2, 17, 256, 512
+    OH = (H - 1) // 2 + 1
+    x8 = torch.randint(-127, 128, (B, H, H, Cin), generator=g, dtype=torch.int32).to(torch.int8).to(DEV)
+    w8 = torch.randint(-127, 128, (Cout, Cin), generator=g, dtype=torch.int32).to(torch.int8).to(DEV)
+    sc = (torch.rand(Cout, generator=g) * 1e-4).to(DEV)
+    bi = torch.randn(Cout, generator=g).to(DEV)
+    outs = []
+    for v in (1, 5, 6, 10, 11):
+        out = torch.zeros(B, OH, OH, Cout, dtype=torch.int8, device=DEV)
+        K.conv_i8(x8, w8, sc, bi, out, B=B, IH=H, IW=H, Cin=Cin, OH=OH, OW=OH, Cout=Cout, k=1, stride=2,
+                  act=None, out_scale=0.05, variant=v)
+        outs.append(out)
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        d = (outs[0].cpu().int() - o.cpu().int()).abs()
+        assert d.max() <= 1 and (d > 0).float().mean() < 2e-3, (d.max(), (d > 0).float().mean())
+
+
 @pytest.mark.parametrize("Cin,Cout,stride,dil,res", [(64, 64, 1, 1, False), (128, 128, 1, 1, True),
                                                     (128, 64, 2, 1, False), (64, 32, 1, 2, False),
                                                     (256, 256, 1, 2, False)])
