@@ -292,13 +292,12 @@ void launch_i8(const I8Args& a, hipStream_t s) {
 // ---------------------------------------------------------------------------
 // LDS-DMA pipelined int8 variant (the structure of conv_gemm.hip's glds kernel):
 // BM x BN tiles, operand rows of 128 K-bytes go global -> LDS with
-// global_load_lds_dwordx4 (XOR-swizzled on the source address, padded chunks
-// read a zero page), a 2-stage ring with one barrier per 128-deep K step, and
+// buffer_load_dwordx4 ... lds (XOR-swizzled on the source address, padded chunks
+// read as zeros through the descriptor's range check), a 2-stage ring with one barrier per 128-deep K step, and
 // the 16-byte fragments of v_mfma_i32_16x16x64_i8 read back from LDS. The
 // register-fed kernel above loads every fragment from global memory in each wave
 // (no reuse across a workgroup's waves); here a 128 x 128 tile's operands are
 // fetched once per workgroup.
-__device__ __attribute__((aligned(16))) int4 g_i8_zero[8];
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 template <int MT, int NT, int WM, int WN>
@@ -322,34 +321,42 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_i8_glds_kernel(I8Args a) {
   const int taps = a.KH * a.KW;
   const int grow = lane >> 3, lc = (lane & 7) ^ grow;
 
-  int ay[GA], ax[GA];
-  long long aoff[GA];
-  bool av[GA];
+  // Operand rows come in through buffer_load ... lds on range-checked descriptors (round 5):
+  // an out-of-image tap, a channel tail or a row past M gets an offset past the descriptor's
+  // end and the hardware writes zeros -- no zero page, no per-row branches or 64-bit
+  // address math in the loop. Each A row keeps its 32-bit pixel offset and a mask of the
+  // taps that land inside the image; the tap's (dy, dx) offset is one scalar add per step.
+  constexpr unsigned kOOB = 0x80000000u;
+  const auto rin = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(a.in), 0,
+                                                     (int)((long long)a.B * a.IH * a.IW * a.Cin), 0x00020000);
+  const auto rwt = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(a.w), 0,
+                                                     (int)((long long)a.Cout * taps * a.Cin), 0x00020000);
+  unsigned aoff[GA];
+  int nrtap[GA];  // taps that fall outside the image (or every tap for a row past M)
   int tapbits = 0;
 #pragma unroll
   for (int i = 0; i < GA; ++i) {
     const int m = m0 + wid * (BM / NW) + i * 8 + grow;
-    av[i] = m < M;
-    const int mm = av[i] ? m : 0;
+    const int mm = m < M ? m : 0;
     const int b = mm / (a.OH * a.OW);
     const int rem = mm - b * a.OH * a.OW;
-    ay[i] = (rem / a.OW) * a.stride;
-    ax[i] = (rem % a.OW) * a.stride;
-    aoff[i] = (((long long)b * a.IH + ay[i]) * a.IW + ax[i]) * a.Cin;
-    if (av[i])
+    const int ay = (rem / a.OW) * a.stride, ax = (rem % a.OW) * a.stride;
+    aoff[i] = (unsigned)((((b * a.IH + ay) * a.IW + ax) * a.Cin) + lc * 16);
+    int bits = 0;
+    if (m < M)
       for (int t = 0; t < taps; ++t) {
-        const int iy = ay[i] + (t / a.KW - a.KH / 2) * a.dil;
-        const int ix = ax[i] + (t % a.KW - a.KW / 2) * a.dil;
-        if (iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW) tapbits |= 1 << t;
+        const int iy = ay + (t / a.KW - a.KH / 2) * a.dil;
+        const int ix = ax + (t % a.KW - a.KW / 2) * a.dil;
+        if (iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW) bits |= 1 << t;
       }
+    nrtap[i] = ~bits;
+    tapbits |= bits;
   }
-  long long boff[GB];
-  bool bv[GB];
+  unsigned boff[GB];
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
     const int n = n0 + wid * (BN / NW) + j * 8 + grow;
-    bv[j] = n < a.Cout;
-    boff[j] = (long long)(bv[j] ? n : 0) * taps * a.Cin;
+    boff[j] = n < a.Cout ? (unsigned)(n * taps * a.Cin + lc * 16) : kOOB;
   }
   if (tid == 0) *s_tap = 0;
   __syncthreads();
@@ -362,28 +369,29 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_i8_glds_kernel(I8Args a) {
     if ((tapmask >> t) & 1) { tl |= (unsigned long long)t << (4 * ntap); ++ntap; }
   const int cch = cdiv_dev(a.Cin, 128);
   const int total = ntap * cch;
+  const int cin_left = a.Cin - lc * 16;  // this lane's 16-byte chunk exists while 128 * c < cin_left
 
   int is_tap = 0, is_c = 0;
   auto issue = [&](int stage) {
     const int t = (int)((tl >> (4 * is_tap)) & 15);
-    const int dy = (t / a.KW - a.KH / 2) * a.dil, dx = (t % a.KW - a.KW / 2) * a.dil;
-    const int c = is_c * 128 + lc * 16;
-    const bool cok = c < a.Cin;
-    const long long doff = ((long long)dy * a.IW + dx) * a.Cin + c;
+    const int ty = a.KW == 3 ? (t * 11) >> 5 : a.KW == 1 ? t : t / a.KW;
+    const int dy = (ty - a.KH / 2) * a.dil, dx = (t - ty * a.KW - a.KW / 2) * a.dil;
+    const int cb = is_c * 128;
+    // branch-free range handling: bit 31 set = past the descriptor's end (reads zeros)
+    const unsigned cbad = (unsigned)(cin_left - cb - 1) & kOOB;
+    const unsigned doff = (unsigned)((dy * a.IW + dx) * a.Cin + cb);
     char* sA = smem + stage * SB;
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
-      const int iy = ay[i] + dy, ix = ax[i] + dx;
-      const bool ok = av[i] && cok && iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW;
-      const void* src = ok ? (const void*)(a.in + aoff[i] + doff) : (const void*)g_i8_zero;
-      __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(sA + (wid * (BM / NW) + i * 8) * ROWB), 16, 0, 0);
+      const unsigned vo = (aoff[i] + doff) | cbad | (((unsigned)nrtap[i] << (31 - t)) & kOOB);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_ptr_t)(sA + (wid * (BM / NW) + i * 8) * ROWB), 16, vo, 0, 0, 0);
     }
     char* sB = sA + BM * ROWB;
-    const long long wofs = (long long)t * a.Cin + c;
+    const unsigned wofs = (unsigned)(t * a.Cin + cb);
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
-      const void* src = (bv[j] && cok) ? (const void*)(a.w + boff[j] + wofs) : (const void*)g_i8_zero;
-      __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(sB + (wid * (BN / NW) + j * 8) * ROWB), 16, 0, 0);
+      const unsigned vo = (boff[j] + wofs) | cbad;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rwt, (lds_ptr_t)(sB + (wid * (BN / NW) + j * 8) * ROWB), 16, vo, 0, 0, 0);
     }
     if (++is_c == cch) { is_c = 0; ++is_tap; }
   };
@@ -403,26 +411,30 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_i8_glds_kernel(I8Args a) {
     if (k + 1 < total) issue((k + 1) % ST);
     const char* sA = smem + (k % ST) * SB;
     const char* sB = sA + BM * ROWB;
+    // both K halves' fragments are requested up front: the second half's reads land
+    // under the first half's MFMAs
+    i32x4v bfr[2][MT], afr[2][NT];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int kc = ks * 4 + kq;
-      i32x4v bfr[MT], afr[NT];
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         const int r = wm * 16 * MT + i * 16 + r16;
-        bfr[i] = *reinterpret_cast<const i32x4v*>(sA + r * ROWB + ((kc ^ (r & 7)) << 4));
+        bfr[ks][i] = *reinterpret_cast<const i32x4v*>(sA + r * ROWB + ((kc ^ (r & 7)) << 4));
       }
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         const int n = wn * 16 * NT + j * 16 + r16;
-        afr[j] = *reinterpret_cast<const i32x4v*>(sB + n * ROWB + ((kc ^ (n & 7)) << 4));
+        afr[ks][j] = *reinterpret_cast<const i32x4v*>(sB + n * ROWB + ((kc ^ (n & 7)) << 4));
       }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[j], bfr[i], acc[i][j], 0, 0, 0);
-    }
+          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[ks][j], bfr[ks][i], acc[i][j], 0, 0, 0);
   }
 
   static_assert(NT == 4, "conv_i8_glds: the LDS epilogue stages 64-channel wave tiles");
@@ -811,10 +823,12 @@ void conv_i8(const ConvI8Params& p, hipStream_t s) {
   // 128 x 256 (8 waves), 4 LDS-DMA 256 x 128 (8 waves), 5 / 6 / 10 / 11 streaming 1x1 (stride 1,
   // Cin % 64 == 0, Cout % 16 == 0, 16-byte aligned output; the widest fitting channel block,
   // then the next narrower ones)
-  const bool glds_ok = p.KH * p.KW <= 16 && (long long)p.B * p.IH * p.IW * p.Cin < (1LL << 40);
+  // the LDS-DMA kernels address both operands through 32-bit buffer offsets below 2^31
+  const bool glds_ok = p.KH * p.KW <= 16 && (long long)p.B * p.IH * p.IW * p.Cin < (1LL << 31) &&
+                       (long long)p.Cout * p.KH * p.KW * p.Cin < (1LL << 31);
   int v = p.variant;
   if (v == 0) v = (glds_ok && p.Cout >= 64 && M >= 8192) ? (p.Cout >= 256 ? 3 : 2) : 1;
-  if (v >= 2 && v <= 4 && !glds_ok) throw std::invalid_argument("conv_i8: LDS-DMA variants need <= 16 taps");
+  if (v >= 2 && v <= 4 && !glds_ok) throw std::invalid_argument("conv_i8: LDS-DMA variants need <= 16 taps and < 2 GiB operands");
   if (v == 5 || v == 6 || v == 10 || v == 11) {
     if (!conv_i8_1x1_ok(p)) throw std::invalid_argument("conv_i8: streaming 1x1 variant does not fit this conv");
     const int which = v == 5 ? 0 : v == 6 ? 1 : v == 10 ? 2 : 3;

@@ -18,6 +18,7 @@
 #   profb1       sequential kernel trace of the B=1 step -> b1_layer_times.txt
 #   profc4       config-4 (ResNet-50 1025^2 int8, B=8) kernel trace -> c4_roofline.txt
 #   pmc          3 SQ counter passes over the sequential B=32 step -> pmc_summary.txt
+#   pmck         the same passes per kernel name + grid (model from BENCH_ARGS) -> kernel_pmc.txt
 #   race         concurrent-plan determinism check (scripts/debug_race.py)
 #   share8 / share:N  the dpN bench path with N ranks sharing this one GPU (SSA_SHARE_GPU=1, gloo;
 #                completes end to end -- its throughput is not a scaling number)
@@ -93,6 +94,14 @@ for step in "$@"; do
                  > $REPO/$O/pmc$i.log 2>&1) || { echo "pmc set $i failed"; tail -5 $O/pmc$i.log; exit 4; }
              done
              python3 scripts/pmc_summary.py $O/pmc1 $O/pmc2 $O/pmc3 > $O/pmc_summary.txt 2>&1; head -60 $O/pmc_summary.txt ;;
+    pmck)    i=0  # the same 3 passes, summarised per kernel name (pmc_kernels.py); model picked by BENCH_ARGS
+             for set in "${PMC_SETS[@]}"; do
+               i=$((i+1))
+               (cd /tmp && export TMPDIR=/tmp && SSA_SLOT_PARALLEL=0 timeout -s KILL 240 rocprofv3 --pmc $set \
+                 -d $REPO/$O/kpmc$i -o run --output-format csv -- python3 $REPO/bench.py --steps 3 --warmup 1 --lag 1 --rpc 0 $BENCH_ARGS \
+                 > $REPO/$O/kpmc$i.log 2>&1) || { echo "pmc set $i failed"; tail -5 $O/kpmc$i.log; exit 4; }
+             done
+             PMC_BY_GRID=1 python3 scripts/pmc_kernels.py $O/kpmc1 $O/kpmc2 $O/kpmc3 > $O/kernel_pmc.txt 2>&1; rm -rf $O/kpmc?; grep -c "^==" $O/kernel_pmc.txt ;;
     race)    timeout -k 10 600 python scripts/debug_race.py $RACE_ARGS > $O/race.txt 2>&1 || { tail -20 $O/race.txt; exit 5; }; tail -5 $O/race.txt ;;
     share8|share:*) n=${step#share}; n=${n#:}
              SSA_SHARE_GPU=1 timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \

@@ -4,7 +4,10 @@ counter set): python scripts/pmc_kernels.py DIR [DIR ...]. Used for standalone h
 import collections
 import csv
 import glob
+import os
 import sys
+
+BY_GRID = os.environ.get("PMC_BY_GRID") == "1"  # key by kernel name + grid size (one layer per key)
 
 
 def load(d):
@@ -12,9 +15,11 @@ def load(d):
     disp = {}
     for r in csv.DictReader(open(f)):
         k = int(r["Dispatch_Id"])
-        e = disp.setdefault(k, {"name": r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
-                                .replace("void ", "").replace("ssa::", ""),
-                                "t": (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3})
+        name = (r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
+                .replace("void ", "").replace("ssa::", ""))
+        if BY_GRID:
+            name += f" grid={r.get('Grid_Size', '?')} vgpr={r.get('VGPR_Count', '?')}/{r.get('Accum_VGPR_Count', '?')}"
+        e = disp.setdefault(k, {"name": name, "t": (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3})
         e[r["Counter_Name"]] = e.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     return list(disp.values())
 
