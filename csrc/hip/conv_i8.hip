@@ -820,7 +820,8 @@ void conv_i8(const ConvI8Params& p, hipStream_t s) {
            p.ldo, p.co_off, p.act};
   const long long M = (long long)p.B * p.OH * p.OW;
   // variant: 0 auto, 1 register-fed, 2 LDS-DMA 128 x 128 (4 waves), 3 LDS-DMA
-  // 128 x 256 (8 waves), 4 LDS-DMA 256 x 128 (8 waves), 5 / 6 / 10 / 11 streaming 1x1 (stride 1,
+  // 128 x 256 (8 waves), 4 LDS-DMA 256 x 128 (8 waves), 7 / 8 LDS-DMA 160 x 128 / 96 x 128
+  // (4 waves: tile counts that fill the 2-per-CU slots without a near-empty last round), 5 / 6 / 10 / 11 streaming 1x1 (stride 1,
   // Cin % 64 == 0, Cout % 16 == 0, 16-byte aligned output; the widest fitting channel block,
   // then the next narrower ones)
   // the LDS-DMA kernels address both operands through 32-bit buffer offsets below 2^31
@@ -828,7 +829,7 @@ void conv_i8(const ConvI8Params& p, hipStream_t s) {
                        (long long)p.Cout * p.KH * p.KW * p.Cin < (1LL << 31);
   int v = p.variant;
   if (v == 0) v = (glds_ok && p.Cout >= 64 && M >= 8192) ? (p.Cout >= 256 ? 3 : 2) : 1;
-  if (v >= 2 && v <= 4 && !glds_ok) throw std::invalid_argument("conv_i8: LDS-DMA variants need <= 16 taps and < 2 GiB operands");
+  if (((v >= 2 && v <= 4) || v == 7 || v == 8) && !glds_ok) throw std::invalid_argument("conv_i8: LDS-DMA variants need <= 16 taps and < 2 GiB operands");
   if (v == 5 || v == 6 || v == 10 || v == 11) {
     if (!conv_i8_1x1_ok(p)) throw std::invalid_argument("conv_i8: streaming 1x1 variant does not fit this conv");
     const int which = v == 5 ? 0 : v == 6 ? 1 : v == 10 ? 2 : 3;
@@ -840,6 +841,8 @@ void conv_i8(const ConvI8Params& p, hipStream_t s) {
     case 2: launch_i8_glds<4, 4, 2, 2>(a, s); return;
     case 3: launch_i8_glds<4, 4, 2, 4>(a, s); return;
     case 4: launch_i8_glds<4, 4, 4, 2>(a, s); return;
+    case 7: launch_i8_glds<5, 4, 2, 2>(a, s); return;
+    case 8: launch_i8_glds<3, 4, 2, 2>(a, s); return;
     default: break;
   }
   if (p.Cout <= 32) launch_i8<4, 1>(a, s);

@@ -26,7 +26,7 @@ from .deeplab import DeepLabV3, synthetic_normalized
 from .quant import calibrate, pack_int8
 
 
-_I8_VARIANTS = (1, 2, 3, 4)  # register-fed, LDS-DMA 128x128 / 128x256 / 256x128
+_I8_VARIANTS = (1, 2, 3, 4, 7, 8)  # register-fed, LDS-DMA 128x128 / 128x256 / 256x128 / 160x128 / 96x128
 # + 5 / 6: streaming 1x1 (weights resident per channel block, prefetched pixel tiles; 6 with
 # a narrower channel block) where it fits
 

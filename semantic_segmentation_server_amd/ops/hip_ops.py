@@ -787,10 +787,11 @@ def conv_i8(x, w8, scale, bias, out, *, B, IH, IW, Cin, OH, OW, Cout, k=1, strid
             ldo=None, co_off=0, act=None, res=None, res_scale=0.0, img_bias=None,
             out_scale=None, variant=0) -> torch.Tensor:
     """int8 NHWC conv. out int8 (out_scale given: v / out_scale rounded) or bf16.
-    variant: 0 auto, 1 register-fed, 2/3/4 LDS-DMA 128x128 / 128x256 / 256x128 tiles,
+    variant: 0 auto, 1 register-fed, 2/3/4/7/8 LDS-DMA 128x128 / 128x256 / 256x128 / 160x128 /
+    96x128 tiles,
     5 / 6 / 10 / 11 streaming 1x1 (stride 1; conv_i8_1x1_ok; the widest fitting channel block,
     then narrower ones)."""
-    if variant not in (0, 1, 2, 3, 4, 5, 6, 10, 11) or (2 <= variant <= 4 and k * k > 16):
+    if variant not in (0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 11) or (variant in (2, 3, 4, 7, 8) and k * k > 16):
         raise ValueError("conv_i8: bad variant")
     if variant in (5, 6, 10, 11) and not conv_i8_1x1_ok(Cin=Cin, Cout=Cout, k=k, stride=stride, ldo=ldo, co_off=co_off,
                                            int8_out=out_scale is not None):

@@ -1227,7 +1227,7 @@ def test_pw_conv_fp16_out():
     assert _rel(out.float().cpu(), ref) < 2e-3
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 7, 8])
 @pytest.mark.parametrize("Cin,Cout,k,stride,dil,res,mode", [
     (64, 256, 1, 1, 1, True, "i8"), (256, 64, 3, 2, 1, False, "i8"), (512, 512, 3, 1, 2, False, "i8"),
     (256, 19, 1, 1, 1, False, "bf16"), (1024, 256, 1, 1, 1, False, "i8"), (208, 136, 3, 1, 3, True, "i8")])
