@@ -308,9 +308,10 @@ PYBIND11_MODULE(_hip, m) {
         [](uintptr_t in, uintptr_t w, uintptr_t scale, uintptr_t bias, uintptr_t img_bias,
            uintptr_t res, float res_scale, uintptr_t out, float inv_out_scale, int out_mode, int B,
            int IH, int IW, int Cin, int OH, int OW, int Cout, int KH, int KW, int stride, int dil,
-           int ldo, int co_off, int act, uintptr_t stream, int variant) {
+           int ldo, int co_off, int act, uintptr_t stream, int variant, uintptr_t perm, int Mp) {
           ConvI8Params p;
           p.variant = variant;
+          p.perm = P<const int>(perm); p.Mp = Mp;
           p.in = P<const int8_t>(in); p.w = P<const int8_t>(w); p.scale = P<const float>(scale);
           p.bias = P<const float>(bias); p.img_bias = P<const float>(img_bias);
           p.res = P<const int8_t>(res); p.res_scale = res_scale; p.out = P<void>(out);
@@ -325,7 +326,30 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("out_mode"), py::arg("B"), py::arg("IH"), py::arg("IW"), py::arg("Cin"),
         py::arg("OH"), py::arg("OW"), py::arg("Cout"), py::arg("KH"), py::arg("KW"),
         py::arg("stride"), py::arg("dil"), py::arg("ldo"), py::arg("co_off"), py::arg("act"),
-        py::arg("stream"), py::arg("variant") = 0);
+        py::arg("stream"), py::arg("variant") = 0, py::arg("perm") = 0, py::arg("Mp") = 0);
+  m.def("conv_i8_grouped",
+        [](py::list groups, uintptr_t order, int nblocks, int variant, uintptr_t stream) {
+          // groups: tuples (in, w, scale, bias, img_bias, res, res_scale, out, inv_out_scale,
+          //                 out_mode, B, IH, IW, Cin, OH, OW, Cout, KH, KW, stride, dil, ldo,
+          //                 co_off, act, perm, Mp)
+          std::vector<ConvI8Params> ps;
+          for (auto item : groups) {
+            auto t = item.cast<py::tuple>();
+            if (t.size() != 26) throw std::invalid_argument("conv_i8_grouped: 26-tuple per conv");
+            auto I = [&](int i) { return t[i].cast<int>(); };
+            auto U = [&](int i) { return t[i].cast<uintptr_t>(); };
+            ConvI8Params p;
+            p.in = P<const int8_t>(U(0)); p.w = P<const int8_t>(U(1)); p.scale = P<const float>(U(2));
+            p.bias = P<const float>(U(3)); p.img_bias = P<const float>(U(4)); p.res = P<const int8_t>(U(5));
+            p.res_scale = t[6].cast<float>(); p.out = P<void>(U(7)); p.inv_out_scale = t[8].cast<float>();
+            p.out_mode = I(9); p.B = I(10); p.IH = I(11); p.IW = I(12); p.Cin = I(13); p.OH = I(14);
+            p.OW = I(15); p.Cout = I(16); p.KH = I(17); p.KW = I(18); p.stride = I(19); p.dil = I(20);
+            p.ldo = I(21); p.co_off = I(22); p.act = I(23); p.perm = P<const int>(U(24)); p.Mp = I(25);
+            ps.push_back(p);
+          }
+          conv_i8_grouped(ps.data(), (int)ps.size(), P<const int>(order), nblocks, variant, S(stream));
+        },
+        py::arg("groups"), py::arg("order"), py::arg("nblocks"), py::arg("variant"), py::arg("stream"));
   m.def("maxpool3x3s2_i8", [](uintptr_t in, uintptr_t out, int B, int IH, int IW, int C, int OH,
                               int OW, uintptr_t stream) {
     maxpool3x3s2_i8(P<const int8_t>(in), P<int8_t>(out), B, IH, IW, C, OH, OW, S(stream));

@@ -25,6 +25,10 @@ struct I8Args {
   const float* img_bias; const int8_t* res; float res_scale; void* out; float inv_out_scale;
   int out_mode;  // 0 int8, 1 bf16
   int B, IH, IW, Cin, OH, OW, Cout, KH, KW, stride, dil, ldo, co_off, act;
+  const int* perm;  // LDS-DMA kernels: GEMM row -> output pixel, -1 = padding (tap-class tiles)
+  int Mp;           // rows of perm
+  int nmajor;       // LDS-DMA tile order: 0 row-major (m-tile, n-tile), 1 n-tile major (the
+                    // dispatcher's consecutive blocks -> one XCD share one channel tile's weights)
 };
 
 __device__ __forceinline__ i32x4v ld16(const int8_t* p) { return *reinterpret_cast<const i32x4v*>(p); }
@@ -99,9 +103,10 @@ __device__ __forceinline__ void i8_epilogue_lds(const I8Args& a, const i32x4v (&
 #pragma unroll
     for (int c = 0; c < 4; ++c) v[c] = *reinterpret_cast<const i32x4v*>(ep + px * kEpPitch + cb + c * 4);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the next group rewrites ep
-    const int m = mbase + i * 16 + px;
+    int m = mbase + i * 16 + px;
     const int n = nbase + cb;
-    if (m >= M || n >= a.Cout) continue;
+    if (m >= (a.perm ? a.Mp : M) || n >= a.Cout) continue;
+    if (a.perm && (m = a.perm[m]) < 0) continue;
     const int b = m / (a.OH * a.OW);
     float f[16];
 #pragma unroll
@@ -300,23 +305,26 @@ void launch_i8(const I8Args& a, hipStream_t s) {
 // fetched once per workgroup.
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
+// One BM x BN output tile (index bid, row-major over (m-tile, n-tile)); shared by the
+// single-conv kernel and the grouped kernel (the int8 ASPP branches in one grid).
 template <int MT, int NT, int WM, int WN>
-__global__ __launch_bounds__(64 * WM * WN) void conv_i8_glds_kernel(I8Args a) {
+__device__ __forceinline__ void i8_glds_tile(const I8Args& a, const int bid, char* smem) {
   constexpr int NW = WM * WN, ST = 2;
   constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN, ROWB = 128;  // 128 int8 of K per row
   constexpr int GA = BM / (8 * NW), GB = BN / (8 * NW);
   static_assert(GA * 8 * NW == BM && GB * 8 * NW == BN, "tile rows must split over the waves");
   constexpr int SB = (BM + BN) * ROWB;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   int* s_tap = reinterpret_cast<int*>(smem + ST * SB);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
   const int r16 = lane & 15, kq = lane >> 4;
-  const int M = a.B * a.OH * a.OW;
-  const int tiles_m = cdiv_dev(M, BM), tiles_n = cdiv_dev(a.Cout, BN);
-  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tn = bid % tiles_n, tm = bid / tiles_n;
+  // GEMM rows: output pixels, or (perm) pixels grouped by tap validity into whole tiles, so
+  // the tile tap mask below skips every all-padding tap of the dilated ASPP branches
+  const int M = a.perm ? a.Mp : a.B * a.OH * a.OW;
+  const int tiles_n = cdiv_dev(a.Cout, BN), tiles_m = cdiv_dev(M, BM);
+  const int tn = a.nmajor ? bid / tiles_m : bid % tiles_n;
+  const int tm = a.nmajor ? bid - tn * tiles_m : bid / tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int taps = a.KH * a.KW;
   const int grow = lane >> 3, lc = (lane & 7) ^ grow;
@@ -337,13 +345,14 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_i8_glds_kernel(I8Args a) {
 #pragma unroll
   for (int i = 0; i < GA; ++i) {
     const int m = m0 + wid * (BM / NW) + i * 8 + grow;
-    const int mm = m < M ? m : 0;
+    const int pm = m < M ? (a.perm ? a.perm[m] : m) : -1;
+    const int mm = pm >= 0 ? pm : 0;
     const int b = mm / (a.OH * a.OW);
     const int rem = mm - b * a.OH * a.OW;
     const int ay = (rem / a.OW) * a.stride, ax = (rem % a.OW) * a.stride;
     aoff[i] = (unsigned)((((b * a.IH + ay) * a.IW + ax) * a.Cin) + lc * 16);
     int bits = 0;
-    if (m < M)
+    if (pm >= 0)
       for (int t = 0; t < taps; ++t) {
         const int iy = ay + (t / a.KW - a.KH / 2) * a.dil;
         const int ix = ax + (t % a.KW - a.KW / 2) * a.dil;
@@ -444,9 +453,52 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_i8_glds_kernel(I8Args a) {
 }
 
 template <int MT, int NT, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void conv_i8_glds_kernel(I8Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN;
+  const int M = a.perm ? a.Mp : a.B * a.OH * a.OW;
+  const int tiles = cdiv_dev(M, BM) * cdiv_dev(a.Cout, BN);
+  i8_glds_tile<MT, NT, WM, WN>(a, xcd_remap(blockIdx.x, tiles), smem);
+}
+
+constexpr int kMaxI8Group = 4;
+struct I8GroupArgs {
+  I8Args g[kMaxI8Group];
+  const int* order;
+};
+
+template <int MT, int NT, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void conv_i8_glds_group_kernel(I8GroupArgs ga) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int e = __builtin_amdgcn_readfirstlane(ga.order[blockIdx.x]);
+  const int t = e & 0xffffff;
+  switch (e >> 24) {  // constant indices: each arm reads its I8Args straight from kernarg
+    case 0: i8_glds_tile<MT, NT, WM, WN>(ga.g[0], t, smem); break;
+    case 1: i8_glds_tile<MT, NT, WM, WN>(ga.g[1], t, smem); break;
+    case 2: i8_glds_tile<MT, NT, WM, WN>(ga.g[2], t, smem); break;
+    default: i8_glds_tile<MT, NT, WM, WN>(ga.g[3], t, smem); break;
+  }
+}
+
+template <int MT, int NT, int WM, int WN>
+void launch_i8_glds_group(const I8GroupArgs& ga, int nblocks, hipStream_t s) {
+  constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN;
+  const size_t lds = 2 * (size_t)(BM + BN) * 128 + 16;
+  static bool attr = false;
+  if (!attr) {
+    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_i8_glds_group_kernel<MT, NT, WM, WN>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
+          "conv_i8_glds_group attr");
+    attr = true;
+  }
+  hipLaunchKernelGGL((conv_i8_glds_group_kernel<MT, NT, WM, WN>), dim3(nblocks), dim3(64 * WM * WN), lds, s, ga);
+  check_launch("conv_i8_glds_group");
+}
+
+template <int MT, int NT, int WM, int WN>
 void launch_i8_glds(const I8Args& a, hipStream_t s) {
   constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN;
-  const int M = a.B * a.OH * a.OW;
+  const int M = a.perm ? a.Mp : a.B * a.OH * a.OW;
   const int grid = cdiv(M, BM) * cdiv(a.Cout, BN);
   const size_t lds = 2 * (size_t)(BM + BN) * 128 + 16;
   static bool attr = false;
@@ -500,6 +552,52 @@ __global__ __launch_bounds__(256) void gap_i8_kernel(const int8_t* __restrict__ 
   int s = 0;
   for (int p = p0; p < p1; ++p) s += in[((long long)b * HW + p) * C + c];
   part[((long long)b * slices + sl) * C + c] = (float)s;
+}
+
+// Vectorised form (C % 16 == 0): a thread sums 16 channels of every PH-th pixel of the
+// slice from 16-byte loads (four in flight), the PH pixel phases of a workgroup meet in LDS.
+// The byte-per-thread kernel above issued one dependent 1-byte load per pixel: 67 us for the
+// config-4 ASPP pool (B = 8, 65 x 65 x 2048 int8, 69 MB) against ~14 us of HBM time.
+template <int CGN, int PH>
+__global__ __launch_bounds__(256) void gap_i8_vec_kernel(const int8_t* __restrict__ in, float* __restrict__ part,
+                                                         int HW, int C, int slices) {
+  static_assert(CGN * PH == 256, "one thread per (channel group, pixel phase)");
+  __shared__ __attribute__((aligned(16))) int red[PH * CGN * 16];
+  const int b = blockIdx.x, sl = blockIdx.y;
+  const int cg = threadIdx.x % CGN, ph = threadIdx.x / CGN;
+  const int cb = blockIdx.z * CGN * 16;
+  const int c0 = cb + cg * 16;
+  const int p0 = (int)((long long)HW * sl / slices), p1 = (int)((long long)HW * (sl + 1) / slices);
+  int acc[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0;
+  auto add = [&](const i32x4v v) {
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[w * 4 + k] += (v[w] << (24 - 8 * k)) >> 24;
+  };
+  if (c0 < C) {
+    const int8_t* src = in + (long long)b * HW * C + c0;
+    int p = p0 + ph;
+    for (; p + 3 * PH < p1; p += 4 * PH) {
+      const i32x4v v0 = ld16(src + (long long)p * C), v1 = ld16(src + (long long)(p + PH) * C);
+      const i32x4v v2 = ld16(src + (long long)(p + 2 * PH) * C), v3 = ld16(src + (long long)(p + 3 * PH) * C);
+      add(v0); add(v1); add(v2); add(v3);
+    }
+    for (; p < p1; p += PH) add(ld16(src + (long long)p * C));
+  }
+#pragma unroll
+  for (int q = 0; q < 16; q += 4)
+    *reinterpret_cast<i32x4v*>(red + (ph * CGN + cg) * 16 + q) = i32x4v{acc[q], acc[q + 1], acc[q + 2], acc[q + 3]};
+  __syncthreads();
+  for (int i = threadIdx.x; i < CGN * 16; i += 256) {
+    if (cb + i >= C) break;
+    int t = 0;
+#pragma unroll
+    for (int k = 0; k < PH; ++k) t += red[k * CGN * 16 + i];
+    part[((long long)b * slices + sl) * C + cb + i] = (float)t;
+  }
 }
 
 __global__ void gap_i8_reduce(const float* __restrict__ part, float* __restrict__ out, int B, int C,
@@ -812,24 +910,61 @@ bool conv_i8_1x1_ok(const ConvI8Params& p) {
   return geom && p.Cin % 64 == 0 && p.Cout % 16 == 0 && (p.ldo % vec) == 0 && (p.co_off % vec) == 0 && inst;
 }
 
-void conv_i8(const ConvI8Params& p, hipStream_t s) {
+static I8Args i8_args(const ConvI8Params& p) {
   if (p.Cin % 16) throw std::invalid_argument("conv_i8: Cin must be a multiple of 16");
   if (p.ldo < p.co_off + p.Cout) throw std::invalid_argument("conv_i8: bad ldo/co_off");
-  I8Args a{p.in, p.w, p.scale, p.bias, p.img_bias, p.res, p.res_scale, p.out, p.inv_out_scale,
-           p.out_mode, p.B, p.IH, p.IW, p.Cin, p.OH, p.OW, p.Cout, p.KH, p.KW, p.stride, p.dil,
-           p.ldo, p.co_off, p.act};
+  if (p.perm && p.Mp <= 0) throw std::invalid_argument("conv_i8: perm needs Mp > 0");
+  return I8Args{p.in, p.w, p.scale, p.bias, p.img_bias, p.res, p.res_scale, p.out, p.inv_out_scale,
+                p.out_mode, p.B, p.IH, p.IW, p.Cin, p.OH, p.OW, p.Cout, p.KH, p.KW, p.stride, p.dil,
+                p.ldo, p.co_off, p.act, p.perm, p.perm ? p.Mp : 0, 0};
+}
+
+// the LDS-DMA kernels address both operands through 32-bit buffer offsets below 2^31
+static bool i8_glds_ok(const ConvI8Params& p) {
+  return p.KH * p.KW <= 16 && (long long)p.B * p.IH * p.IW * p.Cin < (1LL << 31) &&
+         (long long)p.Cout * p.KH * p.KW * p.Cin < (1LL << 31);
+}
+
+void conv_i8_grouped(const ConvI8Params* ps, int n, const int* order, int nblocks, int variant,
+                     hipStream_t s) {
+  if (n < 1 || n > kMaxI8Group) throw std::invalid_argument("conv_i8_grouped: 1..4 convs");
+  if (!order || nblocks <= 0) throw std::invalid_argument("conv_i8_grouped: empty order table");
+  I8GroupArgs ga{};
+  for (int i = 0; i < n; ++i) {
+    if (!i8_glds_ok(ps[i])) throw std::invalid_argument("conv_i8_grouped: conv does not fit the LDS-DMA kernel");
+    ga.g[i] = i8_args(ps[i]);
+  }
+  for (int i = n; i < kMaxI8Group; ++i) ga.g[i] = ga.g[0];
+  ga.order = order;
+  switch (variant) {
+    case 2: launch_i8_glds_group<4, 4, 2, 2>(ga, nblocks, s); return;
+    case 3: launch_i8_glds_group<4, 4, 2, 4>(ga, nblocks, s); return;
+    case 4: launch_i8_glds_group<4, 4, 4, 2>(ga, nblocks, s); return;
+    case 7: launch_i8_glds_group<5, 4, 2, 2>(ga, nblocks, s); return;
+    case 8: launch_i8_glds_group<3, 4, 2, 2>(ga, nblocks, s); return;
+    default: throw std::invalid_argument("conv_i8_grouped: variant must be 2, 3, 4, 7 or 8");
+  }
+}
+
+void conv_i8(const ConvI8Params& p, hipStream_t s) {
+  I8Args a = i8_args(p);
   const long long M = (long long)p.B * p.OH * p.OW;
   // variant: 0 auto, 1 register-fed, 2 LDS-DMA 128 x 128 (4 waves), 3 LDS-DMA
   // 128 x 256 (8 waves), 4 LDS-DMA 256 x 128 (8 waves), 7 / 8 LDS-DMA 160 x 128 / 96 x 128
-  // (4 waves: tile counts that fill the 2-per-CU slots without a near-empty last round), 5 / 6 / 10 / 11 streaming 1x1 (stride 1,
+  // (4 waves: tile counts that fill the 2-per-CU slots without a near-empty last round), 12 / 13
+  // = 7 / 2 with n-tile-major block order, 5 / 6 / 10 / 11 streaming 1x1 (stride 1,
   // Cin % 64 == 0, Cout % 16 == 0, 16-byte aligned output; the widest fitting channel block,
   // then the next narrower ones)
-  // the LDS-DMA kernels address both operands through 32-bit buffer offsets below 2^31
-  const bool glds_ok = p.KH * p.KW <= 16 && (long long)p.B * p.IH * p.IW * p.Cin < (1LL << 31) &&
-                       (long long)p.Cout * p.KH * p.KW * p.Cin < (1LL << 31);
+  const bool glds_ok = i8_glds_ok(p);
   int v = p.variant;
+  if (v == 12 || v == 13) {  // n-tile-major forms of 7 / 2 (weight-heavy convs: the ASPP 3x3s)
+    a.nmajor = 1;
+    v = v == 12 ? 7 : 2;
+  }
   if (v == 0) v = (glds_ok && p.Cout >= 64 && M >= 8192) ? (p.Cout >= 256 ? 3 : 2) : 1;
-  if (((v >= 2 && v <= 4) || v == 7 || v == 8) && !glds_ok) throw std::invalid_argument("conv_i8: LDS-DMA variants need <= 16 taps and < 2 GiB operands");
+  const bool glds_v = (v >= 2 && v <= 4) || v == 7 || v == 8;
+  if (glds_v && !glds_ok) throw std::invalid_argument("conv_i8: LDS-DMA variants need <= 16 taps and < 2 GiB operands");
+  if (p.perm && !glds_v) throw std::invalid_argument("conv_i8: a row permutation needs an LDS-DMA variant");
   if (v == 5 || v == 6 || v == 10 || v == 11) {
     if (!conv_i8_1x1_ok(p)) throw std::invalid_argument("conv_i8: streaming 1x1 variant does not fit this conv");
     const int which = v == 5 ? 0 : v == 6 ? 1 : v == 10 ? 2 : 3;
@@ -861,9 +996,13 @@ void maxpool3x3s2_i8(const int8_t* in, int8_t* out, int B, int IH, int IW, int C
 
 void global_avgpool_i8(const int8_t* in, float* out, float* ws, int B, int HW, int C, float scale,
                        hipStream_t s) {
-  const int slices = 16;
-  hipLaunchKernelGGL(gap_i8_kernel, dim3(B, slices, cdiv(C, 256)), dim3(256), 0, s, in, ws, HW, C,
-                     slices);
+  const int slices = 16;  // the caller's ws holds B * 16 * C partial sums
+  if (C % 16 == 0)
+    hipLaunchKernelGGL((gap_i8_vec_kernel<32, 8>), dim3(B, slices, cdiv(C, 512)), dim3(256), 0, s, in, ws, HW,
+                       C, slices);
+  else
+    hipLaunchKernelGGL(gap_i8_kernel, dim3(B, slices, cdiv(C, 256)), dim3(256), 0, s, in, ws, HW, C,
+                       slices);
   hipLaunchKernelGGL(gap_i8_reduce, dim3(cdiv((long long)B * C, 256)), dim3(256), 0, s, ws, out, B,
                      C, slices, scale / (float)HW);
   check_launch("gap_i8");

@@ -82,9 +82,16 @@ struct ConvI8Params {
   int out_mode = 0;
   int B = 0, IH = 0, IW = 0, Cin = 0, OH = 0, OW = 0, Cout = 0;
   int KH = 1, KW = 1, stride = 1, dil = 1, ldo = 0, co_off = 0, act = 0;
-  int variant = 0;  // 0 auto, 1 register-fed, 2/3/4 LDS-DMA 128x128 / 128x256 / 256x128
+  int variant = 0;  // 0 auto, 1 register-fed, 2/3/4/7/8 LDS-DMA 128x128 / 128x256 / 256x128 / 160x128 / 96x128
+  const int* perm = nullptr;  // LDS-DMA variants: GEMM row -> output pixel (-1 = padding row), Mp rows
+  int Mp = 0;
 };
 void conv_i8(const ConvI8Params& p, hipStream_t s);
+// Up to 4 independent int8 convs (the ASPP branches: one input, disjoint channel slices of
+// the concat buffer) in ONE LDS-DMA grid: block i runs tile order[i] = (group << 24) | tile
+// (host-sorted by live-tap work, heaviest first). variant: 2/3/4/7/8 (the tile shape).
+void conv_i8_grouped(const ConvI8Params* ps, int n, const int* order, int nblocks, int variant,
+                     hipStream_t s);
 void maxpool3x3s2_i8(const int8_t* in, int8_t* out, int B, int IH, int IW, int C, int OH, int OW,
                      hipStream_t s);
 // int8 GAP -> fp32 mean * scale; ws: B * 16 * C floats

@@ -27,6 +27,7 @@ from .quant import calibrate, pack_int8
 
 
 _I8_VARIANTS = (1, 2, 3, 4, 7, 8)  # register-fed, LDS-DMA 128x128 / 128x256 / 256x128 / 160x128 / 96x128
+# (12 / 13, the n-tile-major orders, timed within noise of 7 / 2 or slower: not offered)
 # + 5 / 6: streaming 1x1 (weights resident per channel block, prefetched pixel tiles; 6 with
 # a narrower channel block) where it fits
 
@@ -146,14 +147,7 @@ class HipDeepLabInt8:
         A = self.A
         cat = buf("aspp_cat", B, h, w, self.cat_c)
         s_cat = S["aspp.cat"]
-        w8, sc, bi = self.aspp_b0
-        ops.append(I8(
-            x, w8, sc, bi, cat, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w, Cout=A, ldo=self.cat_c,
-            co_off=0, act="relu", out_scale=s_cat))
-        for j, ((aw, asc, ab), rate) in enumerate(self.aspp_atrous):
-            ops.append(I8(
-                x, aw, asc, ab, cat, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w, Cout=A, k=3, dil=rate,
-                ldo=self.cat_c, co_off=(j + 1) * A, act="relu", out_scale=s_cat))
+        ops.append(self._aspp_branches(bufs, x, cat, B, h, w, c))
         gap = buf("gap", B, c, dtype=torch.float32)
         gws = buf("gap_ws", B * 16 * c, dtype=torch.float32)
         pooled = buf("pooled", B, A, dtype=torch.float32)
@@ -191,6 +185,52 @@ class HipDeepLabInt8:
                 op(*args)
             torch.cuda.synchronize(dev)
         return self._plans[key]
+
+    def _aspp_branches(self, bufs, x, cat, B, h, w, c):
+        """The ASPP 1x1 + atrous branches into the int8 concat buffer, as a Choice between
+        four separate LDS-DMA launches (160x128 tiles, raster rows) and ONE grouped launch per
+        tile shape: the atrous rows permuted into tap-uniform tiles (``tap_group_perm``: at
+        65 x 65 the rate-6/12/18 tiles skip every padding tap, 23 / 43 / 60 % of the raster
+        work) and every branch's tiles in one heaviest-first order, so the light tiles fill
+        the tail instead of each branch's grid idling on its own."""
+        from .hip_model import Choice
+        A, S = self.A, self.scales
+        s_cat = S["aspp.cat"]
+        w8, sc, bi = self.aspp_b0
+        convs = [dict(x=x, w=w8, scale=sc, bias=bi, out=cat, B=B, IH=h, IW=w, Cin=c, OH=h, OW=w,
+                      Cout=A, ldo=self.cat_c, co_off=0, act="relu", out_scale=s_cat)]
+        for j, ((aw, asc, ab), rate) in enumerate(self.aspp_atrous):
+            convs.append(dict(x=x, w=aw, scale=asc, bias=ab, out=cat, B=B, IH=h, IW=w, Cin=c, OH=h,
+                              OW=w, Cout=A, k=3, dil=rate, ldo=self.cat_c, co_off=(j + 1) * A,
+                              act="relu", out_scale=s_cat))
+
+        def sep(cv, v):
+            kw = {k: x for k, x in cv.items() if k not in ("x", "w", "scale", "bias", "out")}
+            return lambda *_: K.conv_i8(cv["x"], cv["w"], cv["scale"], cv["bias"], cv["out"], variant=v, **kw)
+
+        # separate launches (raster 160x128 tiles) or one grouped launch. Measured (r7d-r7g,
+        # B = 8, 65 x 65): sep 481-487 us, grouped 476-551 us over the tile shapes and orders
+        # (global LPT, branch-affine XCD sets per branch / per channel tile), n-tile-major
+        # separate 524 us: the tap-uniform tiles cut the K steps but not the time, so the
+        # grouped form stays an autotune candidate, not the default
+        variants = [("sep", [sep(cv, 7) for cv in convs])]
+        for v in (7,):
+            BM = K.I8_TILE[v][0]
+            gc = []
+            for j, cv in enumerate(convs):
+                cv = dict(cv)
+                if cv.get("k", 1) > 1:
+                    cv["perm"] = K.tap_group_perm(B, h, w, 3, cv["dil"], BM, device=self.device)
+                    bufs[f"aspp_perm{j}_v{v}"] = cv["perm"]
+                gc.append(cv)
+            # branch-affine XCD sets, per branch / per branch channel tile
+            for xcds, by_n, tag in ((8, False, "x"),):
+                order = K.grouped_tile_order_i8(gc, v, device=self.device, xcds=xcds, by_n=by_n)
+                bufs[f"aspp_order_v{v}{tag}"] = order
+                variants.append((f"g{v}{tag}", [lambda *_, gc=gc, order=order, v=v: K.conv_i8_grouped(gc, order, v)]))
+        ch = Choice("aspp_i8", variants)
+        ch.desc = f"M={B * h * w} Cin={c} Cout={A} x {len(convs)} branches"
+        return ch
 
     def _autotune(self, ops, B, Hc, Wc) -> None:
         """Time each int8 conv's kernel variants on the plan's real buffers, keep the fastest.

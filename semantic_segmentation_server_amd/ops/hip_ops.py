@@ -219,10 +219,15 @@ def grouped_tile_order_branch(convs: List[dict], variant: int, device=None, xcds
             for n in range(tn):
                 tiles.append((int(taps[tm]) * kch, (g << 24) | (tm * tn + n), g))
     G = len(convs)
+    return _branch_affine(tiles, [g for g in range(G) if convs[g]["k"] > 1] or list(range(G)), xcds, device)
+
+
+def _branch_affine(tiles, heavy, xcds, device):
+    """XCD assignment of ``grouped_tile_order_branch``. tiles: (cost, entry, key); each key in
+    ``heavy`` (a weight slab: a 3x3 conv, or one of its channel tiles) gets an XCD set."""
     # the dispatcher hands block i to XCD i % xcds whatever its load, so every XCD runs the
     # same NUMBER of blocks: the 3x3 branches get XCD sets in proportion to their work, and
     # the light 1x1 tiles (164 KB of weights) fill every XCD's remaining block count
-    heavy = [g for g in range(G) if convs[g]["k"] > 1] or list(range(G))
     gcost = {g: sum(t[0] for t in tiles if t[2] == g) for g in heavy}
     tot = max(1, sum(gcost.values()))
     share = {g: xcds * gcost[g] / tot for g in heavy}
@@ -785,14 +790,21 @@ def conv_i8_1x1_ok(*, Cin, Cout, k=1, stride=1, ldo=None, co_off=0, int8_out=Tru
 
 def conv_i8(x, w8, scale, bias, out, *, B, IH, IW, Cin, OH, OW, Cout, k=1, stride=1, dil=1,
             ldo=None, co_off=0, act=None, res=None, res_scale=0.0, img_bias=None,
-            out_scale=None, variant=0) -> torch.Tensor:
+            out_scale=None, variant=0, perm=None) -> torch.Tensor:
     """int8 NHWC conv. out int8 (out_scale given: v / out_scale rounded) or bf16.
     variant: 0 auto, 1 register-fed, 2/3/4/7/8 LDS-DMA 128x128 / 128x256 / 256x128 / 160x128 /
-    96x128 tiles,
+    96x128 tiles, 12 / 13 = 7 / 2 in n-tile-major block order,
     5 / 6 / 10 / 11 streaming 1x1 (stride 1; conv_i8_1x1_ok; the widest fitting channel block,
-    then narrower ones)."""
-    if variant not in (0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 11) or (variant in (2, 3, 4, 7, 8) and k * k > 16):
+    then narrower ones).
+    ``perm`` (LDS-DMA variants only; ``tap_group_perm`` with the variant's tile height): GEMM
+    rows -> output pixels, tiles of equal tap validity."""
+    if variant not in (0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 13) or (variant in (2, 3, 4, 7, 8, 12, 13) and k * k > 16):
         raise ValueError("conv_i8: bad variant")
+    Mp = 0
+    if perm is not None:
+        if variant not in I8_TILE:
+            raise ValueError("conv_i8: a row permutation needs an LDS-DMA variant")
+        Mp = _check_perm(perm, I8_TILE[variant][0], B * OH * OW, "conv_i8")
     if variant in (5, 6, 10, 11) and not conv_i8_1x1_ok(Cin=Cin, Cout=Cout, k=k, stride=stride, ldo=ldo, co_off=co_off,
                                            int8_out=out_scale is not None):
         raise ValueError("conv_i8: the streaming 1x1 variant does not fit this conv")
@@ -814,9 +826,103 @@ def conv_i8(x, w8, scale, bias, out, *, B, IH, IW, Cin, OH, OW, Cout, k=1, strid
     _hip_mod().conv_i8(_ptr(x), _ptr(w8), _ptr(scale), _ptr(bias), _ptr(img_bias), _ptr(res),
                        float(res_scale), _ptr(out), 1.0 / out_scale if mode == 0 else 1.0, mode, B,
                        IH, IW, Cin, OH, OW, Cout, k, k, stride, dil, ldo, co_off, ACT[act], _stream(),
-                       variant)
+                       variant, _ptr(perm), Mp)
     _dbg('conv_i8')
     return out
+
+
+# int8 LDS-DMA tile shapes (BM, BN) by conv_i8 variant
+I8_TILE = {2: (128, 128), 3: (128, 256), 4: (256, 128), 7: (160, 128), 8: (96, 128),
+           12: (160, 128), 13: (128, 128)}  # 12 / 13: 7 / 2 with n-tile-major block order
+
+
+def _check_perm(perm, BM, M, who):
+    _chk(perm, torch.int32, "perm")
+    Mp = perm.numel()
+    if Mp % BM:
+        raise ValueError(f"{who}: perm rows must be a multiple of the tile height {BM}")
+    if not getattr(perm, "_ssa_checked", False):
+        pc = perm.cpu()
+        if pc.min().item() < -1 or pc.max().item() >= M:
+            raise ValueError(f"{who}: perm entry out of range")
+        perm._ssa_checked = True
+    return Mp
+
+
+def grouped_tile_order_i8(convs: List[dict], variant: int, device=None, xcds: int = 1,
+                          by_n: bool = False) -> torch.Tensor:
+    """Block -> tile table of ``conv_i8_grouped``: every tile of every conv as
+    (group << 24) | tile, heaviest first (work = live taps x 128-channel K chunks): the
+    longest-processing-time order of ``grouped_tile_order``, so the light 1x1 and
+    border-class tiles fill the tail of the 2-per-CU slots. ``xcds`` > 1: the branch-affine
+    XCD assignment of ``grouped_tile_order_branch`` (each XCD's L2 holds one branch's
+    weights), LPT inside every XCD."""
+    BM, BN = I8_TILE[variant]
+    ent, cost, key = [], [], []
+    for g, c in enumerate(convs):
+        tn = -(-c["Cout"] // BN)
+        taps = _tile_taps(c["B"], c["OH"], c["OW"], c.get("k", 1), c.get("dil", 1), BM, c.get("perm"))
+        kch = -(-c["Cin"] // 128)
+        for tm in range(taps.numel()):
+            for n in range(tn):
+                ent.append((g << 24) | (tm * tn + n))
+                cost.append(int(taps[tm]) * kch)
+                key.append((g, n) if by_n else g)
+    if xcds > 1:  # branch-affine XCD sets: a 3x3 branch's 4.7 MB of int8 weights (or, by_n, one
+        # BN-channel slice of them, 2.4 MB: fits the 4 MiB L2 next to the streamed rows)
+        heavy = [k for k in dict.fromkeys(key) if convs[k[0] if by_n else k].get("k", 1) > 1] or list(dict.fromkeys(key))
+        return _branch_affine(list(zip(cost, ent, key)), heavy, xcds, device)
+    idx = sorted(range(len(ent)), key=lambda i: (-cost[i], i))
+    return torch.tensor([ent[i] for i in idx], dtype=torch.int32).to(device).contiguous()
+
+
+def conv_i8_grouped(convs: List[dict], order: torch.Tensor, variant: int = 7) -> None:
+    """Up to 4 independent int8 convs in ONE LDS-DMA grid (the ASPP 1x1 + atrous branches:
+    one input, disjoint channel slices of the concat buffer), tiles in the
+    ``grouped_tile_order_i8`` table. Each conv is a dict of ``conv_i8``'s arguments (x, w,
+    scale, bias, out, B, IH, IW, Cin, OH, OW, Cout, k, stride, dil, ldo, co_off, act, res,
+    res_scale, img_bias, out_scale, perm)."""
+    if not 1 <= len(convs) <= 4:
+        raise ValueError("conv_i8_grouped: 1..4 convs")
+    if variant not in (2, 3, 4, 7, 8):
+        raise ValueError("conv_i8_grouped: variant must be one of 2, 3, 4, 7, 8")
+    BM, BN = I8_TILE[variant]
+    tiles, groups = [], []
+    for c in convs:
+        B, IH, IW, Cin, OH, OW, Cout = (c[n] for n in ("B", "IH", "IW", "Cin", "OH", "OW", "Cout"))
+        k, stride, dil = c.get("k", 1), c.get("stride", 1), c.get("dil", 1)
+        ldo, co_off = c.get("ldo", Cout), c.get("co_off", 0)
+        if Cin % 16 or k * k > 16 or co_off + Cout > ldo:
+            raise ValueError("conv_i8_grouped: Cin % 16 == 0, <= 16 taps, co_off + Cout <= ldo")
+        out_scale = c.get("out_scale")
+        mode = 0 if out_scale is not None else 1
+        _chk(c["x"], torch.int8, "x", B * IH * IW * Cin)
+        _chk(c["w"], torch.int8, "w", Cout * k * k * Cin)
+        _chk(c["scale"], torch.float32, "scale", Cout)
+        _chk(c["bias"], torch.float32, "bias", Cout)
+        _chk(c["out"], torch.int8 if mode == 0 else torch.bfloat16, "out", B * OH * OW * ldo)
+        res, img_bias, perm = c.get("res"), c.get("img_bias"), c.get("perm")
+        if res is not None:
+            _chk(res, torch.int8, "res", B * OH * OW * Cout)
+        if img_bias is not None:
+            _chk(img_bias, torch.float32, "img_bias", B * Cout)
+        Mp = _check_perm(perm, BM, B * OH * OW, "conv_i8_grouped") if perm is not None else 0
+        tiles.append(-(-(Mp or B * OH * OW) // BM) * -(-Cout // BN))
+        groups.append((_ptr(c["x"]), _ptr(c["w"]), _ptr(c["scale"]), _ptr(c["bias"]), _ptr(img_bias),
+                       _ptr(res), float(c.get("res_scale", 0.0)), _ptr(c["out"]),
+                       1.0 / out_scale if mode == 0 else 1.0, mode, B, IH, IW, Cin, OH, OW, Cout, k, k,
+                       stride, dil, ldo, co_off, ACT[c.get("act")], _ptr(perm), Mp))
+    _chk(order, torch.int32, "order")
+    if not getattr(order, "_ssa_checked", False):  # every block maps to a real tile, once
+        oc = order.cpu().long()
+        g, t = oc >> 24, oc & 0xFFFFFF
+        if (g < 0).any() or (g >= len(convs)).any():
+            raise ValueError("conv_i8_grouped: order entry out of range")
+        if (t >= torch.tensor(tiles)[g]).any() or oc.numel() != sum(tiles) or oc.unique().numel() != oc.numel():
+            raise ValueError("conv_i8_grouped: the order table must list every tile once")
+        order._ssa_checked = True
+    _hip_mod().conv_i8_grouped(groups, _ptr(order), order.numel(), variant, _stream())
+    _dbg('conv_i8_grouped')
 
 
 def maxpool3x3s2_i8(x, out, *, B, IH, IW, C, OH, OW):

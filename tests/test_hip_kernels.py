@@ -375,6 +375,21 @@ def test_maxpool_gap_matvec():
     assert torch.allclose(mv.cpu(), F.relu(gref @ wm.t() + bm), atol=1e-3)
 
 
+@pytest.mark.parametrize("B,HW,C", [(8, 65 * 65, 2048), (3, 37, 528), (2, 50, 40)])
+def test_global_avgpool_i8(B, HW, C):
+    """int8 NHWC global average pool (16-byte vector kernel for C % 16 == 0, byte kernel
+    otherwise) against the fp32 mean of the same bytes times the scale."""
+    K = _hip()
+    g = torch.Generator().manual_seed(C)
+    x = torch.randint(-127, 128, (B, HW, C), generator=g, dtype=torch.int32).to(torch.int8)
+    out = torch.empty(B, C, device=DEV)
+    ws = torch.empty(B * 16 * C, device=DEV)
+    K.global_avgpool_i8(x.to(DEV), out, ws, B=B, HW=HW, C=C, scale=0.03)
+    torch.cuda.synchronize()
+    ref = x.double().mean(1) * 0.03
+    assert torch.allclose(out.cpu().double(), ref, rtol=1e-5, atol=1e-6)
+
+
 @pytest.mark.parametrize("rows,aw", [(32, 41), (1, 41), (7, 3)])
 def test_pack_rows_and_copy_to_host(rows, aw):
     """The RCCL-gather send row [record | metadata] packed from a device tensor and a
@@ -1227,7 +1242,7 @@ def test_pw_conv_fp16_out():
     assert _rel(out.float().cpu(), ref) < 2e-3
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 7, 8])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 7, 8, 12, 13])
 @pytest.mark.parametrize("Cin,Cout,k,stride,dil,res,mode", [
     (64, 256, 1, 1, 1, True, "i8"), (256, 64, 3, 2, 1, False, "i8"), (512, 512, 3, 1, 2, False, "i8"),
     (256, 19, 1, 1, 1, False, "bf16"), (1024, 256, 1, 1, 1, False, "i8"), (208, 136, 3, 1, 3, True, "i8")])
@@ -1265,6 +1280,48 @@ def test_conv_i8(Cin, Cout, k, stride, dil, res, mode, variant):
                   Cout=Cout, k=k, stride=stride, dil=dil, act="relu", variant=variant)
         torch.cuda.synchronize()
         assert _rel(_nchw(out).cpu(), ref) < 5e-3
+
+
+@pytest.mark.parametrize("variant", [7, 2, 8])
+def test_conv_i8_grouped_aspp(variant):
+    """The int8 ASPP branches (1x1 + three atrous 3x3, one input, channel slices of one concat
+    buffer) in ONE grouped LDS-DMA launch with tap-class row permutations and the LPT tile
+    order: byte-identical to the four separate raster-order launches (same exact int32 sums,
+    same epilogue), and the separate launch of a permuted branch matches too."""
+    K = _hip()
+    g = torch.Generator().manual_seed(variant)
+    B, H, Cin, A = 2, 19, 256, 64
+    BM = K.I8_TILE[variant][0]
+    x = torch.randint(-127, 128, (B, H, H, Cin), generator=g, dtype=torch.int32).to(torch.int8).to(DEV)
+    convs = []
+    for j, (k, d) in enumerate([(1, 1), (3, 2), (3, 5), (3, 7)]):
+        w = torch.randint(-127, 128, (A, k, k, Cin), generator=g, dtype=torch.int32).to(torch.int8).to(DEV)
+        convs.append(dict(x=x, w=w, scale=(torch.rand(A, generator=g) * 1e-4).to(DEV),
+                          bias=torch.randn(A, generator=g).to(DEV), B=B, IH=H, IW=H, Cin=Cin, OH=H,
+                          OW=H, Cout=A, k=k, dil=d, ldo=4 * A, co_off=j * A, act="relu", out_scale=0.05))
+    ref = torch.zeros(B, H, H, 4 * A, dtype=torch.int8, device=DEV)
+    for cv in convs:
+        kw = {k: v for k, v in cv.items() if k not in ("x", "w", "scale", "bias")}
+        K.conv_i8(cv["x"], cv["w"], cv["scale"], cv["bias"], ref, variant=variant, **kw)
+    gc = []
+    for cv in convs:
+        cv = dict(cv, out=torch.full((B, H, H, 4 * A), 99, dtype=torch.int8, device=DEV))
+        if cv["k"] > 1:
+            cv["perm"] = K.tap_group_perm(B, H, H, 3, cv["dil"], BM, device=DEV)
+        gc.append(cv)
+    out = torch.full((B, H, H, 4 * A), 99, dtype=torch.int8, device=DEV)
+    for cv in gc:
+        cv["out"] = out
+    order = K.grouped_tile_order_i8(gc, variant, device=DEV)
+    K.conv_i8_grouped(gc, order, variant)
+    one = torch.full_like(out, 99)
+    cv = gc[3]
+    kw = {k: v for k, v in cv.items() if k not in ("x", "w", "scale", "bias", "out")}
+    K.conv_i8(cv["x"], cv["w"], cv["scale"], cv["bias"], one, variant=variant, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), ref.cpu())
+    assert torch.equal(one[..., 3 * A:].cpu(), ref[..., 3 * A:].cpu())
+    assert (one[..., :3 * A] == 99).all()  # the permuted launch wrote only its own slice
 
 
 @pytest.mark.parametrize("Cin,Cout,res,img,mode,M", [

@@ -52,3 +52,46 @@ def test_grouped_tile_order_branch_affine_cpu():
     assert {c.most_common(1)[0][0] for c in seen.values()} == {1, 2, 3}
     counts = [len(b[x::8]) for x in range(8)]  # equal block counts per XCD
     assert max(counts) - min(counts) <= 1
+
+
+def test_grouped_tile_order_i8_cpu():
+    """int8 grouped ASPP order: every tile of every branch exactly once, heaviest (most live
+    taps x K chunks) first; the tap-class permutation leaves whole tiles with fewer taps."""
+    import torch
+    from semantic_segmentation_server_amd.ops import hip_ops as K
+    B, H, C, A = 2, 65, 2048, 256
+    convs = [dict(B=B, OH=H, OW=H, Cin=C, Cout=A, k=1)]
+    for d in (6, 12, 18):
+        convs.append(dict(B=B, OH=H, OW=H, Cin=C, Cout=A, k=3, dil=d,
+                          perm=K.tap_group_perm(B, H, H, 3, d, 160)))
+    o = K.grouped_tile_order_i8(convs, 7).tolist()
+    tiles = []
+    for g, c in enumerate(convs):
+        M = c["perm"].numel() if "perm" in c else B * H * H
+        tiles += [(g << 24) | t for t in range(-(-M // 160) * (A // 128))]
+    assert sorted(o) == sorted(tiles)
+    taps = {g: K._tile_taps(B, H, H, c.get("k", 1), c.get("dil", 1), 160, c.get("perm"))
+            for g, c in enumerate(convs)}
+    cost = [int(taps[e >> 24][(e & 0xFFFFFF) // 2]) for e in o]
+    assert cost == sorted(cost, reverse=True) and cost[0] == 9 and cost[-1] == 1
+    # the permutation: the rate-18 branch's tiles average well under the raster tiles' taps
+    raster = K._tile_taps(B, H, H, 3, 18, 160, None).float().mean()
+    assert taps[3].float().mean() < 0.8 * raster
+    assert torch.is_tensor(K.grouped_tile_order_i8(convs[:1], 2))
+
+
+def test_grouped_tile_order_i8_branch_affine_cpu():
+    """xcds = 8: the same tiles, each XCD (position % 8) dominated by one 3x3 branch (a
+    branch's overflow past its XCD set's block count spills to the neighbours)."""
+    from semantic_segmentation_server_amd.ops import hip_ops as K
+    B, H = 2, 33
+    convs = [dict(B=B, OH=H, OW=H, Cin=1024, Cout=256)]
+    for d in (6, 12, 18):
+        convs.append(dict(B=B, OH=H, OW=H, Cin=1024, Cout=256, k=3, dil=d,
+                          perm=K.tap_group_perm(B, H, H, 3, d, 160)))
+    a = K.grouped_tile_order_i8(convs, 7).tolist()
+    b = K.grouped_tile_order_i8(convs, 7, xcds=8).tolist()
+    assert sorted(a) == sorted(b)
+    for x in range(8):
+        gs = [e >> 24 for e in b[x::8] if e >> 24 > 0]
+        assert max(gs.count(g) for g in set(gs)) >= 0.75 * len(gs)
