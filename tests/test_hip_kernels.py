@@ -375,6 +375,23 @@ def test_maxpool_gap_matvec():
     assert torch.allclose(mv.cpu(), F.relu(gref @ wm.t() + bm), atol=1e-3)
 
 
+@pytest.mark.parametrize("B,N,K,bias", [(8, 256, 2048, True), (9, 37, 2048, False), (1, 40, 64, True),
+                                         (3, 19, 30, True)])
+def test_matvec(B, N, K, bias):
+    """fp32 matvec head (batched 16-byte kernel for K % 4 == 0 and B > 1, per-(b, n) waves
+    otherwise) against torch."""
+    K_ = _hip()
+    g = torch.Generator().manual_seed(N)
+    x = torch.randn(B, K, generator=g)
+    w = torch.randn(N, K, generator=g)
+    b = torch.randn(N, generator=g) if bias else None
+    out = torch.empty(B, N, device=DEV)
+    K_.matvec(x.to(DEV), w.to(DEV), None if b is None else b.to(DEV), out, B=B, N=N, K=K, act="relu")
+    torch.cuda.synchronize()
+    ref = F.relu(x.double() @ w.double().t() + (0 if b is None else b.double()))
+    assert torch.allclose(out.cpu().double(), ref, rtol=1e-4, atol=1e-3)
+
+
 @pytest.mark.parametrize("B,HW,C", [(8, 65 * 65, 2048), (3, 37, 528), (2, 50, 40)])
 def test_global_avgpool_i8(B, HW, C):
     """int8 NHWC global average pool (16-byte vector kernel for C % 16 == 0, byte kernel
