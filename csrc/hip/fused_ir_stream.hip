@@ -672,22 +672,46 @@ void fused_ir_stream(const FusedSpanParams& p, hipStream_t st) {
 // out = act(sum_h part[h] + bias (+ residual)), bf16: the combine of the hidden-split stream
 // and of the split-K grouped ASPP GEMM (fixed summation order h = 0..HS-1, so the result is
 // a function of the inputs alone)
+// HSM: compile-time bound on HS, so every slab's loads (and the residual's) are issued before
+// the first add -- one L2 round trip per unit instead of HS dependent ones (the runtime-HS loop
+// ran 4.5-5 us per combine at batch 1, profiles/r6b_b1_layer_times.txt)
+template <int HSM>
 __global__ __launch_bounds__(256) void stream_combine_kernel(const float* __restrict__ part, const float* __restrict__ bp,
                                                              const bf16* __restrict__ res, bf16* __restrict__ out,
                                                              int HS, long long M, int Cout, int relu) {
   const long long units = M * (Cout / 8);
   const long long slab = M * Cout;
+  const int cg = Cout / 8;
   for (long long u = blockIdx.x * 256ll + threadIdx.x; u < units; u += (long long)gridDim.x * 256) {
-    const long long m = u / (Cout / 8);
-    const int c = (int)(u - m * (Cout / 8)) * 8;
+    const long long m = units < (1ll << 31) ? (long long)((int)u / cg) : u / cg;
+    const int c = (int)(u - m * cg) * 8;
     const float* q = part + m * Cout + c;
     f32x4 s0 = *reinterpret_cast<const f32x4*>(bp + c), s1 = *reinterpret_cast<const f32x4*>(bp + c + 4);
-    for (int h = 0; h < HS; ++h) {
-      s0 += *reinterpret_cast<const f32x4*>(q + h * slab);
-      s1 += *reinterpret_cast<const f32x4*>(q + h * slab + 4);
-    }
     bf16x8 r = zero8();
-    if (res) r = ld8(res + m * Cout + c);
+    if constexpr (HSM > 0) {
+      f32x4 p0[HSM], p1[HSM];
+#pragma unroll
+      for (int h = 0; h < HSM; ++h) {
+        if (h < HS) {
+          p0[h] = *reinterpret_cast<const f32x4*>(q + h * slab);
+          p1[h] = *reinterpret_cast<const f32x4*>(q + h * slab + 4);
+        }
+      }
+      if (res) r = ld8(res + m * Cout + c);
+#pragma unroll
+      for (int h = 0; h < HSM; ++h) {  // fixed order h = 0..HS-1
+        if (h < HS) {
+          s0 += p0[h];
+          s1 += p1[h];
+        }
+      }
+    } else {  // HS > 8 (hidden splits up to the chunk count): the runtime loop
+      for (int h = 0; h < HS; ++h) {
+        s0 += *reinterpret_cast<const f32x4*>(q + h * slab);
+        s1 += *reinterpret_cast<const f32x4*>(q + h * slab + 4);
+      }
+      if (res) r = ld8(res + m * Cout + c);
+    }
     float v[8];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -707,7 +731,12 @@ void stream_combine(const float* part, const float* bp, const bf16* res, bf16* o
   if (Cout % 8 || HS < 1 || M < 1) throw std::invalid_argument("stream_combine: Cout % 8, HS >= 1");
   const long long units = M * (Cout / 8);
   const int grid = (int)std::min<long long>((units + 255) / 256, 2048);
-  hipLaunchKernelGGL(stream_combine_kernel, dim3(grid), dim3(256), 0, st, part, bp, res, out, HS, M, Cout, act);
+  if (HS <= 4)
+    hipLaunchKernelGGL(stream_combine_kernel<4>, dim3(grid), dim3(256), 0, st, part, bp, res, out, HS, M, Cout, act);
+  else if (HS <= 8)
+    hipLaunchKernelGGL(stream_combine_kernel<8>, dim3(grid), dim3(256), 0, st, part, bp, res, out, HS, M, Cout, act);
+  else
+    hipLaunchKernelGGL(stream_combine_kernel<0>, dim3(grid), dim3(256), 0, st, part, bp, res, out, HS, M, Cout, act);
   check_launch("stream_combine");
 }
 
