@@ -54,6 +54,24 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
 
 __host__ __device__ __forceinline__ int cdiv_dev(int a, int b) { return (a + b - 1) / b; }
 
+// Taps (bit ky * KW + kx) of a KH x KW 'same' conv whose input pixel is inside the image for
+// the output pixel at input position (ay, ax): separable in y and x, so O(KH + KW) compares
+// and no per-tap division (the per-tap t / KW, t % KW form was ~40 VALU per tap per row in
+// the LDS-DMA GEMM prologues: a visible share of a short-K tile's VALU stream)
+__device__ __forceinline__ int conv_tap_mask(int ay, int ax, int KH, int KW, int dil, int IH, int IW) {
+  int xb = 0;
+  for (int kx = 0; kx < KW; ++kx) {
+    const int ix = ax + (kx - KW / 2) * dil;
+    xb |= (ix >= 0 && ix < IW ? 1 : 0) << kx;
+  }
+  int bits = 0;
+  for (int ky = 0; ky < KH; ++ky) {
+    const int iy = ay + (ky - KH / 2) * dil;
+    if (iy >= 0 && iy < IH) bits |= xb << (ky * KW);
+  }
+  return bits;
+}
+
 // Letterboxed camera pixels of an IHT x IWT model-input window at (iy0, ix0) ->
 // LDS as normalised bf16 RGB0 (x / 127.5 - 1, BGR -> RGB; -1 for letterbox
 // padding, 0 outside the H x W model input = conv zero padding). Model pixel

@@ -530,12 +530,7 @@ __device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char
     ay[i] = (rem / a.OW) * a.stride;
     ax[i] = (rem % a.OW) * a.stride;
     aoff[i] = ((b * a.IH + ay[i]) * a.IW + ax[i]) * a.Cin;
-    if (av[i])
-      for (int t = 0; t < taps; ++t) {
-        const int iy = ay[i] + (t / a.KW - a.KH / 2) * a.dil;
-        const int ix = ax[i] + (t % a.KW - a.KW / 2) * a.dil;
-        if (iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW) tapbits |= 1 << t;
-      }
+    if (av[i]) tapbits |= conv_tap_mask(ay[i], ax[i], a.KH, a.KW, a.dil, a.IH, a.IW);
   }
   int boff[GB];
   bool bv[GB];
@@ -700,25 +695,37 @@ __device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char
     }
     return;
   }
+  // the lane's 4 output channels of each 16-channel subtile are the same for every pixel
+  // subtile: their bias is loaded once (one 16-byte load per j, not 4 x MT scalar loads)
+  f32x4 bj[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int n = n0 + wn * 16 * NT + j * 16 + kq * 4;
+    if (n + 3 < a.Cout) {
+      bj[j] = *reinterpret_cast<const f32x4*>(a.bias + n);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bj[j][q] = n + q < a.Cout ? a.bias[n + q] : 0.f;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
     const int mg = m0 + wm * 16 * MT + i * 16 + r16;
     if (mg >= M) continue;
     const int m = a.perm ? a.perm[mg] : mg;
     if (m < 0) continue;
-    const int b = m / (a.OH * a.OW);
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       const int n = n0 + wn * 16 * NT + j * 16 + kq * 4;
       if (n >= a.Cout) continue;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      float v[4] = {acc[i][j][0] + bj[j][0], acc[i][j][1] + bj[j][1], acc[i][j][2] + bj[j][2],
+                    acc[i][j][3] + bj[j][3]};
       const bool full = n + 3 < a.Cout;
+      if (a.img_bias) {
+        const int b = m / (a.OH * a.OW);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (n + q < a.Cout) {
-          v[q] += a.bias[n + q];
-          if (a.img_bias) v[q] += a.img_bias[(long long)b * a.Cout + n + q];
-        }
+        for (int q = 0; q < 4; ++q)
+          if (n + q < a.Cout) v[q] += a.img_bias[(long long)b * a.Cout + n + q];
       }
       if (a.res) {
         const bf16* rp = a.res + (long long)m * a.ldr + n;

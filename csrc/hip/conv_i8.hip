@@ -351,13 +351,7 @@ __device__ __forceinline__ void i8_glds_tile(const I8Args& a, const int bid, cha
     const int rem = mm - b * a.OH * a.OW;
     const int ay = (rem / a.OW) * a.stride, ax = (rem % a.OW) * a.stride;
     aoff[i] = (unsigned)((((b * a.IH + ay) * a.IW + ax) * a.Cin) + lc * 16);
-    int bits = 0;
-    if (pm >= 0)
-      for (int t = 0; t < taps; ++t) {
-        const int iy = ay + (t / a.KW - a.KH / 2) * a.dil;
-        const int ix = ax + (t % a.KW - a.KW / 2) * a.dil;
-        if (iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW) bits |= 1 << t;
-      }
+    const int bits = pm >= 0 ? conv_tap_mask(ay, ax, a.KH, a.KW, a.dil, a.IH, a.IW) : 0;
     nrtap[i] = ~bits;
     tapbits |= bits;
   }
