@@ -474,10 +474,8 @@ static int pick_nt(int Cout);
 // regime of every deep-K conv here: 128x128 tiles over M = B*33*33 or B*65*65).
 // One glds wave-instruction writes 1 KiB = 8 rows x 128 B lane-linearly, so the
 // XOR swizzle (phys chunk = logical ^ (row & 7)) is applied on the SOURCE
-// address; padded chunks (outside the image, beyond Cin/Cout, M tail) read from a
-// zero page, so the LDS image is always fully written.
-__device__ __attribute__((aligned(16))) int4 g_zero_page[8];
-
+// address; padded chunks (outside the image, beyond Cin/Cout, M tail) read zeros through
+// the buffer descriptor's range check, so the LDS image is always fully written.
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 // One BM x BN output tile (tile index bid in row-major (m-tile, n-tile) order) of
@@ -532,13 +530,11 @@ __device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char
     aoff[i] = ((b * a.IH + ay[i]) * a.IW + ax[i]) * a.Cin;
     if (av[i]) tapbits |= conv_tap_mask(ay[i], ax[i], a.KH, a.KW, a.dil, a.IH, a.IW);
   }
-  int boff[GB];
-  bool bv[GB];
+  unsigned boff2[GB];  // weight row byte offsets, kOOB past Cout
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
     const int n = n0 + wid * (BN / NW) + j * RPG + grow;
-    bv[j] = n < a.Cout;
-    boff[j] = (bv[j] ? n : 0) * taps * a.Cin;
+    boff2[j] = n < a.Cout ? (unsigned)(n * taps * a.Cin) * 2u : 0x80000000u;
   }
   if (tid == 0) *s_tap = 0;
   __syncthreads();
@@ -561,8 +557,16 @@ __device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char
   // the tap's weight offset. Round 2 recomputed the bounds and offsets for every 64-channel
   // stage: ~135 VALU + ~155 SALU per wave and stage against 32 MFMAs (PMC of the 16-wave
   // grouped ASPP tile, profiles/r3_step_pmc.txt)
-  int asrc[GA];
-  int wtap = 0;
+  // Round 5: the rows arrive through buffer_load ... lds on range-checked descriptors (the
+  // int8 kernel's form): a padding row's byte offset carries bit 31, past the descriptor's
+  // end, and the hardware writes zeros -- no zero-page pointer selects or 64-bit address math.
+  constexpr unsigned kOOB = 0x80000000u;
+  const auto rin = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.in), 0,
+                                                     (int)((long long)a.B * a.IH * a.IW * a.Cin * 2), 0x00020000);
+  const auto rwt = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.w), 0,
+                                                     (int)((long long)a.Cout * taps * a.Cin * 2), 0x00020000);
+  unsigned abyte[GA];  // this tap's row byte offsets (channel 0), kOOB for padding
+  unsigned wbyte = 0;
   auto set_tap = [&]() {
     const int t = (int)((tl >> (4 * is_tap)) & 15);
     const int dy = (t / a.KW - a.KH / 2) * a.dil, dx = (t % a.KW - a.KW / 2) * a.dil;
@@ -571,25 +575,27 @@ __device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char
     for (int i = 0; i < GA; ++i) {
       const int iy = ay[i] + dy, ix = ax[i] + dx;
       const bool ok = av[i] && iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW;
-      asrc[i] = ok ? aoff[i] + doff : -1;
+      abyte[i] = ok ? (unsigned)(aoff[i] + doff) * 2u : kOOB;
     }
-    wtap = t * a.Cin;
+    wbyte = (unsigned)(t * a.Cin) * 2u;
   };
   if (total > 0) set_tap();
+  const int cin_left = a.Cin - lc * 8;  // this lane's 16-byte chunk exists while is_c * BK < cin_left
   auto issue = [&](int stage) {
-    const int c = is_c * BK + lc * 8;
-    const bool cok = c < a.Cin;
+    const int cb = is_c * BK;
+    const unsigned cbad = (unsigned)(cin_left - cb - 1) & kOOB;
+    const unsigned cbyte = (unsigned)(cb + lc * 8) * 2u;
     char* sA = smem + stage * SB;
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
-      const void* src = (asrc[i] >= 0 && cok) ? (const void*)(a.in + asrc[i] + c) : (const void*)g_zero_page;
-      __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(sA + (wid * (BM / NW) + i * RPG) * ROWB), 16, 0, 0);
+      const unsigned vo = (abyte[i] + cbyte) | cbad;  // (a named offset: the host pass rejects the inline form)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_ptr_t)(sA + (wid * (BM / NW) + i * RPG) * ROWB), 16, vo, 0, 0, 0);
     }
     char* sB = sA + BM * ROWB;
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
-      const void* src = (bv[j] && cok) ? (const void*)(a.w + boff[j] + wtap + c) : (const void*)g_zero_page;
-      __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(sB + (wid * (BN / NW) + j * RPG) * ROWB), 16, 0, 0);
+      const unsigned vo = (boff2[j] + wbyte + cbyte) | cbad;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rwt, (lds_ptr_t)(sB + (wid * (BN / NW) + j * RPG) * ROWB), 16, vo, 0, 0, 0);
     }
     if (++is_c == cch) {
       is_c = 0;
@@ -880,8 +886,9 @@ void conv_gemm(const ConvParams& p, hipStream_t s) {
   // auto: LDS-DMA 2-stage for deep K on grids that fill the chip (scripts/bench_conv.py
   // on MI355X: 1.2-1.9x the register-staged LDS kernel from K = 256 up; shallow-K
   // layers are output-write-bound and stay on the register-fed kernel)
-  const bool glds_ok = (long long)p.B * p.IH * p.IW * p.Cin < (1LL << 31) &&
-                       (long long)p.Cout * K < (1LL << 31) && p.KH * p.KW <= 16;  // int32 offsets, tap list
+  // 32-bit buffer byte offsets below 2^31 (bf16: 2^30 elements), <= 16 taps in the tap list
+  const bool glds_ok = (long long)p.B * p.IH * p.IW * p.Cin < (1LL << 30) &&
+                       (long long)p.Cout * K < (1LL << 30) && p.KH * p.KW <= 16;
   int variant = p.variant;
   if (variant == 0) variant = (tiles >= 128 && K >= 256) ? (glds_ok ? 4 : 2) : 1;
   if (p.perm && (variant < 3 || variant == 7 || variant > 10 || !glds_ok))
@@ -971,9 +978,9 @@ void conv_gemm_grouped(const ConvParams* ps, int n, const int* order, int nblock
     const ConvParams& p = ps[i < n ? i : 0];
     if (p.Cin % 8 != 0 || p.KH * p.KW > 16 || p.Cout != ps[0].Cout)
       throw std::invalid_argument("conv_gemm_grouped: Cin % 8, <= 16 taps and one Cout required");
-    if ((long long)p.B * p.IH * p.IW * p.Cin >= (1LL << 31) ||
-        (long long)p.Cout * p.KH * p.KW * p.Cin >= (1LL << 31))
-      throw std::invalid_argument("conv_gemm_grouped: tensor too large for 32-bit offsets");
+    if ((long long)p.B * p.IH * p.IW * p.Cin >= (1LL << 30) ||
+        (long long)p.Cout * p.KH * p.KW * p.Cin >= (1LL << 30))
+      throw std::invalid_argument("conv_gemm_grouped: tensor too large for 32-bit byte offsets");
     ga.g[i] = to_args(p);
   }
   ga.order = order;
