@@ -39,7 +39,27 @@ __device__ __forceinline__ i32x4v ld16(const int8_t* p) { return *reinterpret_ca
 // the activation and the int8 range are one med3 on the +128 offset grid, v_cvt_pk_u8_f32
 // rounds (nearest even) and packs, XOR 0x80 gives the signed bytes. ~8 VALU per value
 // instead of ~13 for the float chain, and within one rounding step of it (round 5).
-__device__ __forceinline__ i32x4v i8_requant16(const I8Args& a, const i32x4v (&v)[4], int m, int n) {
+// the 16 channels' folded constants: s = scale * ios, b = bias * ios + 128 - 128 * rs
+struct I8Fold16 {
+  float s[16], b[16];
+};
+__device__ __forceinline__ I8Fold16 i8_fold16(const I8Args& a, int n) {
+  const float ios = a.inv_out_scale;
+  const float rs = a.res ? a.res_scale * ios : 0.f;
+  I8Fold16 f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const float4 sc = *reinterpret_cast<const float4*>(a.scale + n + c * 4);
+    const float4 bi = *reinterpret_cast<const float4*>(a.bias + n + c * 4);
+    f.s[c * 4 + 0] = sc.x * ios; f.s[c * 4 + 1] = sc.y * ios; f.s[c * 4 + 2] = sc.z * ios; f.s[c * 4 + 3] = sc.w * ios;
+    f.b[c * 4 + 0] = fmaf(bi.x, ios, 128.f - 128.f * rs); f.b[c * 4 + 1] = fmaf(bi.y, ios, 128.f - 128.f * rs);
+    f.b[c * 4 + 2] = fmaf(bi.z, ios, 128.f - 128.f * rs); f.b[c * 4 + 3] = fmaf(bi.w, ios, 128.f - 128.f * rs);
+  }
+  return f;
+}
+
+__device__ __forceinline__ i32x4v i8_requant16(const I8Args& a, const i32x4v (&v)[4], int m, int n,
+                                               const I8Fold16& f) {
   const float ios = a.inv_out_scale;
   const float rs = a.res ? a.res_scale * ios : 0.f;
   const float lo = a.act == ACT_NONE ? 1.f : 128.f;
@@ -53,11 +73,8 @@ __device__ __forceinline__ i32x4v i8_requant16(const I8Args& a, const i32x4v (&v
   i32x4v pk;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    const float4 sc = *reinterpret_cast<const float4*>(a.scale + n + c * 4);
-    const float4 bi = *reinterpret_cast<const float4*>(a.bias + n + c * 4);
-    const float s4[4] = {sc.x * ios, sc.y * ios, sc.z * ios, sc.w * ios};
-    float b4[4] = {fmaf(bi.x, ios, 128.f - 128.f * rs), fmaf(bi.y, ios, 128.f - 128.f * rs),
-                   fmaf(bi.z, ios, 128.f - 128.f * rs), fmaf(bi.w, ios, 128.f - 128.f * rs)};
+    const float s4[4] = {f.s[c * 4], f.s[c * 4 + 1], f.s[c * 4 + 2], f.s[c * 4 + 3]};
+    float b4[4] = {f.b[c * 4], f.b[c * 4 + 1], f.b[c * 4 + 2], f.b[c * 4 + 3]};
     if (a.img_bias) {
       const int b = m / (a.OH * a.OW);
       const float4 ib = *reinterpret_cast<const float4*>(a.img_bias + (size_t)b * a.Cout + n + c * 4);
@@ -77,6 +94,10 @@ __device__ __forceinline__ i32x4v i8_requant16(const I8Args& a, const i32x4v (&v
   return pk;
 }
 
+__device__ __forceinline__ i32x4v i8_requant16(const I8Args& a, const i32x4v (&v)[4], int m, int n) {
+  return i8_requant16(a, v, m, n, i8_fold16(a, n));
+}
+
 // Transposing epilogue (NT == 4: a wave's 64 output channels): the MFMA C layout
 // gives a lane 4 channels of one pixel per 16-channel subtile, so a direct store is
 // 4 bytes per lane at a Cout stride and the int8 residual is read byte by byte.
@@ -93,6 +114,10 @@ __device__ __forceinline__ void i8_epilogue_lds(const I8Args& a, const i32x4v (&
   const int M = a.B * a.OH * a.OW;
   const int r16 = lane & 15, kq = lane >> 4;
   const int px = lane >> 2, cb = (lane & 3) * 16;
+  // the lane's 16 channels are the same for every pixel group: fold their constants once
+  const bool fast = (a.Cout & 15) == 0 && a.out_mode == 0 && ((a.ldo | a.co_off) & 15) == 0;
+  I8Fold16 fold;
+  if (fast && nbase + cb + 16 <= a.Cout) fold = i8_fold16(a, nbase + cb);
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
 #pragma unroll
@@ -113,9 +138,9 @@ __device__ __forceinline__ void i8_epilogue_lds(const I8Args& a, const i32x4v (&
     for (int c = 0; c < 4; ++c)
 #pragma unroll
       for (int q = 0; q < 4; ++q) f[c * 4 + q] = (float)v[c][q];
-    if (n + 16 <= a.Cout && (a.Cout & 15) == 0 && a.out_mode == 0 && ((a.ldo | a.co_off) & 15) == 0) {
+    if (fast && n + 16 <= a.Cout) {
       *reinterpret_cast<i32x4v*>(static_cast<int8_t*>(a.out) + (size_t)m * a.ldo + a.co_off + n) =
-          i8_requant16(a, v, m, n);
+          i8_requant16(a, v, m, n, fold);
     } else if (n + 16 <= a.Cout && (a.Cout & 15) == 0) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {

@@ -378,8 +378,7 @@ def test_maxpool_gap_matvec():
 @pytest.mark.parametrize("B,N,K,bias", [(8, 256, 2048, True), (9, 37, 2048, False), (1, 40, 64, True),
                                          (3, 19, 30, True)])
 def test_matvec(B, N, K, bias):
-    """fp32 matvec head (batched 16-byte kernel for K % 4 == 0 and B > 1, per-(b, n) waves
-    otherwise) against torch."""
+    """fp32 matvec head (one wave per (b, n), lanes split K) against torch."""
     K_ = _hip()
     g = torch.Generator().manual_seed(N)
     x = torch.randn(B, K, generator=g)
