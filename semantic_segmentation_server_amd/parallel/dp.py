@@ -346,10 +346,29 @@ class DataParallelPipeline:
         running counters, the time the batch was prefetched, rank * S + i % S). They
         travel with the records
         through the gather so rank 0 can tag every record with its origin.
-        ``next_frames`` (pinned host batch): its H2D starts on the copy stream as
-        soon as this step's compute is enqueued, so ingest overlaps compute
-        (double-buffered staging) instead of preceding it.
+        ``next_frames`` (pinned host batch): its H2D overlaps compute (double-buffered
+        staging) instead of preceding it. At lag >= 1 it starts after this step's
+        collect (the lag steps still queued on the GPU cover the copy), not right after
+        this step's launch: the next frames then wait one step less in staging, so the
+        capture -> record latency drops by a step interval at the same throughput. At lag
+        0 the collect drains the GPU, so the copy is issued before it.
         """
+        early = next_frames is not None and self.lag == 0
+        out = self._step(frame_ids, ts, streams, next_frames if early else None)
+        if next_frames is not None and not early:
+            self._prefetch_next(next_frames)
+        return out
+
+    def _prefetch_next(self, next_frames) -> None:
+        nxt = (self.slot + 1) % self.nslots
+        on_slot = self._slot_stream(nxt) is not None
+        if self.cuda and not on_slot:  # the slot being refilled was last read nslots - 1 steps ago
+            ev = self._consumed[nxt]
+            self.copy_stream.wait_stream(torch.cuda.current_stream(self.dev)) \
+                if ev is None else self.copy_stream.wait_event(ev)
+        self.prefetch(next_frames)
+
+    def _step(self, frame_ids, ts, streams, next_frames) -> np.ndarray:
         B = self.B
         scatter = self.ingest == "scatter" and self.ctx.initialized
         nb = B * self.ctx.world if (scatter and self.ctx.is_root) else B
@@ -377,13 +396,7 @@ class DataParallelPipeline:
                 consumed.record(torch.cuda.current_stream(self.dev))
             self._consumed[self.slot] = consumed
         if next_frames is not None:
-            nxt = (self.slot + 1) % self.nslots
-            on_slot = self._slot_stream(nxt) is not None
-            if self.cuda and not on_slot:  # the slot being refilled was last read nslots - 1 steps ago
-                ev = self._consumed[nxt]
-                self.copy_stream.wait_stream(torch.cuda.current_stream(self.dev)) \
-                    if ev is None else self.copy_stream.wait_event(ev)
-            self.prefetch(next_frames)
+            self._prefetch_next(next_frames)
         if packed is None:  # host post-processing path (torch backend / exact mode)
             self.frames_done += B * self.ctx.world
             return self.engine.records_from_labels(labels, fids, tss, strm)
