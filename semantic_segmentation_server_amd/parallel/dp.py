@@ -138,6 +138,13 @@ class DataParallelPipeline:
         elif self.lag and auto_lag and hasattr(engine, "preferred_lag"):
             self.lag = max(self.lag, int(engine.preferred_lag()))
         self.nslots = max(2, self.lag + 1)
+        # SSA_EARLY_PREFETCH=1: the next batch's H2D right after this step's launch (the
+        # pre-round-5 order) instead of after its collect
+        self.early_prefetch = os.environ.get("SSA_EARLY_PREFETCH", "0") == "1"
+        # only small batches take the late copy: config 4's 50 MB batches (8 x 2048 x 1024 BGR)
+        # lost 13-15 % of throughput with it (2281-2359 vs 2688-2689 frames/s on one box,
+        # profiles/r7q_late_prefetch.txt); batch 1 (0.9 MB) gains a step of latency
+        self.late_prefetch_max = int(os.environ.get("SSA_LATE_PREFETCH_MAX_BYTES", str(8 << 20)))
         self.gather_mode = gather
         self.engine = engine
         self.B = int(batch)
@@ -347,13 +354,15 @@ class DataParallelPipeline:
         travel with the records
         through the gather so rank 0 can tag every record with its origin.
         ``next_frames`` (pinned host batch): its H2D overlaps compute (double-buffered
-        staging) instead of preceding it. At lag >= 1 it starts after this step's
-        collect (the lag steps still queued on the GPU cover the copy), not right after
-        this step's launch: the next frames then wait one step less in staging, so the
-        capture -> record latency drops by a step interval at the same throughput. At lag
-        0 the collect drains the GPU, so the copy is issued before it.
+        staging) instead of preceding it. At lag >= 1 and for batches up to
+        ``late_prefetch_max`` bytes it starts after this step's collect (the lag steps
+        still queued on the GPU cover the copy), not right after this step's launch: the
+        next frames then wait one step less in staging, so the capture -> record latency
+        drops by a step interval. At lag 0 (the collect drains the GPU) and for large
+        batches (measured slower) the copy is issued right after the launch.
         """
-        early = next_frames is not None and self.lag == 0
+        early = next_frames is not None and (self.lag == 0 or self.early_prefetch
+                                             or next_frames.numel() > self.late_prefetch_max)
         out = self._step(frame_ids, ts, streams, next_frames if early else None)
         if next_frames is not None and not early:
             self._prefetch_next(next_frames)
