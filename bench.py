@@ -21,6 +21,13 @@ subprocess measures GetSegmentedObjects latency while all ranks keep stepping
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
+
+``--gpus N`` means N ranks in both launch forms: under torchrun it must equal WORLD_SIZE
+(else exit 2); without a launcher this process (which never touches the GPU) starts N
+rank processes itself, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 /
+MASTER_PORT set before any GPU call, and rank 0's JSON line is the output. At N > 1 on
+GPUs the records reach rank 0 through the stream-ordered RCCL gather (parallel/rccl.py);
+the JSON reports ``rccl_nranks`` from ``ncclCommCount`` on rank 0's communicator.
 """
 from __future__ import annotations
 
@@ -58,18 +65,21 @@ def main() -> int:
     p.add_argument("--aspp", default="full")
     p.add_argument("--input_size", type=int, default=513)
     p.add_argument("--camera", default="640x480")
-    p.add_argument("--ingest", choices=["local", "scatter"], default="local")
+    p.add_argument("--ingest", choices=["local", "scatter"], default="local",
+                   help="local: each rank uploads its own frames (the default); scatter: rank 0 "
+                        "uploads the node batch and ncclScatter spreads it (an ablation: at N = 8, "
+                        "B = 32 rank 0's one PCIe link carries 256 x 921.6 KB = 236 MB per step, "
+                        "~4.3 ms at ~55 GB/s against a ~0.9 ms step)")
     p.add_argument("--gather", choices=["auto", "host", "rccl"], default="auto",
-                   help="record gather to rank 0: auto = host (each rank's records are "
-                        "written to pinned memory by a kernel and gathered over gloo: no GPU "
-                        "time); rccl = RCCL gather over xGMI on the result stream")
+                   help="record gather to rank 0: rccl = ncclGather of packed record rows over "
+                        "xGMI, enqueued on the result stream (the auto choice on GPUs at N > 1); "
+                        "host = each rank's records written to pinned memory by a kernel and "
+                        "gathered over gloo (the auto choice at N = 1 and on CPU; an ablation at "
+                        "N > 1). World-size-1 cost of the RCCL gather: 1.2-2.5 %% "
+                        "(profiles/r5f_rccl_world1_ab.txt)")
     p.add_argument("--pg", choices=["auto", "nccl", "gloo"], default="auto",
                    help="process-group backend; auto: RCCL (+ a gloo control group) when an "
-                        "RCCL data path is requested (--ingest scatter, --gather rccl), else "
-                        "gloo. Measured on one MI355X with world-size-1 groups "
-                        "(profiles/r4_rccl_gather_ab.txt): gloo + host gather 33.8-33.9k, "
-                        "RCCL group + host gather 32.0k, RCCL group + RCCL gather 30.2-30.6k "
-                        "frames/s")
+                        "RCCL data path is in use (--ingest scatter, the RCCL gather), else gloo")
     p.add_argument("--contour_mode", choices=["fast", "exact", "none"], default="fast")
     p.add_argument("--no-graph", dest="graph", action="store_false")
     p.add_argument("--rpc", type=int, default=2000, help="GetSegmentedObjects calls to time (0: skip)")
@@ -91,6 +101,16 @@ def main() -> int:
                    help="strong scaling: a fixed node-wide batch split over the ranks (per-GPU "
                         "batch = global_batch / N; BASELINE config 3 as written: 32 over 8 GPUs)")
     a = p.parse_args()
+    if a.gpus < 1:
+        p.error("--gpus must be >= 1")
+    if not a.supervise:
+        ws = os.environ.get("WORLD_SIZE")
+        if ws is not None and int(ws) != a.gpus:
+            print(f"bench: --gpus {a.gpus} but the launcher started WORLD_SIZE={ws} ranks",
+                  file=sys.stderr)
+            return 2
+        if ws is None and a.gpus > 1:
+            return _spawn_ranks(a.gpus)
     a.scaling = "weak"
     if a.global_batch:
         nw = int(os.environ.get("WORLD_SIZE", "1")) if not a.supervise else max(1, a.gpus)
@@ -126,6 +146,9 @@ def main() -> int:
         print("bench: --ingest scatter needs RCCL, which SSA_SHARE_GPU=1 rules out; using local ingest",
               file=sys.stderr)
         a.ingest = "local"
+    if a.gather == "auto":
+        # N > 1 on GPUs: the records travel over xGMI (RCCL), as in the north-star config
+        a.gather = "rccl" if (gpu and world > 1 and not share) else "host"
     pg = a.pg if a.pg != "auto" else (
         "nccl" if gpu and not share and (a.ingest == "scatter" or a.gather == "rccl") else "gloo")
     ctx = D.init(pg, device="cuda" if _t.cuda.is_available() and a.backend != "cpu" else "auto")
@@ -249,6 +272,7 @@ def main() -> int:
                 "ingest": a.ingest,
                 "gather": pipe.gather_mode,
                 "process_group": ctx.backend,
+                "rccl_nranks": pipe.rccl_nranks(),
                 "backend": a.backend,
                 "hipgraph": bool(a.graph and ctx.device.type == "cuda"),
                 "contour_mode": a.contour_mode,
@@ -262,6 +286,9 @@ def main() -> int:
             "p99_get_segmented_objects_ms": rpc.get("p99_ms") if rpc else None,
             "p50_frame_latency_ms": None if frame_lat["p50"] is None else round(frame_lat["p50"], 4),
             "p99_frame_latency_ms": None if frame_lat["p99"] is None else round(frame_lat["p99"], 4),
+            "pg_backend": ctx.backend,
+            "gather": pipe.gather_mode,
+            "rccl_nranks": pipe.rccl_nranks(),
             "frames_collected": frames_collected,
             "streams_collected": streams_seen,
             "frame_order_errors": order_errors,
@@ -274,6 +301,47 @@ def main() -> int:
         print(json.dumps(out), flush=True)
     D.destroy(ctx)
     return 0
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _spawn_ranks(n: int) -> int:
+    """``python bench.py --gpus N`` without a launcher: start N rank processes of this
+    same command (one per GPU), each with the torchrun environment set before it makes
+    any GPU call; this parent imports no GPU library. Rank 0 prints the JSON line. The
+    first rank to fail takes the others down (their exact PIDs) and sets the exit code."""
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                   MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for pr in list(live):
+            code = pr.poll()
+            if code is None:
+                continue
+            live.remove(pr)
+            if code != 0 and rc == 0:
+                rc = code
+                print(f"bench: rank {procs.index(pr)} exited with {code}; stopping the others",
+                      file=sys.stderr)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc if rc >= 0 else 128 - rc
 
 
 def _serve_bench(a) -> int:

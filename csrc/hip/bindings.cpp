@@ -399,13 +399,6 @@ PYBIND11_MODULE(_hip, m) {
                         uintptr_t stream) {
     pack_rows(P<void>(dst), P<const void>(a), aw, P<const void>(b), bw, rows, S(stream));
   });
-  m.def("poison_lds", [](uint32_t pat, int blocks, uintptr_t stream) {
-    poison_lds(pat, blocks, S(stream));
-  });
-  m.def("poison_regs", [](int blocks, uintptr_t stream) { poison_regs(blocks, S(stream)); });
-  m.def("lds_canary", [](int iters, uintptr_t bad, int blocks, uintptr_t stream) {
-    lds_canary(iters, P<unsigned>(bad), blocks, S(stream));
-  });
   m.def("postprocess",
         [](uintptr_t labels, int B, int H, int W, int crop_h, int crop_w, uintptr_t palette,
            int thr, double min_area, int num_bins, int K, uintptr_t ws, uintptr_t records,

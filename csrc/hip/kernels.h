@@ -308,11 +308,6 @@ void copy_to_host(const void* src, void* dst, long long nbytes, hipStream_t s);
 void pack_rows(void* dst, const void* a, int a_words, const void* b, int b_words, int rows,
                hipStream_t s);
 
-// Debug only (debug_poison.hip): NaN-pattern fill of every CU's LDS / every SIMD's
-// VGPR+AGPR file, to expose kernels that read on-chip state they did not write.
-void poison_lds(uint32_t pat, int blocks, hipStream_t s);
-void poison_regs(int blocks, hipStream_t s);
-void lds_canary(int iters, unsigned* bad, int blocks, hipStream_t s);
 void postprocess(const PostParams& p, hipStream_t s);
 
 }  // namespace ssa

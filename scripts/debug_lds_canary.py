@@ -15,7 +15,7 @@ _ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, _ROOT)
 from semantic_segmentation_server_amd import config as C  # noqa: E402
 from semantic_segmentation_server_amd.models.hip_model import Choice  # noqa: E402
-from semantic_segmentation_server_amd.ops.native import hip as H  # noqa: E402
+from semantic_segmentation_server_amd.ops.native import hip_debug as H  # noqa: E402
 from semantic_segmentation_server_amd.runtime.engine import Engine  # noqa: E402
 from semantic_segmentation_server_amd.runtime.sources import SyntheticSource  # noqa: E402
 

@@ -4,7 +4,10 @@ Two pybind11 modules are produced next to this file:
 
 * ``_host``  — host C++ (g++): exact contour oracle, result ring, etc.
 * ``_hip``   — HIP kernels for gfx950 (hipcc ``--offload-arch=gfx950``) plus their
-  launch wrappers. No torch C++ headers are involved: tensors cross the boundary
+  launch wrappers.
+* ``_hip_debug`` — diagnostic kernels only (csrc/hip_debug: on-chip state poison, LDS
+  canary), built on demand (``build_hip_debug``, or ``SSA_BUILD_DEBUG=1``), never part of
+  the production module. No torch C++ headers are involved: tensors cross the boundary
   as raw device pointers and the caller's HIP stream handle, so launches are
   capturable by ``torch.cuda.CUDAGraph`` (hipGraph) and compile in seconds.
 
@@ -133,8 +136,30 @@ def build_hip(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
     return out
 
 
+def build_hip_debug(force: bool = False, verbose: bool = False) -> str:
+    srcs = sorted(glob.glob(os.path.join(CSRC, "hip_debug", "*.hip")))
+    binding = os.path.join(CSRC, "hip_debug", "bindings_debug.cpp")
+    out = os.path.join(HERE, "_hip_debug" + EXT_SUFFIX)
+    flags = ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-fno-gpu-rdc"]
+    stamp = _stamp(srcs + [binding], flags)
+    if not force and _up_to_date(out, stamp):
+        return out
+    inc = [f"-I{p}" for p in _pybind_includes()]
+    cmd = [HIPCC] + flags + inc + srcs + [binding, "-o", out + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    _run(cmd)
+    os.replace(out + ".tmp", out)
+    with open(out + ".stamp", "w") as f:
+        f.write(stamp)
+    return out
+
+
 def build_all(force: bool = False, verbose: bool = False):
-    return build_host(force, verbose), build_hip(force, verbose)
+    outs = (build_host(force, verbose), build_hip(force, verbose))
+    if os.environ.get("SSA_BUILD_DEBUG", "0") == "1":
+        outs += (build_hip_debug(force, verbose),)
+    return outs
 
 
 if __name__ == "__main__":

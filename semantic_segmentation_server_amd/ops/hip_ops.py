@@ -1101,10 +1101,11 @@ def poison_chip(lds: bool = True, regs: bool = True, pat: int = 0x7FC07FC0) -> N
     """Debug (scripts/debug_poison.py): fill every CU's LDS and every SIMD's register
     file with a NaN pattern, so the next kernel sees poison wherever it reads on-chip
     state it did not write itself."""
+    from .native import hip_debug
     if lds:
-        _hip_mod().poison_lds(pat, 256 * 8, _stream())
+        hip_debug().poison_lds(pat, 256 * 8, _stream())
     if regs:
-        _hip_mod().poison_regs(256 * 4 * 8, _stream())
+        hip_debug().poison_regs(256 * 4 * 8, _stream())
 
 
 def copy_to_host(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:

@@ -60,6 +60,12 @@ def hip():
         raise NativeUnavailable(f"HIP extension unavailable: {e}") from e
 
 
+def hip_debug():
+    """The diagnostic kernels (csrc/hip_debug), built on first use."""
+    from .build import build_hip_debug
+    return _load("_hip_debug", build_hip_debug)
+
+
 def hip_available() -> bool:
     try:
         hip()

@@ -198,11 +198,12 @@ def reform(ctx: DistContext, settle_s: float = 2.0, timeout_s: float = 60.0) -> 
 
 
 def barrier(ctx: DistContext) -> None:
+    """Host barrier over the gloo group (beside an RCCL default group too): it orders
+    the ranks' host threads, which is all the callers need (they synchronise their own
+    device around it), and it never makes torch create a ProcessGroupNCCL communicator
+    of its own next to the pipeline's stream-ordered ones (parallel/rccl.py)."""
     if ctx.initialized:
-        if ctx.backend == "nccl":
-            dist.barrier(device_ids=[ctx.device.index])
-        else:
-            dist.barrier()
+        dist.barrier(group=ctx.cpu_group)
 
 
 class PeerLost(RuntimeError):

@@ -9,8 +9,12 @@ the same per-step work on ``B`` frames:
                     RCCL-scatters B frames to each rank over xGMI (north-star X1).
   compute  ``Engine.run_device`` — hipGraph replay of preprocess -> model ->
            upsample/argmax -> contour statistics -> packed per-frame records.
-  collect  RCCL gather of the packed records (1 + 5*K floats per frame, ~1.3 KB
-           at K = 64) to rank 0 (X2), one D2H copy, push into the result hub.
+  collect  the packed records (1 + 5*K floats per frame, ~1.3 KB at K = 64) plus
+           frame metadata to rank 0, then one push into the result hub; either an
+           ncclGather of one packed device row per frame on the result stream (X2,
+           ``gather="rccl"``: bench.py's choice at N > 1 on GPUs) or, from pinned host
+           memory, a gloo gather (``gather="host"``: the serving default, where a dead
+           peer must not leave a collective kernel on the survivors' streams).
 
 Bucket sizing for xGMI: the frame scatter moves B x Hc x Wc x 3 bytes per peer
 (e.g. 32 x 640 x 480 x 3 = 29.5 MB), one message per peer over its own link; the
@@ -117,13 +121,12 @@ class DataParallelPipeline:
             tests/test_distributed.py::test_gloo_record_gather_cost_world8).
           * ``rccl``: RCCL gather of [records | metadata] rows (one send buffer, one
             collective) to rank 0's GPU on the result stream, then one D2H there (the X2
-            collective of SURVEY.md §2.5). The communicator is created lazily by the first
-            gather, after the engine's streams exist (eager creation shifted the engine's
-            streams onto a worse hardware-queue mapping: 17.6k vs 21.4k frames/s at world
-            size 1). Measured at world size 1 it costs GPU time the host path does not:
-            30.2-30.6k vs 33.8-33.9k frames/s (profiles/r4_rccl_gather_ab.txt), so it is
-            opt-in; RCCL carries the frame scatter (``ingest="scatter"``), where the
-            payload (B x 921.6 KB per peer) belongs on xGMI."""
+            collective of SURVEY.md §2.5), through the pipeline's own communicator
+            (parallel/rccl.py), created after the engine's streams exist (eager creation
+            shifted the engine's streams onto a worse hardware-queue mapping: 17.6k vs
+            21.4k frames/s at world size 1). Measured at world size 1 it costs 1.2-2.5 %
+            (profiles/r5f_rccl_world1_ab.txt). RCCL also carries the frame scatter
+            (``ingest="scatter"``, 3.2-4.5 % at world size 1)."""
         if gather == "auto":
             gather = "host"
         if gather not in ("host", "rccl"):
@@ -255,6 +258,11 @@ class DataParallelPipeline:
         if self.cuda and hasattr(engine, "bind_inputs"):
             if getattr(engine, "slot_parallel", False):
                 self._prime(int(os.environ.get("SSA_PIPE_PRIME", str(8 * self.nslots))))
+
+    def rccl_nranks(self) -> Optional[int]:
+        """Ranks in the pipeline's RCCL communicator (``ncclCommCount``), None without one."""
+        c = self._gcomm if self._gcomm is not None else (self._scomms[0] if self._scomms else None)
+        return None if c is None else c.nranks
 
     def close(self, abort: bool = False) -> None:
         """Release the pipeline's RCCL communicators (``abort``: a peer is gone -- do not

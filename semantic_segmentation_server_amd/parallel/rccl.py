@@ -3,9 +3,11 @@
 Why not ``torch.distributed`` for the data path: ProcessGroupNCCL runs every collective
 on ONE internal stream per device and fences it against the issuing stream with events.
 The serving pipeline keeps three steps in flight on three slot streams (plus a result
-stream) and HIP maps a process's streams onto 4 hardware queues. Round 4 measured what
-that costs at world size 1 (profiles/r4_rccl_gather_ab.txt): the record gather -10 %,
-the frame scatter -25 %, for ~9 us of actual GPU work per step -- the collectives of all
+stream) and HIP maps a process's streams onto 4 hardware queues. Through
+torch.distributed at world size 1 the record gather cost 6-10 % and the frame scatter
+up to 25 % (profiles/r4_rccl_gather_ab.txt, r5f_rccl_world1_ab.txt), for ~9 us of actual
+GPU work per step; through these stream-ordered communicators the gather costs 1.2-2.5 %
+and the scatter 3.2-4.5 % (r5f_rccl_world1_ab.txt). On the torch path the collectives of all
 three slots funnel through the one internal stream (each slot's scatter waits behind the
 previous slot's gather, which waits for that slot's post-processing), and the lazily
 created internal stream lands on a hardware queue that one of the slot streams already
@@ -65,6 +67,7 @@ def lib():
         for fn in ("ncclScatter", "ncclGather"):
             getattr(L, fn).argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.ncclCommCount.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
         L.ncclCommDestroy.argtypes = [ctypes.c_void_p]
         L.ncclCommAbort.argtypes = [ctypes.c_void_p]
         L.ncclCommGetAsyncError.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
@@ -85,19 +88,41 @@ def available() -> bool:
         return False
 
 
+def uid_bytes(uid: _UniqueId) -> bytes:
+    """The id's raw 128 bytes. NOT ``bytes(uid.internal)``: a ``c_char`` array field reads
+    (and assigns) as a NUL-terminated string, and the id holds NULs -- an 8-byte magic,
+    then the root's sockaddr, whose family field is ``02 00`` -- so the root's address and
+    port would arrive zeroed on the other ranks."""
+    return ctypes.string_at(ctypes.addressof(uid), ctypes.sizeof(uid))
+
+
+def uid_from_bytes(raw: bytes) -> _UniqueId:
+    if len(raw) != ctypes.sizeof(_UniqueId):
+        raise ValueError(f"ncclUniqueId must be {ctypes.sizeof(_UniqueId)} bytes, got {len(raw)}")
+    uid = _UniqueId()
+    ctypes.memmove(ctypes.addressof(uid), raw, len(raw))
+    return uid
+
+
+def share_uid(ctx, uid: Optional[_UniqueId]) -> _UniqueId:
+    """Rank 0's id on every rank, byte for byte, over the host (gloo) group."""
+    if ctx.world == 1:
+        return uid
+    import torch.distributed as dist
+    obj = [uid_bytes(uid) if ctx.rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=ctx.cpu_group)
+    return uid if ctx.rank == 0 else uid_from_bytes(obj[0])
+
+
 class StreamComm:
     """One RCCL communicator over the ranks of ``ctx``; collectives on a given stream."""
 
     def __init__(self, ctx, tag: str = "slot"):
-        import torch.distributed as dist
         L = lib()
         uid = _UniqueId()
         if ctx.rank == 0:
             _check(L.ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
-        if ctx.world > 1:
-            obj = [bytes(uid.internal) if ctx.rank == 0 else None]
-            dist.broadcast_object_list(obj, src=0, group=ctx.cpu_group)
-            uid.internal = obj[0]
+        uid = share_uid(ctx, uid)
         self.world, self.rank = ctx.world, ctx.rank
         self.device = ctx.device
         self.comm = ctypes.c_void_p()
@@ -105,6 +130,13 @@ class StreamComm:
             _check(L.ncclCommInitRank(ctypes.byref(self.comm), ctx.world, uid, ctx.rank),
                    f"ncclCommInitRank({tag})")
         self.alive = True
+        n = ctypes.c_int(0)
+        _check(L.ncclCommCount(self.comm, ctypes.byref(n)), "ncclCommCount")
+        # the communicator's own view of the group size (bench.py reports it: proof of how
+        # many ranks RCCL actually joined)
+        self.nranks = int(n.value)
+        if self.nranks != ctx.world:
+            raise RcclError(f"ncclCommCount({tag}) = {self.nranks}, expected {ctx.world}")
 
     @staticmethod
     def _stream(stream: Optional[torch.cuda.Stream]) -> ctypes.c_void_p:

@@ -7,9 +7,10 @@ Every rank owns ``--streams`` frame sources (global stream id = launch rank * S 
 one engine on its GPU. Each rank's loop is the measured pipeline (``runtime/driver.py``):
 a feeder thread fills a ring of pinned batches, ``DataParallelPipeline`` (lag 1, bound
 per-slot hipGraphs, post-processing on its own stream) runs the step and gathers the
-packed records plus frame metadata to rank 0 -- by default from pinned host memory over
-gloo (a latency-bound ~41 KB per rank and step that the host thread's slack absorbs;
-``--gather rccl``: one RCCL gather of a packed device row) -- which pushes them into the
+packed records plus frame metadata to rank 0 -- with P-1 degradation on (the default)
+from pinned host memory over gloo (a latency-bound ~41 KB per rank and step that the
+host thread's slack absorbs); with ``--no_degrade`` or ``--gather rccl`` as one RCCL
+gather of a packed device row on the result stream -- which pushes them into the
 per-stream result hub behind the v1/v2 services. With ``--ingest scatter`` rank 0 owns
 the sources for the whole node and scatters frames over RCCL (xGMI) and their metadata
 over gloo instead. The per-step heartbeat is a gloo all-reduce of a host flag. (The CLI
@@ -68,8 +69,11 @@ class DistributedServer:
         # the group is re-formed; --no_degrade (or --gather rccl) keeps the
         # RCCL data path, which bench.py measures. The pipeline's completion wait polls
         # for a peer's abort key on that path, so a lost peer still surfaces as PeerLost.
-        # (auto = host at any world size: the RCCL gather costs GPU time, see dp.py)
-        self.gather = "host" if cfg.gather == "auto" else cfg.gather
+        # auto: RCCL (xGMI) on GPUs at N > 1 with --no_degrade, else the host gather
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.gather = cfg.gather if cfg.gather != "auto" else (
+            "rccl" if gpu and world > 1 and not cfg.degrade
+            and os.environ.get("SSA_SHARE_GPU", "0") != "1" else "host")
         # SSA_SHARE_GPU=1 (several ranks on one GPU, a rehearsal): RCCL refuses that, gloo
         share = os.environ.get("SSA_SHARE_GPU", "0") == "1"
         if share and cfg.ingest == "scatter":

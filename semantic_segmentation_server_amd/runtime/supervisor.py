@@ -31,10 +31,14 @@ inside a write cannot leave a lock held or half a message behind for its success
   monitor.
 
 Restart policy: a worker that exits non-zero, goes stale (no step for
-``heartbeat_timeout_s`` once up), or does not come up within ``startup_timeout_s`` is
+``heartbeat_timeout_s`` after its first step), or has not completed its first step
+within ``startup_timeout_s`` (lazy plan build and autotune, hipGraph capture, priming
+steps and the first camera frame all come before it) is
 killed and replaced by a FRESH child process (never an exec of the faulted one), with
 exponential backoff, at most ``max_restarts`` times per ``restart_window_s`` (per rank).
-Health is SERVING while every rank is up; the v2 Health RPC reports ranks alive / total;
+Health is SERVING while at least one rank is up (a rank that restarts or gave up costs
+only its own streams: the others keep serving, and the detail says "degraded: up/total");
+the v2 Health RPC reports ranks alive / total;
 ``worker_restarts`` counts the restarts. Records already in the hub keep being served
 throughout. All workers exiting 0 (end of stream) ends the server, as in the reference.
 
@@ -47,7 +51,8 @@ record gather and the P-1 group re-form.
 Fault injection (tests): ``--inject_fault worker:N`` makes the first incarnation of every
 worker exit abruptly (``os._exit``, like a crashed process) after N steps;
 ``worker:R:N`` only rank R's; ``hang:R:N`` makes rank R's producer stop stepping after N
-steps while its process stays alive (a hung GPU).
+steps while its process stays alive (a hung GPU); ``slowstart:R:S`` delays rank R's
+first step by S seconds (a cold plan autotune or graph capture after "up").
 """
 from __future__ import annotations
 
@@ -182,8 +187,8 @@ def _fault_for(spec: Optional[str], rank: int, incarnation: int):
     parts = spec.split(":")
     if parts[0] == "worker" and len(parts) == 2:
         return "crash", int(parts[1])
-    if parts[0] in ("worker", "hang") and len(parts) == 3 and int(parts[1]) == rank:
-        return ("crash" if parts[0] == "worker" else "hang"), int(parts[2])
+    if parts[0] in ("worker", "hang", "slowstart") and len(parts) == 3 and int(parts[1]) == rank:
+        return {"worker": "crash"}.get(parts[0], parts[0]), float(parts[2])
     return None
 
 
@@ -223,6 +228,8 @@ def _worker_main(cfg: Config, rank: int, ring_name: str, q, stop_evt, incarnatio
 
     prod.on_step = on_step
     q.put(("up", rank, incarnation, f"{engine.backend} {engine.device}"))
+    if fault is not None and fault[0] == "slowstart":
+        time.sleep(fault[1])  # a first step that takes long (cold autotune, graph capture)
     prod.start()
     last_snap = 0.0
     while prod.is_alive():
@@ -267,7 +274,9 @@ class _Worker:
         self.error: Optional[str] = None
         self.restarts: List[float] = []
         self.restart_at: Optional[float] = None
+        self.first_step = False  # the current incarnation has completed a step
         self.snap: dict = {}
+        self.base: dict = {}  # counters of the retired incarnations (added to snap's)
 
 
 class SupervisedServer:
@@ -347,17 +356,25 @@ class SupervisedServer:
         w.proc.start()
         w.started = time.time()
         w.progress_seen = w.started
+        w.first_step = False
         w.restart_at = None
         log.info("worker %d incarnation %d started (pid %d)", w.rank, w.incarnation, w.proc.pid)
 
     def _health(self):
+        """SERVING while any rank is up: a lost rank degrades the server (its streams
+        pause) but the others keep serving."""
         up = sum(1 for w in self.workers if w.up and not self._stale(w))
-        ok = up == self.nw
-        detail = "ok" if ok else (self.error or f"{up}/{self.nw} workers up")
+        ok = up > 0
+        if up == self.nw:
+            detail = "ok"
+        else:
+            detail = f"degraded: {up}/{self.nw} workers up" + (f"; {self.error}" if self.error else "")
         return ok, up, self.nw, detail
 
     def _stale(self, w: _Worker) -> bool:
-        return w.up and time.time() - w.progress_seen > self.heartbeat_timeout_s
+        """No step for heartbeat_timeout_s -- counted only after the incarnation's first
+        step; until then the startup deadline applies."""
+        return w.up and w.first_step and time.time() - w.progress_seen > self.heartbeat_timeout_s
 
     def _pull(self, w: _Worker) -> None:
         if w.ring is None:
@@ -369,6 +386,9 @@ class SupervisedServer:
         st = w.ring.steps
         if st != w.steps:
             w.steps = st
+            w.progress_seen = time.time()
+        if st > 0 and not w.first_step:
+            w.first_step = True
             w.progress_seen = time.time()
 
     def _drain(self, w: _Worker) -> None:
@@ -412,6 +432,9 @@ class SupervisedServer:
                     ext[f"worker_{k}" if self.nw == 1 else f"worker{w.rank}_{k}"] = v
                 elif isinstance(v, (int, float)) and k not in ("uptime_s", "fps"):
                     ext[f"worker_{k}"] = ext.get(f"worker_{k}", 0.0) + float(v)
+            # retired incarnations' counters: totals never go backwards across a restart
+            for k, v in w.base.items():
+                ext[f"worker_{k}"] = ext.get(f"worker_{k}", 0.0) + v
         with self.metrics._lock:
             self.metrics.external = ext
 
@@ -421,6 +444,12 @@ class SupervisedServer:
             w.proc.join(timeout=10)
         self._pull(w)
         self._drain(w)
+        for k, v in (w.snap or {}).items():  # fold the incarnation's counters into the base
+            if isinstance(v, (int, float)) and not isinstance(v, bool) and k not in ("uptime_s", "fps"):
+                w.base[k] = w.base.get(k, 0.0) + float(v)
+        # the histogram summaries stay until the next incarnation sends its own
+        w.snap = {k: v for k, v in (w.snap or {}).items() if isinstance(v, dict)}
+        self._merge_snapshots()
         if w.ring is not None:
             dropped = w.ring.drops
             if dropped:
@@ -449,11 +478,11 @@ class SupervisedServer:
         p = w.proc
         now = time.time()
         stale = self._stale(w)
-        no_start = not w.up and now - w.started > self.startup_timeout_s
+        no_start = not (w.up and w.first_step) and now - w.started > self.startup_timeout_s
         if p.is_alive() and not stale and not no_start:
             return
         if p.is_alive():
-            why = "stopped making progress" if stale else "did not come up"
+            why = "stopped making progress" if stale else "did not complete a first step"
             log.error("worker %d incarnation %d %s; killing it", w.rank, w.incarnation, why)
             w.error = f"worker {w.rank}.{w.incarnation} {why}"
             p.kill()

@@ -375,3 +375,46 @@ def test_gloo_record_gather_cost_world8():
     # only a sanity bound applies
     bound = 0.7e-3 if (os.cpu_count() or 1) >= 2 * world else 10e-3
     assert p50 < bound, p50
+
+
+def test_rccl_uid_bytes_roundtrip_with_nuls():
+    """an ncclUniqueId holds NUL bytes (magic, then a sockaddr whose
+    family field is 02 00); reading or assigning the c_char field truncates at the first
+    NUL. The raw-bytes path must keep all 128 bytes."""
+    from semantic_segmentation_server_amd.parallel import rccl
+    raw = bytes([0x4e, 0x43, 0, 0, 0x12, 0, 0, 0, 2, 0, 0x75, 0x31, 127, 0, 0, 1]) + \
+        bytes((i * 37) % 256 for i in range(112))
+    uid = rccl.uid_from_bytes(raw)
+    assert rccl.uid_bytes(uid) == raw
+    assert len(bytes(uid.internal)) < len(raw)  # the truncating accessor this path avoids
+    with pytest.raises(ValueError):
+        rccl.uid_from_bytes(raw[:64])
+
+
+def _uid_worker(rank, world, port, raw, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from semantic_segmentation_server_amd.parallel import dist as D
+    from semantic_segmentation_server_amd.parallel import rccl
+    ctx = D.init("gloo")
+    uid = rccl.uid_from_bytes(raw) if rank == 0 else rccl._UniqueId()
+    got = rccl.share_uid(ctx, uid)
+    q.put((rank, rccl.uid_bytes(got)))
+    D.barrier(ctx)
+    D.destroy(ctx)
+
+
+def test_rccl_uid_broadcast_world3():
+    """The id rank 0 made reaches every rank byte for byte over the host group."""
+    raw = bytes([0, 0, 0, 0, 2, 0, 0x75, 0x31]) + bytes(range(1, 121))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_uid_worker, args=(r, 3, port, raw, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(3))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(got[r] == raw for r in range(3))

@@ -124,3 +124,42 @@ def test_hung_worker_is_detected_by_progress_and_replaced():
         assert sup.workers[0].incarnation == 0
     finally:
         sup.stop(0)
+
+
+def test_slow_first_step_is_not_stale():
+    """the progress deadline starts at the incarnation's first step. A first
+    step that takes longer than heartbeat_timeout_s (cold autotune, graph capture) is
+    under the startup deadline, so the worker is not killed."""
+    sup = SupervisedServer(_cfg(inject_fault="slowstart:0:4"), heartbeat_timeout_s=1.5,
+                           startup_timeout_s=120.0).start()
+    try:
+        t_end = time.time() + 240
+        assert _wait(lambda: sup.worker_steps >= 3, t_end), sup.error
+        assert sup.incarnation == 0 and sup.metrics.counters.get("worker_restarts", 0) == 0
+    finally:
+        sup.stop(0)
+
+
+def test_counters_survive_a_restart_and_health_degrades():
+    """Retired incarnations' counters stay in the totals (they never go backwards), and a
+    rank that is down leaves the server SERVING but degraded while another rank is up."""
+    from semantic_segmentation_server_amd.runtime.supervisor import _Worker
+    from semantic_segmentation_server_amd.utils.metrics import Metrics
+    sup = SupervisedServer.__new__(SupervisedServer)
+    sup.nw, sup.metrics, sup.heartbeat_timeout_s = 2, Metrics(), 60.0
+    sup.workers = [_Worker(0), _Worker(1)]
+    for w in sup.workers:
+        w.up, w.first_step, w.progress_seen = True, True, time.time()
+    sup.workers[0].snap = {"frames": 100.0, "step_ms": {"p50": 1.0}}
+    sup.workers[1].snap = {"frames": 50.0}
+    sup._merge_snapshots()
+    assert sup.metrics.snapshot()["worker_frames"] == 150.0
+    w0 = sup.workers[0]
+    sup._retire(w0)                      # incarnation 0 ends after 100 frames
+    w0.snap = {"frames": 7.0}            # the fresh incarnation starts from zero
+    sup._merge_snapshots()
+    assert sup.metrics.snapshot()["worker_frames"] == 157.0
+    ok, up, total, detail = sup._health()
+    assert ok and (up, total) == (1, 2) and detail.startswith("degraded: 1/2")
+    sup.workers[1].up = False
+    assert not sup._health()[0]
