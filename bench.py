@@ -299,6 +299,7 @@ def main() -> int:
             "host_ms_per_step": host_ms,
         }
         print(json.dumps(out), flush=True)
+    pipe.close()  # the pipeline's RCCL communicators, before the process group
     D.destroy(ctx)
     return 0
 

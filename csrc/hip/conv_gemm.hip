@@ -478,6 +478,9 @@ static int pick_nt(int Cout);
 // the buffer descriptor's range check, so the LDS image is always fully written.
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
+// the in-launch split-K combine's compile-time bound on ks (conv_gemm_grouped checks it)
+constexpr int kInlineKS = 8;
+
 // One BM x BN output tile (tile index bid in row-major (m-tile, n-tile) order) of
 // the LDS-DMA conv GEMM; shared by the single-conv kernel and the grouped kernel.
 // BK: K depth of one stage (64: 128-byte rows, 8 per glds; 32: 64-byte rows, 16 per
@@ -691,7 +694,15 @@ __device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char
           if (m < 0) continue;
           const float* q = part + (size_t)m * a.ldo + a.co_off + n;
           f32x4 v = *reinterpret_cast<const f32x4*>(a.bias + n);
-          for (int sl = 0; sl < ks; ++sl) v += *reinterpret_cast<const f32x4*>(q + sl * slab);
+          // every slice's load issued before the first add (one L2 round trip, not ks
+          // dependent ones); slices past ks re-read the last one and are not added
+          f32x4 pv[kInlineKS];
+#pragma unroll
+          for (int sl = 0; sl < kInlineKS; ++sl)
+            pv[sl] = *reinterpret_cast<const f32x4*>(q + (size_t)(sl < ks ? sl : ks - 1) * slab);
+#pragma unroll
+          for (int sl = 0; sl < kInlineKS; ++sl)
+            if (sl < ks) v += pv[sl];
           bf16x4 o;
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = (bf16)apply_act(v[e], a.act);
@@ -969,6 +980,8 @@ void conv_gemm_grouped(const ConvParams* ps, int n, const int* order, int nblock
     for (int i = 0; i < n; ++i)
       if (ps[i].ldo != ps[0].ldo || ps[i].Cout % 4 || (ps[i].ldo | ps[i].co_off) % 4)
         throw std::invalid_argument("conv_gemm_grouped: split-K needs one ldo and 4-aligned channels");
+  if (ks > kInlineKS && cnt != nullptr)
+    throw std::invalid_argument("conv_gemm_grouped: the in-launch combine takes ks <= 8");
   ConvGroupArgs ga{};
   ga.ks = ks;
   ga.part = ks > 1 ? part : nullptr;

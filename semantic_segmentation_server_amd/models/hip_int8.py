@@ -96,6 +96,9 @@ class HipDeepLabInt8:
         self.logits_p = pack_int8(model.logits, S["aspp.proj"], dev)
         self._plans: Dict[tuple, Tuple[List[Callable], Dict[str, torch.Tensor]]] = {}
         self._labels_out: Optional[torch.Tensor] = None  # segment(out=): caller's label maps
+        self.kind = "resnet50_int8"  # tune-file key prefix
+        self.pick_sync = None  # set by the DP pipeline: rank 0's picks on every rank
+        self.choices: Dict[str, str] = {}
 
     def _plan(self, B: int, Hc: int, Wc: int, part: int = 0):
         """``part`` > 0: an independent copy of the plan (own buffers, part 0's picks) for
@@ -106,6 +109,7 @@ class HipDeepLabInt8:
         dev, S = self.device, self.scales
         bufs: Dict[str, torch.Tensor] = {}
         ops: List[Callable] = []
+        I8.n = 0  # conv choices named i8conv1.. by position: stable keys for the tune file
 
         def buf(name, *shape, dtype=torch.int8):
             t = torch.zeros(shape, dtype=dtype, device=dev)  # plan copies start identical
@@ -232,31 +236,18 @@ class HipDeepLabInt8:
         ch.desc = f"M={B * h * w} Cin={c} Cout={A} x {len(convs)} branches"
         return ch
 
+    def _tune_inputs(self, B: int, Hc: int, Wc: int):
+        from .hip_model import HipDeepLab
+        return HipDeepLab._tune_inputs(self, B, Hc, Wc)
+
     def _autotune(self, ops, B, Hc, Wc) -> None:
-        """Time each int8 conv's kernel variants on the plan's real buffers, keep the fastest.
-        Inputs: synthetic camera frames through the real letterbox LUTs (HipDeepLab's); with
-        all-zero LUTs every stem gather hit one cached camera pixel and the stem variants
-        were timed on a degenerate path."""
-        from .hip_model import Choice, HipDeepLab
-        if torch.cuda.is_current_stream_capturing():
-            return
-        dev = self.device
-        frames, lx, ly = HipDeepLab._tune_inputs(self, B, Hc, Wc)
-        for op in ops:  # populate every buffer once
-            op(frames, lx, ly)
-        for op in ops:
-            if isinstance(op, Choice):
-                op.autotune((frames, lx, ly), reps=3)
-        torch.cuda.synchronize(dev)
-        self.choices = {op.name: op.variants[op.pick][0] for op in ops if isinstance(op, Choice)}
-        import os
-        if os.environ.get("SSA_LOG_AUTOTUNE", "0") == "1":
-            import sys
-            for op in ops:
-                if isinstance(op, Choice) and hasattr(op, "times"):
-                    print(f"[autotune int8 B={B}] {op.name} {getattr(op, 'desc', '')}: " + ", ".join(
-                        f"{n}={t * 1e3:.1f}us" for (n, _), t in zip(op.variants, op.times)) +
-                        f" -> {op.variants[op.pick][0]}", file=sys.stderr)
+        """The bf16 model's plan tuning (hip_model.HipDeepLab._autotune): picks from the
+        committed tune file (key ``resnet50_int8:B=..:cam=..:in=..``) when it has this
+        shape, else timed on synthetic frames through the real letterbox LUTs -- on rank 0
+        only under the DP pipeline's ``pick_sync``, so every rank runs the same kernels (the
+        int8 variants differ by up to one requantisation step) and no rank tunes cold."""
+        from .hip_model import HipDeepLab
+        HipDeepLab._autotune(self, ops, B, Hc, Wc)
 
     def _block(self, ops, buf, i, d, x, B, h, w, c):
         S = self.scales

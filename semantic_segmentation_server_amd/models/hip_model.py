@@ -507,11 +507,12 @@ class HipDeepLab:
         labels = buf("labels", B, H, W, dtype=torch.uint8)
         # labels_out (segment's out=): write the label maps straight into a caller
         # buffer (the engine's per-slot maps) instead of the plan's static one
-        # upsample + argmax: row-block (LDS-staged, coalesced stores) or per-lane stores
+        # upsample + argmax: row-block (LDS-staged, coalesced stores), per-lane stores, or
+        # cell-bound class pruning (one workgroup per source row interval)
         ops.append(Choice("upsample", [(name, [lambda *_, h=h, w=w, v=K.UPSAMPLE_VARIANTS[name]:
                                                K.upsample_argmax(
             logits, self._labels_out if self._labels_out is not None else labels, B=B, h=h, w=w,
-            K=self.num_classes, ldk=self.ldk, H=H, W=W, variant=v)]) for name in ("rows", "lane")]))
+            K=self.num_classes, ldk=self.ldk, H=H, W=W, variant=v)]) for name in ("rows", "lane", "cell")]))
         self._plans[key] = (ops, bufs)
         if part == 0:
             self._autotune(ops, B, Hc, Wc)
@@ -582,6 +583,12 @@ class HipDeepLab:
                 elif op in choices and len(op.variants) > 1:
                     op.autotune(args)  # a variant set the saved plan does not know: time it
                     retimed = True
+            if retimed and self.pick_sync is not None:
+                # (every rank reads the same file, so every rank re-timed the same choices:
+                # the broadcast is collective) rank 0's timings decide, as in a cold tune
+                picks = self.pick_sync({op.name: op.pick for op in every} if rank0 else None)
+                for op in every:
+                    op.pick = picks.get(op.name, op.pick)
         else:
             if self.pick_sync is None or rank0:
                 for op in choices:

@@ -448,15 +448,24 @@ def test_aspp_pool(B, h, w, C, N):
     assert _rel(ib.cpu(), ref) < 1e-4
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("h,H,K", [(33, 513, 21), (65, 1025, 19), (9, 65, 21), (33, 257, 30)])
-def test_upsample_argmax(h, H, K, variant):
+@pytest.mark.parametrize("field", ["noise", "smooth"])
+def test_upsample_argmax(h, H, K, variant, field):
+    """``smooth``: a coarse random field upsampled to h x h (large regions: the cell-bound
+    variant's single-survivor path); ``noise``: i.i.d. logits (most cells keep several
+    classes)."""
     from semantic_segmentation_server_amd.ops import reference_ops as R
     Kh = _hip()
     g = torch.Generator().manual_seed(7)
     B = 2
     ldk = (K + 7) // 8 * 8
-    logits = torch.randn(B, h, h, ldk, generator=g).to(torch.bfloat16)
+    if field == "noise":
+        logits = torch.randn(B, h, h, ldk, generator=g).to(torch.bfloat16)
+    else:
+        coarse = torch.randn(B, ldk, 4, 4, generator=g) * 4
+        logits = F.interpolate(coarse, size=(h, h), mode="bilinear", align_corners=True) \
+            .permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
     ref = R.upsample_argmax(_nchw(logits[..., :K]).float(), H, H)
     out = torch.empty(B, H, H, dtype=torch.uint8, device=DEV)
     Kh.upsample_argmax(logits.to(DEV), out, B=B, h=h, w=h, K=K, ldk=ldk, H=H, W=H,
@@ -1454,6 +1463,50 @@ def test_int8_resnet50_matches_fake_quant():
     assert e_fp < 0.15
     agree = (got.argmax(1) == fp.argmax(1)).float().mean().item()
     assert agree > 0.95, agree
+
+
+def test_int8_resnet50_headline_shape():
+    """BASELINE config 4 as benchmarked: DeepLabv3-ResNet50 1025^2, B = 8, 2048x1024
+    camera, the engine's own model / calibration and the COMMITTED plan
+    (assets/tune_mi355x.json) -- the 160x128 LDS-DMA tiles, streaming 1x1 / 3x3 kernels
+    and the grouped ASPP at the grids that produce the bench number -- against the fp32
+    fake-quant replay of the same int8 arithmetic. Reruns of the plan are
+    bit-identical."""
+    import json
+    from semantic_segmentation_server_amd import config as C
+    from semantic_segmentation_server_amd.models.hip_model import TUNE_FILE_DEFAULT
+    from semantic_segmentation_server_amd.models.quant import fake_quant_forward
+    from semantic_segmentation_server_amd.ops import reference_ops as R
+    from semantic_segmentation_server_amd.runtime.engine import Engine
+    from semantic_segmentation_server_amd.runtime.sources import SyntheticSource
+    B, S, cw, ch = 8, 1025, 2048, 1024
+    key = f"resnet50_int8:B={B}:cam={cw}x{ch}:in={S}"
+    saved = json.load(open(TUNE_FILE_DEFAULT))
+    assert key in saved, "config 4 has no committed plan"
+    cfg = C.Config(arch="resnet50", dtype="int8", input_size=S, batch=B, backend="hip", graph=False,
+                   num_classes=19, dataset="cityscapes", camera_width=cw, camera_height=ch)
+    eng = Engine(cfg, torch.device(DEV))
+    eng.set_camera(cw, ch)
+    hm = eng._hip_model
+    f, _, _ = SyntheticSource(cw, ch, pool=4, seed=21).read_batch(B)
+    frames = torch.from_numpy(np.ascontiguousarray(f)).to(DEV)
+    got = hm.logits(frames, eng.lut_x, eng.lut_y).clone()
+    again = hm.logits(frames, eng.lut_x, eng.lut_y)
+    torch.cuda.synchronize()
+    assert torch.equal(got, again), "int8 plan reruns differ"
+    assert all(saved[key].get(n) == v for n, v in hm.choices.items() if n in saved[key]), \
+        "the plan under test is not the committed one"
+    x = R.preprocess(frames.cpu(), eng.lut_x.cpu(), eng.lut_y.cpu()).to(DEV)
+    import copy
+    m32 = copy.deepcopy(eng.model).float().to(DEV)
+    ref = fake_quant_forward(m32, hm.scales, x).float()
+    got = _nchw(got.float())
+    e_fq = _rel(got.cpu(), ref.cpu())
+    d_agree, frac = R.decisive_agreement(got, ref)
+    print(f"int8 resnet50 1025^2 B={B}: rel err vs fake-quant {e_fq:.4f}; decisive pixels "
+          f"({frac:.3f} of all) agreement {d_agree:.4f}")
+    assert e_fq < 0.03, e_fq
+    assert frac >= 0.05 and d_agree >= 0.995, (frac, d_agree)
 
 
 def _records_equal(pa: torch.Tensor, pb: torch.Tensor) -> bool:
