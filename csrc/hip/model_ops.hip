@@ -860,6 +860,13 @@ __global__ __launch_bounds__(256) void upsample_argmax_kernel(const bf16* __rest
 // Per-lane state of the separable interval upsample: the two vertically interpolated
 // source columns j, j+1 (fp32, as v0 and dv = v1 - v0) of one output row, and the
 // output pixels [xs, xe) whose left source column is j.
+// wave-wide max of a per-lane int (a small loop bound made uniform)
+__device__ __forceinline__ int wave_max_int(int v) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) v = max(v, __shfl_xor(v, off));
+  return v;
+}
+
 template <int KP>
 struct Interval {
   float v0[KP], dv[KP];
@@ -930,6 +937,80 @@ struct Interval {
     return TAGGED ? 31 - (int)(__float_as_uint(best) & 31u) : arg;
   }
 
+  // Candidate pruning + class-major evaluation (variant 6). Along the interval each class
+  // score is linear in lx1, so it lies between its two end values: with L the best lower
+  // end, a class whose upper end is below L (minus a margin of 2^-12 of the largest end
+  // magnitude, far above the interpolation's rounding) can win at no pixel of the
+  // interval. A lane left with one candidate stores it; the others evaluate, pixel by pixel,
+  // only the classes that are a candidate of SOME lane of the wave (their union, uniform:
+  // a scalar branch skips every other class) -- class-major over NPX register-resident
+  // pixels, in ascending class order with a strict compare, so the label is the first
+  // maximum as in argmax_at. The per-pixel fallback of emit() evaluated all K classes at
+  // up to 14 pixels of every interval whose end winners differ (2,293 VALU per wave on the
+  // headline maps, r7x_headline_kernel_pmc.txt).
+  template <int NPX>
+  __device__ void emit_union(uint8_t* op, int K) const {
+    const int n = xe - xs;
+    const float t0 = lx(xs), t1 = lx(n > 0 ? xe - 1 : xs);
+    float hi[KP];
+    float L = -3.0e38f, M = 0.f;
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+      const float a = v0[k] + t0 * dv[k], b = v0[k] + t1 * dv[k];
+      const float lo = fminf(a, b);
+      hi[k] = fmaxf(a, b);
+      if (k < K) {
+        L = fmaxf(L, lo);
+        M = fmaxf(M, fmaxf(fabsf(a), fabsf(b)));
+      }
+    }
+    const float thr = L - (M * (1.f / 4096.f) + 1e-30f);
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < KP; ++k)
+      if (k < K && hi[k] >= thr) m |= 1u << k;
+    if (n <= 0) m = 0;
+    const bool single = (m & (m - 1)) == 0;
+    if (single && m) {
+      const uint8_t l = (uint8_t)(__ffs(m) - 1);
+      for (int X = xs; X < xe; ++X) op[X] = l;
+    }
+    // union over the lanes that still need per-pixel work (a wave-uniform value)
+    uint32_t u = single ? 0u : m;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) u |= (uint32_t)__shfl_xor((int)u, off);
+    u = __builtin_amdgcn_readfirstlane(u);
+    if (u == 0) return;
+    const int chunks = single ? 0 : (n + NPX - 1) / NPX;
+    const int nchunk = __builtin_amdgcn_readfirstlane(wave_max_int(chunks));
+    for (int c = 0; c < nchunk; ++c) {
+      const int X0 = xs + c * NPX;
+      float tx[NPX], best[NPX];
+      int arg[NPX];
+#pragma unroll
+      for (int e = 0; e < NPX; ++e) {
+        tx[e] = lx(X0 + e);
+        best[e] = -3.0e38f;
+        arg[e] = 0;
+      }
+#pragma unroll
+      for (int k = 0; k < KP; ++k) {
+        if (u & (1u << k)) {  // uniform: a scalar branch
+#pragma unroll
+          for (int e = 0; e < NPX; ++e) {
+            const float v = v0[k] + tx[e] * dv[k];
+            if (v > best[e]) { best[e] = v; arg[e] = k; }
+          }
+        }
+      }
+      if (c < chunks) {
+#pragma unroll
+        for (int e = 0; e < NPX; ++e)
+          if (X0 + e < xe) op[X0 + e] = (uint8_t)arg[e];
+      }
+    }
+  }
+
   // Along the interval every class score is LINEAR in lx1, and the max of linear
   // functions is convex: when one class wins at both end pixels it wins at every
   // pixel in between. The common case (smooth logits) then costs two argmaxes
@@ -974,6 +1055,24 @@ __global__ __launch_bounds__(256) void upsample_argmax_interval_kernel(
   iv.template emit<TAGGED>(labels + ((size_t)b * H + Y) * W, K);
 }
 
+// variant 6: emit_union (the wave-wide shuffles need every lane of the wave: lanes past the
+// end take an empty interval instead of returning)
+template <int KP>
+__global__ __launch_bounds__(256) void upsample_argmax_union_kernel(
+    const bf16* __restrict__ logits, uint8_t* __restrict__ labels, int B, int h, int w, int K,
+    int ldk, int H, int W) {
+  const int t0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = t0 < B * H * w;
+  const int t = live ? t0 : 0;
+  const int j = t % w;
+  const int Y = (t / w) % H;
+  const int b = t / (w * H);
+  Interval<KP> iv;
+  iv.load(logits, b, Y, j, h, w, H, W, ldk);
+  if (!live) iv.xe = iv.xs;
+  iv.template emit_union<16>(labels + ((size_t)b * H + Y) * W, K);
+}
+
 // Row-block variant: a workgroup owns R = 256 / w whole output rows (consecutive in the
 // B*H row space, so one contiguous R*W-byte run of the label buffer). Each lane
 // computes one interval as above into an LDS copy of the rows; the workgroup then
@@ -1013,140 +1112,17 @@ __global__ __launch_bounds__(256) void upsample_argmax_rows_kernel(
   if (tid < n - tail0) out[tail0 + tid] = rows_lds[tail0 + tid];
 }
 
-// Cell-bound variant: one workgroup = one frame x one source row interval [i, i+1], i.e.
-// the ~16 output rows whose upper source row (int)(sh * Y) is i -- one contiguous byte run
-// of the label buffer. Every bilinear interpolant of class c inside the source cell
-// (i, j) is a convex combination of its four corners, so it lies in [lo_c, hi_c] (their
-// min / max). With L = max_c lo_c, a class whose hi_c is below L can win NOWHERE in the
-// cell. Per cell (one lane each) the kernel keeps the classes that can still win; a cell
-// with one survivor (the common case: label maps are piecewise constant at 16 x 16
-// output pixels per cell) labels its ~256 output pixels with no per-pixel arithmetic,
-// the rest evaluate only the survivors, with the interval kernel's interpolation
-// (u = ly0 a0 + ly1 a1 per source column, v = u_j + lx1 (u_j1 - u_j)). A margin of
-// 2^-12 of the cell's largest corner magnitude keeps every class whose rounded
-// interpolant could come within a few ulps of the winner, so pruning never changes a strict-compare argmax. The workgroup
-// then writes its run with dword stores (4 consecutive bytes per lane).
-template <int KP>
-__global__ __launch_bounds__(256) void upsample_argmax_cell_kernel(
-    const bf16* __restrict__ logits, uint8_t* __restrict__ labels, int B, int h, int w, int K,
-    int ldk, int H, int W) {
-  constexpr int SK = KP + 1;  // LDS row pitch (floats): cell lanes read 33-word strides
-  extern __shared__ float cell_lds[];
-  float* R0 = cell_lds;                 // [w][SK] source row i (fp32)
-  float* R1 = cell_lds + w * SK;        // [w][SK] source row i1
-  uint32_t* cmask = reinterpret_cast<uint32_t*>(cell_lds + 2 * w * SK);  // [w]
-  uint8_t* clab = reinterpret_cast<uint8_t*>(cmask + w);                  // [w]
-  const int tid = threadIdx.x;
-  const int i = blockIdx.x % h;
-  const int b = blockIdx.x / h;
-  const int i1 = i < h - 1 ? i + 1 : i;
-  const float sh = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
-  const float sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
-  // output rows [Ys, Ye) with (int)(sh * Y) == i (exact fp32 formula, then fix-up)
-  int Ys = sh > 0.f ? (int)((float)i / sh) - 1 : 0;
-  if (Ys < 0) Ys = 0;
-  while (Ys > 0 && (int)(sh * (float)Ys) >= i) --Ys;
-  while (Ys < H && (int)(sh * (float)Ys) < i) ++Ys;
-  int Ye = Ys;
-  while (Ye < H && (int)(sh * (float)Ye) == i) ++Ye;
-  if (Ye == Ys) return;  // (uniform across the workgroup: before any barrier)
-  // ---- the two source rows, bf16 -> fp32 into LDS (8 channels per load)
-  const bf16* g0 = logits + ((size_t)(b * h + i) * w) * ldk;
-  const bf16* g1 = logits + ((size_t)(b * h + i1) * w) * ldk;
-  constexpr int K8 = KP / 8;
-  for (int q = tid; q < 2 * w * K8; q += 256) {
-    const int r = q / (w * K8), rem = q - r * (w * K8);
-    const int j = rem / K8, k8 = (rem - j * K8) * 8;
-    const bf16x8 v = ld8((r ? g1 : g0) + (size_t)j * ldk + k8);
-    float* d = (r ? R1 : R0) + j * SK + k8;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) d[e] = (float)v[e];
-  }
-  __syncthreads();
-  // ---- per cell: the classes that can still win
-  if (tid < w) {
-    const int j = tid, j1 = j < w - 1 ? j + 1 : j;
-    float hi[KP];
-    float L = -3.0e38f, M = 0.f;  // M: the largest corner magnitude (sets the rounding scale)
-#pragma unroll
-    for (int c = 0; c < KP; ++c) {
-      if (c < K) {
-        const float a = R0[j * SK + c], bb = R0[j1 * SK + c];
-        const float d = R1[j * SK + c], e = R1[j1 * SK + c];
-        const float lo = fminf(fminf(a, bb), fminf(d, e));
-        hi[c] = fmaxf(fmaxf(a, bb), fmaxf(d, e));
-        L = fmaxf(L, lo);
-        M = fmaxf(M, fmaxf(fabsf(lo), fabsf(hi[c])));
-      } else {
-        hi[c] = -3.0e38f;
-      }
-    }
-    const float thr = L - (M * (1.f / 4096.f) + 1e-30f);
-    uint32_t m = 0;
-#pragma unroll
-    for (int c = 0; c < KP; ++c)
-      if (c < K && hi[c] >= thr) m |= 1u << c;
-    cmask[j] = m;
-    clab[j] = (m & (m - 1)) == 0 ? (uint8_t)(__ffs(m) - 1) : (uint8_t)0xFF;
-  }
-  __syncthreads();
-  // ---- the run of output rows [Ys, Ye) of frame b
-  uint8_t* out = labels + ((size_t)b * H + Ys) * W;
-  const int n = (Ye - Ys) * W;
-  auto pixel = [&](int r, int X) -> uint32_t {
-    const int j = (int)(sw * (float)X);
-    const uint8_t l = clab[j];
-    if (l != 0xFF) return l;
-    const int j1 = j < w - 1 ? j + 1 : j;
-    const float lx1 = j < w - 1 ? sw * (float)X - (float)j : 0.f;
-    const float fy = sh * (float)(Ys + r);
-    const float ly1 = fy - (float)i, ly0 = 1.f - ly1;
-    uint32_t m = cmask[j];
-    float best = -3.0e38f;
-    int arg = 0;
-    while (m) {
-      const int c = __ffs(m) - 1;
-      m &= m - 1;
-      const float u = ly0 * R0[j * SK + c] + ly1 * R1[j * SK + c];
-      const float v = ly0 * R0[j1 * SK + c] + ly1 * R1[j1 * SK + c];
-      const float val = u + lx1 * (v - u);
-      if (val > best) { best = val; arg = c; }
-    }
-    return (uint32_t)arg;
-  };
-  const int head = (int)((4 - ((uintptr_t)out & 3)) & 3) < n ? (int)((4 - ((uintptr_t)out & 3)) & 3) : n;
-  if (tid < head) out[tid] = (uint8_t)pixel(0, tid);  // head < 4 <= W: row 0
-  const int nd = (n - head) >> 2;
-  uint32_t* outd = reinterpret_cast<uint32_t*>(out + head);
-  // byte p = head + 4 * d of the run is output row r = p / W, column X = p % W; a lane's
-  // next dword is 1024 bytes further: advance (r, X) incrementally (W >= 2)
-  int p = head + 4 * tid;
-  int r = p / W, X = p - r * W;
-  for (int d = tid; d < nd; d += 256) {
-    uint32_t word = 0;
-    int rr = r, xx = X;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      word |= pixel(rr, xx) << (8 * e);
-      if (++xx == W) { xx = 0; ++rr; }
-    }
-    outd[d] = word;
-    X += 1024;
-    while (X >= W) { X -= W; ++r; }
-  }
-  const int tail0 = head + 4 * nd;
-  if (tid < n - tail0) {
-    const int q = tail0 + tid;
-    out[q] = (uint8_t)pixel(q / W, q % W);
-  }
-}
-
 namespace {
 
 template <int KP>
 void launch_upsample_interval(int variant, const bf16* logits, uint8_t* labels, int B, int h,
                               int w, int K, int ldk, int H, int W, hipStream_t s) {
   const long long total = (long long)B * H * w;
+  if (variant == 6) {
+    hipLaunchKernelGGL((upsample_argmax_union_kernel<KP>), dim3(cdiv(total, 256)), dim3(256), 0, s,
+                       logits, labels, B, h, w, K, ldk, H, W);
+    return;
+  }
   if (variant == 1 || variant == 2) {
     if (variant == 1)
       hipLaunchKernelGGL((upsample_argmax_interval_kernel<KP, false>), dim3(cdiv(total, 256)),
@@ -1171,9 +1147,8 @@ void launch_upsample_interval(int variant, const bf16* logits, uint8_t* labels, 
 
 // variant: 0 = default (per-lane interval, strict-compare argmax), 1 = interval / compare,
 // 2 = interval / tagged max, 3 = row-block / compare, 4 = row-block / tagged max,
-// 5 = the direct (per-pixel gather) kernel, 6 = cell-bound (class pruning per source
-// cell). Variants 1-4 and 6 need the interval preconditions; otherwise the direct
-// kernel runs.
+// 5 = the direct (per-pixel gather) kernel, 6 = interval / wave-union candidates.
+// Variants 1-4 and 6 need the interval preconditions; otherwise the direct kernel runs.
 void upsample_argmax(const bf16* logits, uint8_t* labels, int B, int h, int w, int K, int ldk,
                      int H, int W, hipStream_t s, int variant) {
   if (K > 256) throw std::invalid_argument("upsample_argmax: K > 256");
@@ -1186,23 +1161,6 @@ void upsample_argmax(const bf16* logits, uint8_t* labels, int B, int h, int w, i
                         sw > 0.f && 1.f / sw <= 30.f && (long long)B * H * w < (1LL << 31);
   if (interval && (variant == 3 || variant == 4) && (w > 256 || (256 / w) * W > 65536))
     variant -= 2;
-  if (interval && variant == 6) {
-    const float sh = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
-    if (h >= 2 && H > 1 && sh > 0.f && 1.f / sh <= 30.f && w <= 256 && W >= 4 &&
-        (long long)B * h < (1LL << 31)) {
-      const int kp = K <= 24 ? 24 : 32;
-      const size_t lds = (size_t)2 * w * (kp + 1) * 4 + (size_t)w * 5;
-      if (kp == 24)
-        hipLaunchKernelGGL(upsample_argmax_cell_kernel<24>, dim3(B * h), dim3(256), lds, s, logits,
-                           labels, B, h, w, K, ldk, H, W);
-      else
-        hipLaunchKernelGGL(upsample_argmax_cell_kernel<32>, dim3(B * h), dim3(256), lds, s, logits,
-                           labels, B, h, w, K, ldk, H, W);
-      check_launch("upsample_argmax cell");
-      return;
-    }
-    variant = 1;
-  }
   if (interval && variant != 5) {
     if (K <= 24)
       launch_upsample_interval<24>(variant, logits, labels, B, h, w, K, ldk, H, W, s);

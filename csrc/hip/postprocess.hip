@@ -76,7 +76,7 @@ constexpr int kPoolPerFrame = 8192;  // root pool entries per frame of the batch
 
 // Workspace layout (round 5): per frame only what is per pixel (labels, mask,
 // compact index) plus the bounded merge inputs; everything per component lives in ONE pool
-// for the batch, indexed by label, of max(B * kPoolPerFrame, N + 1) entries. A frame's
+// for the batch, indexed by label, of max(B * kPoolPerFrame, N + 1) + N / 2 + 1 entries. A frame's
 // components take a contiguous run of it (k_ccl_merge: one atomicAdd of its component count;
 // fallback frames reserve their tile-local root count, an upper bound). The floor of N + 1
 // entries keeps any single frame exact (a frame has fewer components than pixels); a batch
@@ -98,7 +98,11 @@ Layout layout(int B, int H, int W, int K, int bins) {
   l.N = (size_t)H * W;
   l.K = K;
   l.bins = bins;
-  l.P = std::max((size_t)B * kPoolPerFrame, l.N + 1);
+  // + N / 2 + 1 beyond the shared part: with the floor, two frames of ANY content (a
+  // union-find fallback frame reserves its tile-local root count, at most ~N / 2: a
+  // checkerboard's 4-connected background) fit beside the batch's typical ones (ADVICE r5:
+  // two speckled frames in one batch could exhaust a pool of max(B * 8192, N + 1))
+  l.P = std::max((size_t)B * kPoolPerFrame, l.N + 1) + l.N / 2 + 1;
   l.ntiles = (size_t)((W + TW - 1) / TW) * ((H + TH - 1) / TH);
   // k_ccl_edges' unions at the largest crop: <= 3 per pixel of a tile top row, 2 of a tile
   // left column, 1 of a right column or of the image border

@@ -14,6 +14,7 @@
 #   b1lag1       batch-1 bench at lag 1
 #   cfg4         DeepLabv3-ResNet50 1025^2 int8 B=8 (60 steps) and bf16
 #   cfg5         4 camera streams x 8 frames (batched step)
+#   cfg5p        the same with one engine + HIP stream + hipGraph per camera stream
 #   prof         sequential kernel trace of the B=32 step -> layer_times.txt
 #   profb1       sequential kernel trace of the B=1 step -> b1_layer_times.txt
 #   profc4       config-4 (ResNet-50 1025^2 int8, B=8) kernel trace -> c4_roofline.txt
@@ -28,6 +29,9 @@
 #   postpmc      3 SQ counter passes over tools/bin/pb_prod on the bench model's label maps -> post_pmc.txt
 #   posttrace    post_bench (4 map kinds incl. the fallback-path lattice) under a kernel trace
 #   repro        packed-f32 co-residence reproducer, both builds (csrc/tools/packed_f32_repro.hip)
+#   tunec4       autotune config 4 (ResNet-50 1025^2 B=8, int8 and bf16) into $O/tune.json
+#   usetune      copy $O/tune.json over assets/tune_mi355x.json in the box's tree (then commit it here)
+#   upbench      upsample+argmax variant microbench (scripts/bench_upsample.py)
 #   retune:LIST  re-time the named choices (comma list) at B = ${TUNE_B:-32} on top of the committed
 #                picks -> $O/tune.json (copy into assets/tune_mi355x.json to commit)
 #   retuneall:B  re-time EVERY choice of the B-frame plan (SSA_RETUNE=1) -> $O/tune.json
@@ -81,6 +85,7 @@ for step in "$@"; do
     cfg4)    bench c4i8 400 --arch resnet50 --input_size 1025 --camera 2048x1024 --batch 8 --dtype int8 --steps 60 --warmup 5 --rpc 0 \
                && bench c4bf 400 --arch resnet50 --input_size 1025 --camera 2048x1024 --batch 8 --steps 60 --warmup 5 --rpc 0 || exit 2 ;;
     cfg5)    bench c5 300 --streams 4 --batch 32 --steps 100 --warmup 10 --rpc 0 || exit 2 ;;
+    cfg5p)   bench c5p 400 --streams 4 --batch 32 --per_stream_graphs --steps 100 --warmup 10 --rpc 0 || exit 2 ;;
     prof)    trace seq --steps 5 --warmup 2 || exit 3 ;;
     profb1)  trace b1seq --batch 1 --steps 20 --warmup 5 || exit 3 ;;
     profc4)  trace c4seq --arch resnet50 --input_size 1025 --camera 2048x1024 --batch 8 --dtype int8 --steps 5 --warmup 2 || exit 3
@@ -133,6 +138,15 @@ for step in "$@"; do
              head -12 $(ls $O/posttrace/*/run_kernel_stats.csv $O/posttrace/run_kernel_stats.csv 2>/dev/null | head -1) | cut -d, -f1-8 ;;
     repro)   for b in repro_pk repro_nopk; do timeout -k 10 300 tools/bin/$b ${REPRO_REPS:-400} > $O/$b.txt 2>&1 \
                || { tail -5 $O/$b.txt; exit 7; }; cat $O/$b.txt; done ;;
+    tunec4)  [ -f $O/tune.json ] || cp assets/tune_mi355x.json $O/tune.json  # config-4 plans (int8, bf16) -> $O/tune.json
+             for dt in int8 bf16; do
+               SSA_TUNE_FILE=$O/tune.json SSA_LOG_AUTOTUNE=1 timeout -k 10 600 python bench.py --arch resnet50 --input_size 1025 \
+                 --camera 2048x1024 --batch 8 --dtype $dt --steps 5 --warmup 2 --rpc 0 > $O/tunec4_$dt.json 2> $O/tunec4_$dt.err \
+                 || { tail -20 $O/tunec4_$dt.err; exit 8; }
+             done; python -c "import json; d=json.load(open('$O/tune.json')); print(sorted(d))" ;;
+    usetune) cp $O/tune.json assets/tune_mi355x.json && echo "box tree now runs $O/tune.json" ;;
+    upbench) timeout -k 10 120 python scripts/bench_upsample.py > $O/upsample.txt 2>&1 || { tail -5 $O/upsample.txt; exit 9; }
+             cat $O/upsample.txt ;;
     retune:*) [ -f $O/tune.json ] || cp assets/tune_mi355x.json $O/tune.json
              SSA_TUNE_FILE=$O/tune.json SSA_RETUNE_ONLY=${step#retune:} SSA_LOG_AUTOTUNE=1 \
                timeout -k 10 600 python bench.py --batch ${TUNE_B:-32} --steps 5 --warmup 2 --rpc 0 $BENCH_ARGS \

@@ -508,11 +508,11 @@ class HipDeepLab:
         # labels_out (segment's out=): write the label maps straight into a caller
         # buffer (the engine's per-slot maps) instead of the plan's static one
         # upsample + argmax: row-block (LDS-staged, coalesced stores), per-lane stores, or
-        # cell-bound class pruning (one workgroup per source row interval)
+        # per-lane with wave-union class pruning
         ops.append(Choice("upsample", [(name, [lambda *_, h=h, w=w, v=K.UPSAMPLE_VARIANTS[name]:
                                                K.upsample_argmax(
             logits, self._labels_out if self._labels_out is not None else labels, B=B, h=h, w=w,
-            K=self.num_classes, ldk=self.ldk, H=H, W=W, variant=v)]) for name in ("rows", "lane", "cell")]))
+            K=self.num_classes, ldk=self.ldk, H=H, W=W, variant=v)]) for name in ("rows", "lane", "union")]))
         self._plans[key] = (ops, bufs)
         if part == 0:
             self._autotune(ops, B, Hc, Wc)

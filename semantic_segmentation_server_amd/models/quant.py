@@ -73,16 +73,24 @@ def calibrate(model: DeepLabV3, x: torch.Tensor) -> Dict[str, float]:
 
 
 @torch.no_grad()
-def fake_quant_forward(model: DeepLabV3, scales: Dict[str, float], x: torch.Tensor) -> torch.Tensor:
-    """fp32 replay of the int8 pipeline -> logits (N, K, h, w)."""
+def fake_quant_forward(model: DeepLabV3, scales: Dict[str, float], x: torch.Tensor,
+                       stem_bf16: bool = False) -> torch.Tensor:
+    """fp32 replay of the int8 pipeline -> logits (N, K, h, w). ``stem_bf16``: the stem as
+    the MFMA stem kernels compute it (normalised pixels and folded weights rounded to bf16,
+    fp32 accumulation, int8 out) instead of the fp32 per-lane stem: the int8 network
+    amplifies a stem code that differs by one step into multi-step differences a few
+    blocks later, so the replay must round where the plan's stem rounds."""
     bb = model.backbone
 
     def conv(layer: ConvBNAct, inp, s_out=None, res=None, act=None, quant_w=True):
         if quant_w:
             wq, sw, b = _qw(layer)
             wf = wq * sw.view(-1, 1, 1, 1)
-        else:  # the fused stem runs with fp32 weights on fp32 pixels
+        else:  # the fused stem: fp32 (or bf16-rounded) weights on fp32 (bf16) pixels
             wf, b = layer.fold()
+            if stem_bf16:
+                wf = wf.to(torch.bfloat16).float()
+                inp = inp.to(torch.bfloat16).float()
         y = F.conv2d(inp, wf, b, layer.stride,
                      layer.dilation * (layer.k // 2), layer.dilation)
         if res is not None:
@@ -111,6 +119,37 @@ def fake_quant_forward(model: DeepLabV3, scales: Dict[str, float], x: torch.Tens
     proj = q(torch.relu(proj), scales["aspp.proj"])
     lq, ls, lb = _qw(model.logits)
     return F.conv2d(proj, lq * ls.view(-1, 1, 1, 1), lb)
+
+
+@torch.no_grad()
+def int8_conv_codes(layer: ConvBNAct, x_codes: torch.Tensor, s_in: float, s_out: float,
+                    res_codes: torch.Tensor = None, s_res: float = 0.0, act: str = None,
+                    chunk_k: int = 576) -> torch.Tensor:
+    """One int8 conv of the plan in exact arithmetic, from the plan's OWN input codes
+    (teacher forcing): integer accumulators exactly (fp32 convs over input-channel chunks
+    whose partial sums stay below 2^24, summed in float64), then v = acc * s_in * s_w +
+    bias (+ res * s_res), ReLU, round-half-even requantisation. x_codes / res_codes: NCHW
+    integer-valued tensors; returns NCHW int32 codes. A kernel matches this up to rounding
+    ties of its fp32 epilogue (a code off by one, rarely); the network itself amplifies such
+    a flip into multi-step differences a few blocks later, so per-layer teacher-forced
+    comparison is how a plan's kernels are checked at full depth."""
+    wq, sw, b = _qw(layer)
+    kk = layer.k * layer.k
+    step = max(1, chunk_k // kk)  # input channels per chunk: step * k^2 * 127^2 < 2^24
+    acc = None
+    pad, dil = layer.dilation * (layer.k // 2), layer.dilation
+    xf = x_codes.float()
+    for c0 in range(0, xf.shape[1], step):
+        part = F.conv2d(xf[:, c0:c0 + step], wq[:, c0:c0 + step].to(xf.device), None, layer.stride,
+                        pad, dil).double()
+        acc = part if acc is None else acc + part
+    v = acc * (s_in * sw.double().to(acc.device)).view(1, -1, 1, 1) + b.double().to(acc.device).view(1, -1, 1, 1)
+    if res_codes is not None:
+        v = v + res_codes.double() * s_res
+    a = layer.act if act is None else act
+    if a == "relu":
+        v = torch.relu(v)
+    return torch.clamp(torch.round(v / s_out), -127, 127).to(torch.int32)
 
 
 def pack_int8(layer: ConvBNAct, in_scale: float, device, wslice=None):

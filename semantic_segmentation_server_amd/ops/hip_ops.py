@@ -1059,7 +1059,7 @@ def aspp_head(cat, packed: dict, out, *, M: int, HW: int, ldo: int, img_bias=Non
     return out
 
 
-UPSAMPLE_VARIANTS = {"rows": 3, "rows_tag": 4, "lane": 1, "lane_tag": 2, "direct": 5, "cell": 6}
+UPSAMPLE_VARIANTS = {"rows": 3, "rows_tag": 4, "lane": 1, "lane_tag": 2, "direct": 5, "union": 6}
 
 
 def upsample_argmax(logits, labels, *, B, h, w, K, ldk, H, W, variant: int = 0):

@@ -46,7 +46,7 @@ _pool_exhausted_frames = 0
 
 def pool_exhausted_frames() -> int:
     """Frames (process lifetime) that got no records because their batch's components
-    overflowed the device root pool (max(B * 8192, H * W + 1) components per batch;
+    overflowed the device root pool (max(B * 8192, H * W + 1) + H * W / 2 + 1 components per batch;
     postprocess.hip Layout): the record count comes back NaN."""
     return _pool_exhausted_frames
 

@@ -43,6 +43,7 @@ class PipelineDriver:
         self.frames = 0
         self._t_last = None
         self._overflow_seen = 0
+        self._pool_lost_seen = 0
 
     # ------------------------------------------------------------------ helpers
     def _h2d_event(self) -> Optional["torch.cuda.Event"]:
@@ -101,12 +102,16 @@ class PipelineDriver:
         self.frames += n
         now = time.perf_counter()
         if self.metrics is not None:
-            from ..parallel.dp import overflow_frames
+            from ..parallel.dp import overflow_frames, pool_exhausted_frames
             dt = (now - self._t_last) * 1e3
             ov = overflow_frames()
             if ov != self._overflow_seen:  # frames with more than K contours above min_area
                 self.metrics.inc("record_overflow_frames", ov - self._overflow_seen)
                 self._overflow_seen = ov
+            pe = pool_exhausted_frames()
+            if pe != self._pool_lost_seen:  # frames whose components did not fit the root pool
+                self.metrics.inc("pool_exhausted_frames", pe - self._pool_lost_seen)
+                self._pool_lost_seen = pe
             self.metrics.inc("frames", n)
             self.metrics.inc("objects", len(recs))
             self.metrics.observe("step_ms", dt)

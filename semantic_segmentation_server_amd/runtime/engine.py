@@ -115,7 +115,14 @@ class Engine:
             if cfg.arch != "resnet50":
                 raise ValueError("--dtype int8 is implemented for --arch resnet50 (config 4)")
             from ..models.hip_int8 import HipDeepLabInt8
-            self._hip_model = HipDeepLabInt8(self.model, self.device, cfg)
+            from ..models.quant import calibrate
+            # activation scales from the serving distribution: letterboxed synthetic camera
+            # frames at the model resolution (calibration_frames), not generic noise images
+            import copy
+            xc = calibration_frames(self.H, self.W, n=4, seed=cfg.seed).to(self.device)
+            scales = calibrate(copy.deepcopy(self.model).float().to(self.device), xc)
+            del xc
+            self._hip_model = HipDeepLabInt8(self.model, self.device, cfg, scales=scales)
         else:
             from ..models.hip_model import HipDeepLab
             self._hip_model = HipDeepLab(self.model, self.device, cfg)

@@ -108,13 +108,15 @@ def test_letterbox_crop_geometry():
 def test_device_post_workspace_is_compact():
     """the device post-processing workspace keeps per component state in a
     batch-shared root pool indexed by label, not per raster pixel: <= 4 MB per 513^2 frame
-    at the bench batch (round 4: ~46 MB), with a floor that still holds any single frame."""
+    at the bench batch (round 4: ~46 MB; the <= 4 MB of round 5 plus N / 2 + 1 pool entries
+    per batch since ADVICE r5, so that two worst-case fallback frames fit: <= 4.25 MB), with
+    a floor that still holds any single frame."""
     hip_ops = pytest.importorskip("semantic_segmentation_server_amd.ops.hip_ops")
     try:
         per32 = hip_ops.post_workspace_bytes(32, 513, 513, 64, 21) / 32
         one = hip_ops.post_workspace_bytes(1, 513, 513, 64, 21)
     except Exception as e:  # pragma: no cover - extension not built
         pytest.skip(f"HIP extension unavailable: {e}")
-    assert per32 <= 4 * 2 ** 20, per32
+    assert per32 <= 4.25 * 2 ** 20, per32
     # pool floor: H * W + 1 components (more than any frame can have), ~112 B each
     assert one >= (513 * 513 + 1) * (24 + 4 * 21)
