@@ -278,7 +278,7 @@ __device__ __forceinline__ void dwproj_groups(const char* Wp, const char* misc, 
 }
 
 // the in-launch combine's compile-time bound on the hidden split (fused_ir_stream checks it)
-constexpr int kCombineHS = 6;
+constexpr int kCombineHS = 8;
 
 template <int KS, int NS, int XQ, int DIL, int WCP, int MODE>
 __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kernel(StreamArgs a) {
@@ -641,7 +641,7 @@ void fused_ir_stream(const FusedSpanParams& p, hipStream_t st) {
   if (p.hsplit < 1 || p.hsplit > p.hidP / 32 || (p.hsplit > 1 && p.part == nullptr))
     throw std::invalid_argument("fused_ir_stream: hsplit in [1, hidP / 32], partials buffer for hsplit > 1");
   if (p.hsplit > kCombineHS && p.cnt != nullptr)
-    throw std::invalid_argument("fused_ir_stream: the in-launch combine takes hsplit <= 6");
+    throw std::invalid_argument("fused_ir_stream: the in-launch combine takes hsplit <= 8");
   StreamArgs a{p.in, reinterpret_cast<const char*>(p.w), p.bp, p.table, p.out, p.B, p.H, p.W, p.Cin,
                p.Cout, p.hidP / 32, p.S, p.dil, p.residual, p.WCP, p.WR, p.hstride, p.trace,
                p.hsplit, p.part, p.hsplit > 1 ? p.cnt : nullptr};

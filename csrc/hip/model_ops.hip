@@ -1055,18 +1055,21 @@ __global__ __launch_bounds__(256) void upsample_argmax_interval_kernel(
   iv.template emit<TAGGED>(labels + ((size_t)b * H + Y) * W, K);
 }
 
-// variant 6: emit_union (the wave-wide shuffles need every lane of the wave: lanes past the
-// end take an empty interval instead of returning)
+// variant 6: emit_union. A wave owns a compact 16-row x 4-interval block (lane = row dy +
+// 16 x interval dj): at 33 -> 513 its 16 rows share one upper source row, so the wave's
+// union of candidate classes is that of ~4 source cells, not of a whole map row as with
+// the row-major lane order. The wave-wide shuffles need every lane: lanes past the map
+// take an empty interval instead of returning.
 template <int KP>
 __global__ __launch_bounds__(256) void upsample_argmax_union_kernel(
     const bf16* __restrict__ logits, uint8_t* __restrict__ labels, int B, int h, int w, int K,
     int ldk, int H, int W) {
-  const int t0 = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = t0 < B * H * w;
-  const int t = live ? t0 : 0;
-  const int j = t % w;
-  const int Y = (t / w) % H;
-  const int b = t / (w * H);
+  const int nyb = (H + 15) >> 4, njb = (w + 3) >> 2;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int jb = wave % njb, yb = (wave / njb) % nyb, b0 = wave / (njb * nyb);
+  const int Y0 = yb * 16 + (lane & 15), j0 = jb * 4 + (lane >> 4);
+  const bool live = b0 < B && Y0 < H && j0 < w;
+  const int b = live ? b0 : 0, Y = live ? Y0 : 0, j = live ? j0 : 0;
   Interval<KP> iv;
   iv.load(logits, b, Y, j, h, w, H, W, ldk);
   if (!live) iv.xe = iv.xs;
@@ -1119,7 +1122,8 @@ void launch_upsample_interval(int variant, const bf16* logits, uint8_t* labels, 
                               int w, int K, int ldk, int H, int W, hipStream_t s) {
   const long long total = (long long)B * H * w;
   if (variant == 6) {
-    hipLaunchKernelGGL((upsample_argmax_union_kernel<KP>), dim3(cdiv(total, 256)), dim3(256), 0, s,
+    const long long waves = (long long)B * ((H + 15) / 16) * ((w + 3) / 4);
+    hipLaunchKernelGGL((upsample_argmax_union_kernel<KP>), dim3(cdiv(waves, 4)), dim3(256), 0, s,
                        logits, labels, B, h, w, K, ldk, H, W);
     return;
   }

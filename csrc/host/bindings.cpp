@@ -4,6 +4,7 @@
 #include <pybind11/stl.h>
 
 #include "contours.h"
+#include "records.h"
 #include "v4l2.h"
 
 namespace py = pybind11;
@@ -100,6 +101,29 @@ py::list segments(const U8& labels, const I32& palette, double min_area) {
 
 PYBIND11_MODULE(_host, m) {
   m.doc() = "Host-side exact contour analysis (Suzuki-Abe border following, OpenCV-equivalent).";
+  m.def(
+      "unpack_records",
+      [](py::array packed, int K, py::array meta, py::array out) {
+        // packed: float32 (F, >= 1 + 5K) C-contiguous rows; meta: float64 (F, 3); out: a
+        // writable C-contiguous RECORD_DTYPE (40-byte) array of >= F * K rows
+        if (packed.ndim() != 2 || packed.dtype().kind() != 'f' || packed.itemsize() != 4 ||
+            !(packed.flags() & py::array::c_style) || packed.shape(1) < 1 + 5 * (ssize_t)K)
+          throw std::invalid_argument("unpack_records: packed must be C-contiguous float32 (F, 1 + 5K)");
+        const ssize_t F = packed.shape(0);
+        if (meta.ndim() != 2 || meta.shape(0) != F || meta.shape(1) != 3 || meta.itemsize() != 8 ||
+            meta.dtype().kind() != 'f' || !(meta.flags() & py::array::c_style))
+          throw std::invalid_argument("unpack_records: meta must be C-contiguous float64 (F, 3)");
+        if (out.ndim() != 1 || out.itemsize() != (ssize_t)sizeof(Record) || !out.writeable() ||
+            !(out.flags() & py::array::c_style) || out.shape(0) < F * K)
+          throw std::invalid_argument("unpack_records: out must be a writable RECORD_DTYPE array of F * K rows");
+        const UnpackStats st = unpack_records(static_cast<const float*>(packed.data()), F, K, packed.shape(1),
+                                              static_cast<const double*>(meta.data()),
+                                              static_cast<Record*>(out.mutable_data()), out.shape(0));
+        return py::make_tuple(st.records, st.overflow, st.pool_lost);
+      },
+      py::arg("packed"), py::arg("K"), py::arg("meta"), py::arg("out"),
+      "Packed per-frame device records -> RECORD_DTYPE rows in push order; returns (rows, "
+      "overflow frames, pool-exhausted frames)");
   m.def("find_contours", &find_contours, py::arg("mask"),
         "findContours(RETR_TREE, CHAIN_APPROX_SIMPLE) on a 0/nonzero uint8 mask.");
   m.def("contour_area", [](const I32& p) { return contour_area(to_pts(p)); });

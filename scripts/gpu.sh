@@ -17,6 +17,7 @@
 #   cfg5p        the same with one engine + HIP stream + hipGraph per camera stream
 #   prof         sequential kernel trace of the B=32 step -> layer_times.txt
 #   profb1       sequential kernel trace of the B=1 step -> b1_layer_times.txt
+#   prof0        the B=32 trace at lag 0 (post-processing not overlapping the next step)
 #   profc4       config-4 (ResNet-50 1025^2 int8, B=8) kernel trace -> c4_roofline.txt
 #   pmc          3 SQ counter passes over the sequential B=32 step -> pmc_summary.txt
 #   pmck         the same passes per kernel name + grid (model from BENCH_ARGS) -> kernel_pmc.txt
@@ -55,7 +56,7 @@ PMC_SETS=(
 trace() {  # trace <name> <bench args...>: sequential-model kernel trace + layer table
   local name=$1; shift
   (cd /tmp && export TMPDIR=/tmp && SSA_SLOT_PARALLEL=0 timeout -k 10 400 rocprofv3 --kernel-trace --stats \
-    -d $REPO/$O/$name -o run --output-format csv -- python3 $REPO/bench.py "$@" --lag 1 --rpc 0 $BENCH_ARGS \
+    -d $REPO/$O/$name -o run --output-format csv -- python3 $REPO/bench.py "$@" --lag ${TRACE_LAG:-1} --rpc 0 $BENCH_ARGS \
     > $REPO/$O/$name.log 2>&1) || { echo "trace $name failed"; tail -5 $O/$name.log; return 1; }
   python3 scripts/layer_times.py $(ls $O/$name/*/run_kernel_trace.csv 2>/dev/null || ls $O/$name/run_kernel_trace.csv) \
     > $O/${name}_layer_times.txt && tail -45 $O/${name}_layer_times.txt
@@ -88,6 +89,7 @@ for step in "$@"; do
     cfg5p)   bench c5p 400 --streams 4 --batch 32 --per_stream_graphs --steps 100 --warmup 10 --rpc 0 || exit 2 ;;
     prof)    trace seq --steps 5 --warmup 2 || exit 3 ;;
     profb1)  trace b1seq --batch 1 --steps 20 --warmup 5 || exit 3 ;;
+    prof0)   TRACE_LAG=0 trace seq0 --steps 5 --warmup 2 || exit 3 ;;
     profc4)  trace c4seq --arch resnet50 --input_size 1025 --camera 2048x1024 --batch 8 --dtype int8 --steps 5 --warmup 2 || exit 3
              python3 scripts/roofline_int8.py $(ls $O/c4seq/*/run_kernel_trace.csv 2>/dev/null || ls $O/c4seq/run_kernel_trace.csv) 8 \
                > $O/c4_roofline.txt && head -3 $O/c4_roofline.txt && tail -3 $O/c4_roofline.txt ;;

@@ -100,6 +100,46 @@ def unpack_records(packed: np.ndarray, K: int, frame_ids, ts, streams) -> np.nda
     return out
 
 
+_native_unpack = None
+
+
+def _count_lost(lost: int, over: int, K: int) -> None:
+    global _overflow_frames, _pool_exhausted_frames
+    if lost:
+        if _pool_exhausted_frames == 0:
+            log.warning("a batch of label maps had more components than the device root pool "
+                        "holds; %d frame(s) returned no records", lost)
+        _pool_exhausted_frames += lost
+    if over:
+        if _overflow_frames == 0:
+            log.warning("a frame had more than K=%d contours above min_area; the first K by "
+                        "discovery order were kept (raise --max_segments)", K)
+        _overflow_frames += over
+
+
+def unpack_records_meta(packed: np.ndarray, K: int, meta: np.ndarray) -> np.ndarray:
+    """``unpack_records`` with the frame metadata as one (F, 3) float64 array (frame id,
+    stream, capture ts), in native code (ops/_host ``unpack_records``): at small batches the
+    numpy form is all call overhead (~30 us per step at batch 1, the collect being on the
+    host's critical path). Same rows as ``unpack_records`` (tests/test_host_path.py)."""
+    global _native_unpack
+    if _native_unpack is None:
+        try:
+            from ..ops import native
+            _native_unpack = native.host().unpack_records
+        except Exception:  # pragma: no cover - no compiler on this host
+            _native_unpack = False
+    if _native_unpack is False:
+        return unpack_records(packed, K, meta[:, 0].astype(np.int64), meta[:, 2],
+                              meta[:, 1].astype(np.int64))
+    packed = np.ascontiguousarray(packed, dtype=np.float32)
+    meta = np.ascontiguousarray(meta, dtype=np.float64)
+    out = np.empty(packed.shape[0] * K, RECORD_DTYPE)
+    n, over, lost = _native_unpack(packed, K, meta, out)
+    _count_lost(lost, over, K)
+    return out[:n]
+
+
 class DataParallelPipeline:
     def __init__(self, ctx: DistContext, engine, cam_w: int, cam_h: int, batch: int,
                  ingest: str = "local", hub: Optional[ResultHub] = None,
@@ -529,8 +569,24 @@ class DataParallelPipeline:
                     raise PeerLost(f"RCCL gather not complete after {self.rank_timeout_s:.0f} s")
             time.sleep(2e-5)
 
+    @staticmethod
+    def _single_stream(meta: np.ndarray) -> Optional[int]:
+        """The one source stream of a collected batch, or None if it mixes streams (a hint
+        that lets the hub skip its per-stream split)."""
+        if len(meta) <= 8:
+            s0 = meta[0, 1]
+            for i in range(1, len(meta)):
+                if meta[i, 1] != s0:
+                    return None
+            return int(s0)
+        col = meta[:, 1]
+        return int(col[0]) if (col == col[0]).all() else None
+
     def _observe(self, meta: np.ndarray) -> None:
         """Per collected frame (rank 0): capture -> hub latency and per-stream frame order."""
+        if len(meta) <= 8:  # small batches: plain Python (numpy's per-call overhead dominates)
+            DataParallelPipeline._observe_small(self, meta)
+            return
         now = time.time()
         ts = meta[:, 2]
         lat = (now - ts[ts > 0]) * 1e3
@@ -549,6 +605,22 @@ class DataParallelPipeline:
             self.frame_order_errors += int((cur <= prev).sum())
             self.stream_last_id[st] = int(seq[-1])
             self.stream_frames[st] = self.stream_frames.get(st, 0) + len(seq)
+
+    def _observe_small(self, meta: np.ndarray) -> None:
+        now = time.time()
+        rows = meta.tolist()
+        lat = [(now - r[2]) * 1e3 for r in rows if r[2] > 0]
+        if lat:
+            self.frame_latency.add_many(lat)
+            if self.metrics is not None:
+                self.metrics.observe_many("frame_latency_ms", lat)
+        for fid, st, _ in rows:
+            fid, st = int(fid), int(st)
+            last = self.stream_last_id.get(st)
+            if last is not None and fid <= last:
+                self.frame_order_errors += 1
+            self.stream_last_id[st] = fid
+            self.stream_frames[st] = self.stream_frames.get(st, 0) + 1
 
     @staticmethod
     def _node_meta(fids, strm, tss) -> np.ndarray:
@@ -590,11 +662,10 @@ class DataParallelPipeline:
             else:
                 meta = lm.numpy()
                 flat = self.local_rec[slot].numpy()
-            recs = unpack_records(flat, self.K, meta[:, 0].astype(np.int64), meta[:, 2],
-                                  meta[:, 1].astype(np.int64))
+            recs = unpack_records_meta(flat, self.K, meta)
             self.records_out += len(recs)
             if self.hub is not None:
-                self.hub.push_records(recs)
+                self.hub.push_records(recs, self._single_stream(meta))
             self._observe(meta)
             return recs
         if not self.ctx.is_root:
@@ -608,10 +679,9 @@ class DataParallelPipeline:
             meta = np.stack([np.asarray(fids, np.float64), np.asarray(strm, np.float64),
                              np.asarray(tss, np.float64)], 1)
             flat = self.host_rec[slot].numpy().reshape(-1, self.rec_width)
-        recs = unpack_records(flat, self.K, meta[:, 0].astype(np.int64), meta[:, 2],
-                              meta[:, 1].astype(np.int64))
+        recs = unpack_records_meta(flat, self.K, meta)
         self.records_out += len(recs)
         if self.hub is not None:
-            self.hub.push_records(recs)
+            self.hub.push_records(recs, self._single_stream(meta))
         self._observe(meta)
         return recs

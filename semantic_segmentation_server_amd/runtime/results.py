@@ -153,13 +153,17 @@ class ResultHub:
                 buf = self.buffers[stream] = ResultBuffer(self.maxlen)
             return buf
 
-    def push_records(self, recs: np.ndarray) -> None:
+    def push_records(self, recs: np.ndarray, stream: Optional[int] = None) -> None:
         """Push a batch of records (any streams/frames), preserving order.
 
         Records must be ordered by (frame, contour index) within each stream,
-        which is how the post-processing stage emits them.
+        which is how the post-processing stage emits them. ``stream``: the caller knows
+        every record comes from this one stream (skips the per-stream split).
         """
         if len(recs) == 0:
+            return
+        if stream is not None:
+            self.buffer(int(stream)).push_frame(recs)
             return
         streams = recs["stream"]
         for s in np.unique(streams):

@@ -27,7 +27,14 @@ class Reservoir:
         self.n += 1
 
     def add_many(self, vs) -> None:
-        """add() of every value of ``vs``, in order (one numpy scatter, not a Python loop)."""
+        """add() of every value of ``vs``, in order (one numpy scatter, not a Python loop;
+        a few values: plain add()s, cheaper than the scatter's call overhead)."""
+        if isinstance(vs, list) and len(vs) <= 8:
+            L = len(self.buf)
+            for v in vs:
+                self.buf[self.n % L] = v
+                self.n += 1
+            return
         vs = np.asarray(vs, dtype=np.float64).ravel()
         L = len(self.buf)
         if len(vs) > L:  # only the last L can survive

@@ -99,3 +99,39 @@ def test_rank0_host_time_at_world8():
     assert len(recs) >= 2 * F
     print(f"rank-0 host time per world-8 step: {best * 1e3:.3f} ms")
     assert best < 1.0e-3
+
+
+def test_native_unpack_matches_numpy():
+    """The native record unpacker (ops/_host unpack_records) writes exactly the rows of the
+    numpy reference (parallel/dp.unpack_records), counts included: negative counts
+    (overflow, |count| kept), NaN counts (pool exhausted: no rows), counts past K."""
+    from semantic_segmentation_server_amd.parallel import dp
+    rng = np.random.default_rng(3)
+    K, F = 8, 40
+    packed = rng.standard_normal((F, 1 + 5 * K)).astype(np.float32)
+    packed[:, 1::5] = rng.integers(0, 21, (F, K))
+    counts = rng.integers(0, K + 3, F).astype(np.float32)
+    counts[::7] *= -1
+    counts[3] = np.nan
+    counts[11] = 2.7
+    packed[:, 0] = counts
+    meta = np.stack([np.arange(100, 100 + F), rng.integers(0, 4, F), rng.random(F) * 1e9], 1)
+    ov0, pl0 = dp.overflow_frames(), dp.pool_exhausted_frames()
+    ref = dp.unpack_records(packed, K, meta[:, 0].astype(np.int64), meta[:, 2], meta[:, 1].astype(np.int64))
+    ov1, pl1 = dp.overflow_frames(), dp.pool_exhausted_frames()
+    got = dp.unpack_records_meta(packed, K, meta)
+    assert dp._native_unpack not in (None, False), "native unpack not loaded"
+    assert got.dtype == ref.dtype and len(got) == len(ref) > 0
+    assert got.tobytes() == ref.tobytes()
+    assert dp.overflow_frames() - ov1 == ov1 - ov0 and dp.pool_exhausted_frames() - pl1 == pl1 - pl0 == 1
+
+
+def test_hub_single_stream_hint_matches_split():
+    from semantic_segmentation_server_amd.runtime.results import RECORD_DTYPE, ResultHub
+    recs = np.zeros(5, RECORD_DTYPE)
+    recs["stream"] = 2
+    recs["frame"] = np.arange(5)
+    a, b = ResultHub(4), ResultHub(4)
+    a.push_records(recs)
+    b.push_records(recs, 2)
+    assert [r["frame"] for r in a.get(2).pop(5)] == [r["frame"] for r in b.get(2).pop(5)]

@@ -134,3 +134,17 @@ def test_reservoir_add_many_and_frame_order_bookkeeping():
     assert p.frame_order_errors == 2
     assert p.stream_frames == {0: 4, 1: 4} and p.stream_last_id == {0: 3, 1: 9}
     assert p.frame_latency.n == 8
+    # the plain-Python path (batches of <= 8 frames) and the vectorised one agree
+    big = np.concatenate([meta] * 3)
+    big[:, 0] += np.repeat([0, 100, 200], 8)
+
+    def fresh():
+        q = P()
+        q.frame_latency, q.stream_last_id, q.stream_frames, q.frame_order_errors = Reservoir(64), {}, {}, 0
+        return q
+    q1, q2 = fresh(), fresh()
+    DataParallelPipeline._observe(q1, big)          # 24 frames: numpy
+    for k in range(0, 24, 8):
+        DataParallelPipeline._observe(q2, big[k:k + 8])  # 8 at a time: plain Python
+    assert (q1.frame_order_errors, q1.stream_frames, q1.stream_last_id) == \
+        (q2.frame_order_errors, q2.stream_frames, q2.stream_last_id)
