@@ -478,7 +478,7 @@ static int pick_nt(int Cout);
 // the buffer descriptor's range check, so the LDS image is always fully written.
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-// the in-launch split-K combine's compile-time bound on ks (conv_gemm_grouped checks it)
+// slices the in-launch split-K combine loads per round trip
 constexpr int kInlineKS = 8;
 
 // One BM x BN output tile (tile index bid in row-major (m-tile, n-tile) order) of
@@ -694,15 +694,18 @@ __device__ __forceinline__ void glds_tile(const ConvArgs& a, const int bid, char
           if (m < 0) continue;
           const float* q = part + (size_t)m * a.ldo + a.co_off + n;
           f32x4 v = *reinterpret_cast<const f32x4*>(a.bias + n);
-          // every slice's load issued before the first add (one L2 round trip, not ks
-          // dependent ones); slices past ks re-read the last one and are not added
-          f32x4 pv[kInlineKS];
+          // the slices' loads issued kInlineKS at a time before their adds (one L2 round
+          // trip per group, not one per slice); slices past ks re-read the last one and are
+          // not added; order sl = 0..ks-1
+          for (int s0 = 0; s0 < ks; s0 += kInlineKS) {
+            f32x4 pv[kInlineKS];
 #pragma unroll
-          for (int sl = 0; sl < kInlineKS; ++sl)
-            pv[sl] = *reinterpret_cast<const f32x4*>(q + (size_t)(sl < ks ? sl : ks - 1) * slab);
+            for (int sl = 0; sl < kInlineKS; ++sl)
+              pv[sl] = *reinterpret_cast<const f32x4*>(q + (size_t)(s0 + sl < ks ? s0 + sl : ks - 1) * slab);
 #pragma unroll
-          for (int sl = 0; sl < kInlineKS; ++sl)
-            if (sl < ks) v += pv[sl];
+            for (int sl = 0; sl < kInlineKS; ++sl)
+              if (s0 + sl < ks) v += pv[sl];
+          }
           bf16x4 o;
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = (bf16)apply_act(v[e], a.act);
@@ -980,8 +983,6 @@ void conv_gemm_grouped(const ConvParams* ps, int n, const int* order, int nblock
     for (int i = 0; i < n; ++i)
       if (ps[i].ldo != ps[0].ldo || ps[i].Cout % 4 || (ps[i].ldo | ps[i].co_off) % 4)
         throw std::invalid_argument("conv_gemm_grouped: split-K needs one ldo and 4-aligned channels");
-  if (ks > kInlineKS && cnt != nullptr)
-    throw std::invalid_argument("conv_gemm_grouped: the in-launch combine takes ks <= 8");
   ConvGroupArgs ga{};
   ga.ks = ks;
   ga.part = ks > 1 ? part : nullptr;

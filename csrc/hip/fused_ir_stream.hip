@@ -277,7 +277,7 @@ __device__ __forceinline__ void dwproj_groups(const char* Wp, const char* misc, 
   }
 }
 
-// the in-launch combine's compile-time bound on the hidden split (fused_ir_stream checks it)
+// slabs the in-launch combine loads per round trip
 constexpr int kCombineHS = 8;
 
 template <int KS, int NS, int XQ, int DIL, int WCP, int MODE>
@@ -572,24 +572,26 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
         const int px = u / C8, c = (u - px * C8) * 8;
         f32x4 s0 = *reinterpret_cast<const f32x4*>(a.bp + c), s1 = *reinterpret_cast<const f32x4*>(a.bp + c + 4);
         const float* q = pb + (size_t)px * a.Cout + c;
-        // every slab's loads (and the residual's) issued before the first add: one L2 round
-        // trip per unit instead of HS dependent ones (as stream_combine_kernel's HSM form;
-        // slabs past HS re-read the last one and are not added)
-        f32x4 v0[kCombineHS], v1[kCombineHS];
-#pragma unroll
-        for (int h = 0; h < kCombineHS; ++h) {
-          const size_t o = (size_t)(h < a.HS ? h : a.HS - 1) * slab;
-          v0[h] = *reinterpret_cast<const f32x4*>(q + o);
-          v1[h] = *reinterpret_cast<const f32x4*>(q + o + 4);
-        }
+        // the slabs' loads (and the residual's) issued kCombineHS at a time before their adds:
+        // one L2 round trip per group instead of one per slab (as stream_combine_kernel's HSM
+        // form; slabs past HS re-read the last one and are not added; order h = 0..HS-1)
         bf16x8 r = zero8();
         if (a.residual) r = ld8(resb + (size_t)px * a.Cin + c);
+        for (int h0 = 0; h0 < a.HS; h0 += kCombineHS) {
+          f32x4 v0[kCombineHS], v1[kCombineHS];
 #pragma unroll
-        for (int h = 0; h < kCombineHS; ++h)
-          if (h < a.HS) {
-            s0 += v0[h];
-            s1 += v1[h];
+          for (int h = 0; h < kCombineHS; ++h) {
+            const size_t o = (size_t)(h0 + h < a.HS ? h0 + h : a.HS - 1) * slab;
+            v0[h] = *reinterpret_cast<const f32x4*>(q + o);
+            v1[h] = *reinterpret_cast<const f32x4*>(q + o + 4);
           }
+#pragma unroll
+          for (int h = 0; h < kCombineHS; ++h)
+            if (h0 + h < a.HS) {
+              s0 += v0[h];
+              s1 += v1[h];
+            }
+        }
         bf16x8 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -640,8 +642,6 @@ void fused_ir_stream(const FusedSpanParams& p, hipStream_t st) {
   if (p.nh_max > kXQ * 4 * 16) throw std::invalid_argument("fused_ir_stream: halo over 320 pixels");
   if (p.hsplit < 1 || p.hsplit > p.hidP / 32 || (p.hsplit > 1 && p.part == nullptr))
     throw std::invalid_argument("fused_ir_stream: hsplit in [1, hidP / 32], partials buffer for hsplit > 1");
-  if (p.hsplit > kCombineHS && p.cnt != nullptr)
-    throw std::invalid_argument("fused_ir_stream: the in-launch combine takes hsplit <= 8");
   StreamArgs a{p.in, reinterpret_cast<const char*>(p.w), p.bp, p.table, p.out, p.B, p.H, p.W, p.Cin,
                p.Cout, p.hidP / 32, p.S, p.dil, p.residual, p.WCP, p.WR, p.hstride, p.trace,
                p.hsplit, p.part, p.hsplit > 1 ? p.cnt : nullptr};
