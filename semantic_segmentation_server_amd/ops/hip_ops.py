@@ -22,7 +22,9 @@ _DEBUG_SYNC = os.environ.get("SSA_DEBUG_SYNC", "0") == "1"
 
 
 def _stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
+    # the raw handle of the current stream by two C calls (utils/fast_cuda.py: the
+    # torch.cuda.current_stream() path resolves the device on every launch)
+    return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
 
 
 def _dbg(name: str, **shapes) -> None:

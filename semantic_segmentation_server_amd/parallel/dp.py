@@ -34,6 +34,7 @@ import torch.distributed as dist
 
 from .dist import DistContext, PeerLost, _abort_key
 from ..runtime.results import RECORD_DTYPE, ResultHub
+from ..utils import fast_cuda
 from ..utils.metrics import Reservoir
 from ..utils.tracing import NULL_TRACER
 
@@ -204,6 +205,11 @@ class DataParallelPipeline:
         NS = self.nslots
         self.staging = [torch.zeros(shape, dtype=torch.uint8, device=dev) for _ in range(NS)]
         self.ready = [torch.cuda.Event() if self.cuda else None for _ in range(NS)]
+        self._up_ev = [torch.cuda.Event() for _ in range(2 * NS + 2)] if self.cuda else []
+        self._up_i = 0
+        self._rec_ev = [torch.cuda.Event() for _ in range(NS)] if self.cuda else []
+        self.dev_index = dev.index if (self.cuda and dev.index is not None) else \
+            (torch.cuda.current_device() if self.cuda else -1)
         self.last_upload = None  # event of the most recent prefetch's H2D copy
         self.slot = 0
         # capture time of each slot's frames when the caller gives none: the time the host
@@ -362,15 +368,18 @@ class DataParallelPipeline:
             return
         up = self._slot_stream(s)
         st = up if up is not None else self.copy_stream
-        with torch.cuda.stream(st):
+        with fast_cuda.StreamSwitch(st):
             if self.ingest == "scatter":
                 if self.ctx.is_root:
                     self.node_batch[s].copy_(host_frames, non_blocking=True)
             else:
                 self.staging[s].copy_(host_frames, non_blocking=True)
-            # a fresh event per upload: the serving driver hands the pinned host batch back
-            # to its feeder only once THIS copy has completed (last_upload)
-            ev = torch.cuda.Event()
+            # an event per upload from a ring of 2 * nslots + 2 (no per-step allocation): the
+            # serving driver hands the pinned host batch back to its feeder only once this
+            # copy has completed (last_upload); a ring event re-recorded while an older
+            # batch still waits on it only delays that release to the newer copy
+            ev = self._up_ev[self._up_i]
+            self._up_i = (self._up_i + 1) % len(self._up_ev)
             ev.record(st)
             self.ready[s] = ev
             self.last_upload = ev
@@ -463,12 +472,17 @@ class DataParallelPipeline:
         # post-processing runs on a stream of its own: gather + D2H go there too
         rs = getattr(self.engine, "result_stream", None) if self.cuda else None
         if self.gather_mode == "host":
-            with (torch.cuda.stream(rs) if rs is not None else contextlib.nullcontext()):
+            ev = None
+            if rs is not None:
+                with fast_cuda.StreamSwitch(rs):
+                    self._d2h(packed, self.local_rec[slot])
+                ev = self._rec_ev[slot]  # per record slot: collected before the slot is reused
+                ev.record(rs)
+            else:
                 self._d2h(packed, self.local_rec[slot])
-                ev = None
                 if self.cuda:
-                    ev = torch.cuda.Event()
-                    ev.record(torch.cuda.current_stream(self.dev))
+                    ev = self._rec_ev[slot]
+                    ev.record(fast_cuda.current_stream(self.dev_index))
             self.frames_done += B * self.ctx.world
             return self._enqueue((slot, ev, fids, strm, tss))
         with (torch.cuda.stream(rs) if rs is not None else contextlib.nullcontext()):

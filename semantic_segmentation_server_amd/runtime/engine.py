@@ -38,6 +38,8 @@ from ..ops import reference_ops as R
 from ..postprocess import reference as PR
 from .results import RECORD_DTYPE
 
+from ..utils import fast_cuda
+
 log = logging.getLogger(__name__)
 
 DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32, "int8": torch.bfloat16}
@@ -257,6 +259,9 @@ class Engine:
         self.slot_parallel = (os.environ.get("SSA_SLOT_PARALLEL", "1") == "1" and self._split
                               and hasattr(getattr(self, "_hip_model", None), "_labels_out"))
         self.slot_streams: List[torch.cuda.Stream] = []
+        self._slot_ev: List[tuple] = []  # per slot: (fork, ready) events, reused every step
+        self.device_index = (self.device.index if self.device.index is not None
+                             else torch.cuda.current_device() if self.is_cuda else -1)
         self.last_consumed = None
         # uploads on the slot streams (default; SSA_H2D_ON_SLOT=0: a copy stream): the
         # pipeline uploads a slot's frames on that slot's model stream, in order before its
@@ -377,32 +382,37 @@ class Engine:
                 if gpost is None:
                     g.replay()
                     return labels, post
-                cur = torch.cuda.current_stream(self.device)
-                if not self.h2d_on_slot:
-                    cur.wait_event(post_done)  # this slot's previous post-processing read `labels`
                 if self.slot_parallel:
                     # this slot's model on its own stream: the previous step (other slot,
-                    # other stream, other plan copy) may still be running
+                    # other stream, other plan copy) may still be running. Per-step host work
+                    # kept to C calls (utils/fast_cuda.py; per-slot events reused: a slot's
+                    # next step is at least one step later)
                     i = self._slot_of[frames.data_ptr()]
                     while len(self.slot_streams) <= i:
                         self.slot_streams.append(torch.cuda.Stream(self.device))
+                    while len(self._slot_ev) <= i:
+                        self._slot_ev.append((torch.cuda.Event(), torch.cuda.Event()))
+                    fork, ready = self._slot_ev[i]
                     ms, rs = self.slot_streams[i], self.result_stream
                     if self.h2d_on_slot:  # frames were uploaded on ms itself
                         ms.wait_event(post_done)
                     else:
-                        fork = torch.cuda.Event()
+                        cur = fast_cuda.current_stream(self.device_index)
+                        cur.wait_event(post_done)  # this slot's previous post-processing read `labels`
                         fork.record(cur)  # cur waited for this slot's frames (H2D)
                         ms.wait_event(fork)
-                    with torch.cuda.stream(ms):
+                    with fast_cuda.StreamSwitch(ms):
                         g.replay()
-                    ready = torch.cuda.Event()
                     ready.record(ms)
                     self.last_consumed = ready  # the staging slot may be refilled after this
                     rs.wait_event(ready)
-                    with torch.cuda.stream(rs):
+                    with fast_cuda.StreamSwitch(rs):
                         gpost.replay()
                     post_done.record(rs)
                     return labels, post
+                cur = torch.cuda.current_stream(self.device)
+                if not self.h2d_on_slot:
+                    cur.wait_event(post_done)  # this slot's previous post-processing read `labels`
                 if isinstance(g, list):
                     # model parts on cur + model_streams, each part's post-processing on
                     # the result stream as soon as its labels exist; cur joins every part
