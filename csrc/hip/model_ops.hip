@@ -1011,6 +1011,67 @@ struct Interval {
     }
   }
 
+  // Per-lane candidates (variant 7): the candidate mask as in emit_union, then each lane
+  // evaluates ITS OWN candidates only. Registers cannot be indexed by a lane-varying class,
+  // so the lane's (v0, dv) pairs go to a private LDS column first ([class][lane] float2:
+  // every read conflict-free whatever the classes) and the candidate loop reads them back
+  // by class. A wave runs max over its lanes of the candidate count (compact 16-row x
+  // 4-interval waves keep the counts alike), instead of the union's class count.
+  template <int NPX>
+  __device__ void emit_cand(uint8_t* op, int K, float2* col) const {
+    const int n = xe - xs;
+    const float t0 = lx(xs), t1 = lx(n > 0 ? xe - 1 : xs);
+    float hi[KP];
+    float L = -3.0e38f, M = 0.f;
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+      const float a = v0[k] + t0 * dv[k], b = v0[k] + t1 * dv[k];
+      const float lo = fminf(a, b);
+      hi[k] = fmaxf(a, b);
+      if (k < K) {
+        L = fmaxf(L, lo);
+        M = fmaxf(M, fmaxf(fabsf(a), fabsf(b)));
+      }
+    }
+    const float thr = L - (M * (1.f / 4096.f) + 1e-30f);
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < KP; ++k)
+      if (k < K && hi[k] >= thr) m |= 1u << k;
+    if (n <= 0) return;
+    if ((m & (m - 1)) == 0) {
+      const uint8_t l = (uint8_t)(__ffs(m) - 1);
+      for (int X = xs; X < xe; ++X) op[X] = l;
+      return;
+    }
+#pragma unroll
+    for (int k = 0; k < KP; ++k) col[k * 256] = make_float2(v0[k], dv[k]);
+    for (int X0 = xs; X0 < xe; X0 += NPX) {
+      float tx[NPX], best[NPX];
+      int arg[NPX];
+#pragma unroll
+      for (int e = 0; e < NPX; ++e) {
+        tx[e] = lx(X0 + e);
+        best[e] = -3.0e38f;
+        arg[e] = 0;
+      }
+      uint32_t mm = m;
+      while (mm) {  // ascending class order, strict compare: the first maximum wins
+        const int k = __ffs(mm) - 1;
+        mm &= mm - 1;
+        const float2 c = col[k * 256];
+#pragma unroll
+        for (int e = 0; e < NPX; ++e) {
+          const float v = c.x + tx[e] * c.y;
+          if (v > best[e]) { best[e] = v; arg[e] = k; }
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < NPX; ++e)
+        if (X0 + e < xe) op[X0 + e] = (uint8_t)arg[e];
+    }
+  }
+
   // Along the interval every class score is LINEAR in lx1, and the max of linear
   // functions is convex: when one class wins at both end pixels it wins at every
   // pixel in between. The common case (smooth logits) then costs two argmaxes
@@ -1076,6 +1137,23 @@ __global__ __launch_bounds__(256) void upsample_argmax_union_kernel(
   iv.template emit_union<16>(labels + ((size_t)b * H + Y) * W, K);
 }
 
+// variant 7: emit_cand on the union kernel's compact waves; a lane's private LDS column
+// holds its (v0, dv) pairs (KP x 8 B per lane: 48 KiB per 256-lane workgroup at KP = 24)
+template <int KP>
+__global__ __launch_bounds__(256) void upsample_argmax_cand_kernel(
+    const bf16* __restrict__ logits, uint8_t* __restrict__ labels, int B, int h, int w, int K,
+    int ldk, int H, int W) {
+  __shared__ float2 cols[KP * 256];
+  const int nyb = (H + 15) >> 4, njb = (w + 3) >> 2;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int jb = wave % njb, yb = (wave / njb) % nyb, b = wave / (njb * nyb);
+  const int Y = yb * 16 + (lane & 15), j = jb * 4 + (lane >> 4);
+  if (b >= B || Y >= H || j >= w) return;  // no wave-wide operation below
+  Interval<KP> iv;
+  iv.load(logits, b, Y, j, h, w, H, W, ldk);
+  iv.template emit_cand<16>(labels + ((size_t)b * H + Y) * W, K, cols + threadIdx.x);
+}
+
 // Row-block variant: a workgroup owns R = 256 / w whole output rows (consecutive in the
 // B*H row space, so one contiguous R*W-byte run of the label buffer). Each lane
 // computes one interval as above into an LDS copy of the rows; the workgroup then
@@ -1121,10 +1199,14 @@ template <int KP>
 void launch_upsample_interval(int variant, const bf16* logits, uint8_t* labels, int B, int h,
                               int w, int K, int ldk, int H, int W, hipStream_t s) {
   const long long total = (long long)B * H * w;
-  if (variant == 6) {
+  if (variant == 6 || variant == 7) {
     const long long waves = (long long)B * ((H + 15) / 16) * ((w + 3) / 4);
-    hipLaunchKernelGGL((upsample_argmax_union_kernel<KP>), dim3(cdiv(waves, 4)), dim3(256), 0, s,
-                       logits, labels, B, h, w, K, ldk, H, W);
+    if (variant == 6)
+      hipLaunchKernelGGL((upsample_argmax_union_kernel<KP>), dim3(cdiv(waves, 4)), dim3(256), 0, s,
+                         logits, labels, B, h, w, K, ldk, H, W);
+    else
+      hipLaunchKernelGGL((upsample_argmax_cand_kernel<KP>), dim3(cdiv(waves, 4)), dim3(256), 0, s,
+                         logits, labels, B, h, w, K, ldk, H, W);
     return;
   }
   if (variant == 1 || variant == 2) {
@@ -1151,12 +1233,13 @@ void launch_upsample_interval(int variant, const bf16* logits, uint8_t* labels, 
 
 // variant: 0 = default (per-lane interval, strict-compare argmax), 1 = interval / compare,
 // 2 = interval / tagged max, 3 = row-block / compare, 4 = row-block / tagged max,
-// 5 = the direct (per-pixel gather) kernel, 6 = interval / wave-union candidates.
-// Variants 1-4 and 6 need the interval preconditions; otherwise the direct kernel runs.
+// 5 = the direct (per-pixel gather) kernel, 6 = interval / wave-union candidates,
+// 7 = interval / per-lane candidates. Variants 1-4, 6 and 7 need the interval
+// preconditions; otherwise the direct kernel runs.
 void upsample_argmax(const bf16* logits, uint8_t* labels, int B, int h, int w, int K, int ldk,
                      int H, int W, hipStream_t s, int variant) {
   if (K > 256) throw std::invalid_argument("upsample_argmax: K > 256");
-  if (variant < 0 || variant > 6) throw std::invalid_argument("upsample_argmax: bad variant");
+  if (variant < 0 || variant > 7) throw std::invalid_argument("upsample_argmax: bad variant");
   if (variant == 0) variant = 1;
   // interval path: at most 32 output pixels share a left source column; the row-block
   // variant needs a whole row of intervals in one workgroup and R * W bytes of LDS

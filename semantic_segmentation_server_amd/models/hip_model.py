@@ -512,7 +512,7 @@ class HipDeepLab:
         ops.append(Choice("upsample", [(name, [lambda *_, h=h, w=w, v=K.UPSAMPLE_VARIANTS[name]:
                                                K.upsample_argmax(
             logits, self._labels_out if self._labels_out is not None else labels, B=B, h=h, w=w,
-            K=self.num_classes, ldk=self.ldk, H=H, W=W, variant=v)]) for name in ("rows", "lane", "union")]))
+            K=self.num_classes, ldk=self.ldk, H=H, W=W, variant=v)]) for name in ("rows", "lane", "union", "cand")]))
         self._plans[key] = (ops, bufs)
         if part == 0:
             self._autotune(ops, B, Hc, Wc)

@@ -1061,7 +1061,7 @@ def aspp_head(cat, packed: dict, out, *, M: int, HW: int, ldo: int, img_bias=Non
     return out
 
 
-UPSAMPLE_VARIANTS = {"rows": 3, "rows_tag": 4, "lane": 1, "lane_tag": 2, "direct": 5, "union": 6}
+UPSAMPLE_VARIANTS = {"rows": 3, "rows_tag": 4, "lane": 1, "lane_tag": 2, "direct": 5, "union": 6, "cand": 7}
 
 
 def upsample_argmax(logits, labels, *, B, h, w, K, ldk, H, W, variant: int = 0):
@@ -1071,7 +1071,7 @@ def upsample_argmax(logits, labels, *, B, h, w, K, ldk, H, W, variant: int = 0):
     _chk(labels, torch.uint8, "labels", B * H * W)
     if K > ldk:
         raise ValueError("K > ldk")
-    if not 0 <= variant <= 6:
+    if not 0 <= variant <= 7:
         raise ValueError(f"bad upsample variant {variant}")
     _hip_mod().upsample_argmax(_ptr(logits), _ptr(labels), B, h, w, K, ldk, H, W, _stream(),
                                variant)

@@ -448,7 +448,7 @@ def test_aspp_pool(B, h, w, C, N):
     assert _rel(ib.cpu(), ref) < 1e-4
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("h,H,K", [(33, 513, 21), (65, 1025, 19), (9, 65, 21), (33, 257, 30)])
 @pytest.mark.parametrize("field", ["noise", "smooth"])
 def test_upsample_argmax(h, H, K, variant, field):
