@@ -1,11 +1,13 @@
 """GPU busy fraction and kernel concurrency of a slot-parallel bench run, from a
-rocprofv3 kernel trace (``--kernel-trace``, csv): over the middle of the run (steady state,
-the start-up / plan build / drain excluded), the share of wall time with at least one
-kernel executing, the mean number of kernels executing, and the time-weighted share of
-each kernel family. Answers whether the step is bound by kernel work (busy ~1) or by gaps
+rocprofv3 kernel trace (``--kernel-trace``, csv): over the last ``count`` steps of the run
+(from the start of the count-th last ``marker`` kernel -- one per step, default the
+post-processing's ``k_records`` -- to the end of the last one: the timed steps, start-up,
+plan build and autotune excluded), the share of wall time with at least one kernel
+executing, the mean number of kernels executing, and the time-weighted share of each
+kernel family. Answers whether the step is bound by kernel work (busy ~1) or by gaps
 (launch, host, event waits).
 
-  python scripts/busy_fraction.py run_kernel_trace.csv [lo_frac hi_frac]
+  python scripts/busy_fraction.py run_kernel_trace.csv [marker] [count]
 """
 import csv
 import sys
@@ -14,14 +16,16 @@ from collections import defaultdict
 
 def main():
     path = sys.argv[1]
-    lo_f = float(sys.argv[2]) if len(sys.argv) > 2 else 0.5
-    hi_f = float(sys.argv[3]) if len(sys.argv) > 3 else 0.9
+    marker = sys.argv[2] if len(sys.argv) > 2 else "k_records"
+    count = int(sys.argv[3]) if len(sys.argv) > 3 else 40
     ks = []
     for r in csv.DictReader(open(path)):
         ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     ks.sort()
-    t0, t1 = ks[0][0], max(k[1] for k in ks)
-    a, b = t0 + (t1 - t0) * lo_f, t0 + (t1 - t0) * hi_f
+    marks = [k for k in ks if marker in k[2]]
+    if len(marks) < count + 1:
+        raise SystemExit(f"only {len(marks)} {marker} kernels in the trace")
+    a, b = marks[-count - 1][1], marks[-1][1]  # count whole steps: end of one marker to the last
     ev = []
     fam = defaultdict(float)
     for s, e, n in ks:
@@ -41,7 +45,7 @@ def main():
         cur += d
         last = t
     span = b - a
-    print(f"window {span / 1e3:.1f} us: busy {busy / span:.3f}, mean kernels in flight "
+    print(f"last {count} steps ({marker}): window {span / 1e3:.1f} us, {span / count / 1e3:.1f} us per step: busy {busy / span:.3f}, mean kernels in flight "
           f"{conc / span:.2f} (while busy {conc / max(busy, 1):.2f})")
     tot = sum(fam.values())
     for n, v in sorted(fam.items(), key=lambda x: -x[1])[:20]:
