@@ -335,7 +335,7 @@ class HipDeepLab:
                 stem_variants = [("fp32", [stem_op])]
                 for tile in ((16, 32), (32, 32)):
                     for dn in (None, dense):
-                        stem_variants.append(((f"densew" if dn is not None else "mfmaw") + f"{tile[0]}x{tile[1]}", [
+                        stem_variants.append((("densew" if dn is not None else "mfmaw") + f"{tile[0]}x{tile[1]}", [
                             lambda frames, lx, ly, x=x, OH=OH, OW=OW, tile=tile, dn=dn: K.stem_mfma(
                                 frames, lx, ly, wpk, sb, x, H=H, W=W, OH=OH, OW=OW, Cout=sc, k=sk, stride=ss,
                                 act=sact, tile=tile, per_wave=True, dense=dn)]))
