@@ -327,6 +327,15 @@ def _spawn_ranks(n: int) -> int:
                    MASTER_PORT=port)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
                                       env=env))
+    import signal
+
+    def _stop(signum, _frame):  # a stopped parent takes its ranks down (exact PIDs)
+        for q in procs:
+            if q.poll() is None:
+                q.terminate()
+        raise SystemExit(128 + signum)
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, _stop)
     rc = 0
     live = list(procs)
     while live:
