@@ -253,16 +253,14 @@ PYBIND11_MODULE(_hip, m) {
   m.def("stem_mfma",
         [](uintptr_t frames, uintptr_t lut_x, uintptr_t lut_y, uintptr_t w, uintptr_t bias,
            uintptr_t out, int B, int Hc, int Wc, int H, int W, int OH, int OW, int Cout, int K,
-           int stride, int act, float out_inv_scale, int TY, int TX, uintptr_t stream, int mode,
-           uintptr_t dense) {
+           int stride, int act, float out_inv_scale, int TY, int TX, uintptr_t stream, int mode) {
           stem_mfma(P<const uint8_t>(frames), P<const int32_t>(lut_x), P<const int32_t>(lut_y),
                     P<const bf16>(w), P<const float>(bias), P<void>(out), B, Hc, Wc, H, W, OH, OW,
-                    Cout, K, stride, act, out_inv_scale, TY, TX, S(stream), mode, P<bf16>(dense));
+                    Cout, K, stride, act, out_inv_scale, TY, TX, S(stream), mode);
         }, py::arg("frames"), py::arg("lut_x"), py::arg("lut_y"), py::arg("w"), py::arg("bias"),
         py::arg("out"), py::arg("B"), py::arg("Hc"), py::arg("Wc"), py::arg("H"), py::arg("W"),
         py::arg("OH"), py::arg("OW"), py::arg("Cout"), py::arg("K"), py::arg("stride"), py::arg("act"),
-        py::arg("out_inv_scale"), py::arg("TY"), py::arg("TX"), py::arg("stream"), py::arg("mode") = 0,
-        py::arg("dense") = 0);
+        py::arg("out_inv_scale"), py::arg("TY"), py::arg("TX"), py::arg("stream"), py::arg("mode") = 0);
   m.def("stem_conv",
         [](uintptr_t frames, uintptr_t lut_x, uintptr_t lut_y, uintptr_t w, uintptr_t bias,
            uintptr_t out, int B, int Hc, int Wc, int H, int W, int OH, int OW, int Cout, int K,

@@ -253,7 +253,7 @@ void depthwise3x3(const bf16* in, const float* w, const float* bias, bf16* out, 
 void stem_mfma(const uint8_t* frames, const int32_t* lut_x, const int32_t* lut_y, const bf16* w,
                const float* bias, void* out, int B, int Hc, int Wc, int H, int W, int OH, int OW,
                int Cout, int K, int stride, int act, float out_inv_scale, int TY, int TX,
-               hipStream_t s, int mode = 0, bf16* dense = nullptr);
+               hipStream_t s, int mode = 0);
 void stem_conv(const uint8_t* frames, const int32_t* lut_x, const int32_t* lut_y, const float* w,
                const float* bias, void* out, int B, int Hc, int Wc, int H, int W, int OH, int OW,
                int Cout, int K, int stride, int act, hipStream_t s, float out_inv_scale = 0.f);

@@ -342,35 +342,8 @@ __global__ __launch_bounds__(256) void stem_mfma_kernel(SMArgs a) {
 // reads of the input fragments (each wave reads every group's), which LDS absorbs; the
 // smaller per-wave state also lets a workgroup own bigger tiles (up to 32 x 32 pixels),
 // which cuts the gathered halo per output pixel.
-// The letterboxed, normalised model input as dense bf16 RGB0 pixels [B][H][W][4] (8 bytes:
-// the stem kernels' LDS layout), each camera pixel gathered through the LUTs ONCE: the
-// tiled stems gather their (2T + K - 2)^2 input halo per T^2 outputs (~5 input pixels per
-// output pixel at the 7x7 / 2 stem), each a LUT load chained to three byte loads. Values
-// are those of gather_letterbox_rgb0 (common.h): -1 in the letterbox, camera / 127.5 - 1.
-__global__ __launch_bounds__(256) void letterbox_rgb0_kernel(const uint8_t* __restrict__ frames,
-                                                             const int32_t* __restrict__ lut_x,
-                                                             const int32_t* __restrict__ lut_y,
-                                                             bf16* __restrict__ out, int B, int Hc,
-                                                             int Wc, int H, int W) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long long)B * H * W) return;
-  const int x = (int)(i % W), y = (int)((i / W) % H), b = (int)(i / ((long long)W * H));
-  const int sy = lut_y[y], sx = lut_x[x];
-  float rgb[3] = {-1.f, -1.f, -1.f};
-  if (sy >= 0 && sx >= 0) {
-    const uint8_t* px = frames + (((size_t)b * Hc + sy) * Wc + sx) * 3;
-    rgb[0] = px[2] * (1.f / 127.5f) - 1.f;
-    rgb[1] = px[1] * (1.f / 127.5f) - 1.f;
-    rgb[2] = px[0] * (1.f / 127.5f) - 1.f;
-  }
-  const bf16x4 v = {(bf16)rgb[0], (bf16)rgb[1], (bf16)rgb[2], (bf16)0.f};
-  *reinterpret_cast<bf16x4*>(out + i * 4) = v;
-}
-
-// DENSE: the tile comes from letterbox_rgb0_kernel's image (8-byte loads along the rows,
-// zeros outside the model input) instead of the per-tile LUT gather.
-template <int KG, bool DENSE>
-__global__ __launch_bounds__(256) void stem_mfma_ws_kernel(SMArgs a, const bf16* __restrict__ dense) {
+template <int KG>
+__global__ __launch_bounds__(256) void stem_mfma_ws_kernel(SMArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* IN = reinterpret_cast<bf16*>(smem);
   const int IHT = (a.TY - 1) * a.stride + a.K, IWT = (a.TX - 1) * a.stride + a.K;
@@ -383,30 +356,8 @@ __global__ __launch_bounds__(256) void stem_mfma_ws_kernel(SMArgs a, const bf16*
   const int sub = __builtin_amdgcn_readfirstlane(tid >> 6);  // this wave's 16 channels
   const int r16 = lane & 15, kq = lane >> 4;
   const float inv_tx = 1.f / a.TX;
-  if (DENSE) {
-    const uint2* src = reinterpret_cast<const uint2*>(dense) + (size_t)b * a.H * a.W;
-    uint2* dst = reinterpret_cast<uint2*>(IN);
-    const int n_in = IHT * IWT;
-    const float inv_iwt = 1.f / IWT;
-    constexpr int U = 8;  // loads in flight per thread
-    for (int i0 = tid; i0 < n_in; i0 += 256 * U) {
-      uint2 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = i0 + u * 256;
-        const int ry = (int)(((float)i + 0.5f) * inv_iwt);  // i / IWT (i < 2^14)
-        const int y = iy0 + ry, x = ix0 + (i - ry * IWT);
-        const bool in = i < n_in && y >= 0 && y < a.H && x >= 0 && x < a.W;
-        v[u] = in ? src[(size_t)y * a.W + x] : make_uint2(0u, 0u);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (i0 + u * 256 < n_in) dst[i0 + u * 256] = v[u];
-    }
-  } else {
-    const uint8_t* fb = a.frames + (size_t)b * a.Hc * a.Wc * 3;
-    gather_letterbox_rgb0<6, 256>(IN, fb, a.lut_x, a.lut_y, a.Wc, a.H, a.W, iy0, ix0, IHT, IWT, tid);
-  }
+  const uint8_t* fb = a.frames + (size_t)b * a.Hc * a.Wc * 3;
+  gather_letterbox_rgb0<6, 256>(IN, fb, a.lut_x, a.lut_y, a.Wc, a.H, a.W, iy0, ix0, IHT, IWT, tid);
   s16x4m wf[KG];
 #pragma unroll
   for (int m = 0; m < KG; ++m)
@@ -459,29 +410,19 @@ __global__ __launch_bounds__(256) void stem_mfma_ws_kernel(SMArgs a, const bf16*
 void stem_mfma(const uint8_t* frames, const int32_t* lut_x, const int32_t* lut_y, const bf16* w,
                const float* bias, void* out, int B, int Hc, int Wc, int H, int W, int OH, int OW,
                int Cout, int K, int stride, int act, float out_inv_scale, int TY, int TX,
-               hipStream_t s, int mode, bf16* dense) {
-  if (mode == 1 || mode == 2) {  // wave per 16-channel block: 7x7 / 64-channel stem only
+               hipStream_t s, int mode) {
+  if (mode == 1) {  // wave per 16-channel block: 7x7 / 64-channel stem only
     if (Cout != 64 || (K * K + 3) / 4 != 13) throw std::invalid_argument("stem_mfma ws: (Cout, K) must be (64, 7)");
     if (TY < 1 || TX < 1 || TY * TX > 1024) throw std::invalid_argument("stem_mfma ws: bad tile");
     const size_t lds = (size_t)((TY - 1) * stride + K) * ((TX - 1) * stride + K) * 8;
     if (lds > 64 * 1024) throw std::invalid_argument("stem_mfma ws: tile too large");
     SMArgs a{frames, lut_x, lut_y, w, bias, out, B, Hc, Wc, H, W, OH, OW, K, stride, act, TY, TX,
              cdiv(OH, TY), cdiv(OW, TX), out_inv_scale};
-    if (mode == 2) {  // letterbox once into the dense image, then dense tiles
-      if (dense == nullptr) throw std::invalid_argument("stem_mfma dense: needs the [B, H, W, 4] bf16 image");
-      const long long npx = (long long)B * H * W;
-      hipLaunchKernelGGL(letterbox_rgb0_kernel, dim3(cdiv(npx, 256)), dim3(256), 0, s, frames, lut_x, lut_y,
-                         dense, B, Hc, Wc, H, W);
-      hipLaunchKernelGGL((stem_mfma_ws_kernel<13, true>), dim3(B * a.tiles_y * a.tiles_x), dim3(256), lds, s,
-                         a, dense);
-    } else {
-      hipLaunchKernelGGL((stem_mfma_ws_kernel<13, false>), dim3(B * a.tiles_y * a.tiles_x), dim3(256), lds, s,
-                         a, nullptr);
-    }
+    hipLaunchKernelGGL((stem_mfma_ws_kernel<13>), dim3(B * a.tiles_y * a.tiles_x), dim3(256), lds, s, a);
     check_launch("stem_mfma ws");
     return;
   }
-  if (mode != 0) throw std::invalid_argument("stem_mfma: mode must be 0, 1 or 2");
+  if (mode != 0) throw std::invalid_argument("stem_mfma: mode must be 0 or 1");
   if (TY < 1 || TX < 1 || TY * TX > 256 || TX > 120) throw std::invalid_argument("stem_mfma: bad tile");
   const int IHT = (TY - 1) * stride + K, IWT = (TX - 1) * stride + K;
   const size_t lds = (size_t)IHT * IWT * 8;

@@ -134,18 +134,13 @@ class HipDeepLabInt8:
                         frames, lx, ly, wpk, self.stem_b, x, H=H, W=W, OH=OH, OW=OW, Cout=c, k=k,
                         stride=st, act="relu", out_scale=S["stem"], tile=tile)]))
             if (c, k) == (64, 7):  # one wave per 16 output channels (26 weight VGPRs, not 104)
-                dense = buf("stem_in", B, H, W, 4, dtype=torch.bfloat16)
+                # (a letterbox pre-pass with dense tiles measured slower: 148.7 vs 127.9 us,
+                # profiles/r8k_stem_prepass_negative.txt)
                 for tile in ((16, 16), (16, 32), (32, 32)):
                     stem_variants.append((f"mfmaw{tile[0]}x{tile[1]}", [
                         lambda frames, lx, ly, x=x, OH=OH, OW=OW, c=c, tile=tile, wpk=wpk: K.stem_mfma(
                             frames, lx, ly, wpk, self.stem_b, x, H=H, W=W, OH=OH, OW=OW, Cout=c, k=k,
                             stride=st, act="relu", out_scale=S["stem"], tile=tile, per_wave=True)]))
-                    # letterbox pre-pass: every camera pixel gathered once, dense tiles
-                    stem_variants.append((f"densew{tile[0]}x{tile[1]}", [
-                        lambda frames, lx, ly, x=x, OH=OH, OW=OW, c=c, tile=tile, wpk=wpk, dense=dense:
-                        K.stem_mfma(frames, lx, ly, wpk, self.stem_b, x, H=H, W=W, OH=OH, OW=OW, Cout=c,
-                                    k=k, stride=st, act="relu", out_scale=S["stem"], tile=tile,
-                                    per_wave=True, dense=dense)]))
         ops.append(Choice("stem", stem_variants))
         PH, PW = conv_out_hw(OH, OW, 3, 2, 1)
         y = buf("pool0", B, PH, PW, c)

@@ -327,18 +327,16 @@ class HipDeepLab:
         h, w, c = OH, OW, sc
         if self.kind == "resnet50":
             if (sc, sk) == (64, 7):
-                # the dense 7x7 stem on bf16 MFMA (one wave per 16 channels), gathering its
-                # tiles through the LUTs or from a letterbox pre-pass image (config 4 bf16)
+                # the dense 7x7 stem on bf16 MFMA, one wave per 16 channels (config 4 bf16:
+                # 792 -> 127 us per 8 frames against the fp32 per-lane kernel, r8k)
                 wpk = K.pack_stem_mfma(sw, sk, sc)
                 bufs["const_stem_wpk"] = wpk
-                dense = buf("stem_in", B, H, W, 4)
                 stem_variants = [("fp32", [stem_op])]
                 for tile in ((16, 32), (32, 32)):
-                    for dn in (None, dense):
-                        stem_variants.append((("densew" if dn is not None else "mfmaw") + f"{tile[0]}x{tile[1]}", [
-                            lambda frames, lx, ly, x=x, OH=OH, OW=OW, tile=tile, dn=dn: K.stem_mfma(
-                                frames, lx, ly, wpk, sb, x, H=H, W=W, OH=OH, OW=OW, Cout=sc, k=sk, stride=ss,
-                                act=sact, tile=tile, per_wave=True, dense=dn)]))
+                    stem_variants.append((f"mfmaw{tile[0]}x{tile[1]}", [
+                        lambda frames, lx, ly, x=x, OH=OH, OW=OW, tile=tile: K.stem_mfma(
+                            frames, lx, ly, wpk, sb, x, H=H, W=W, OH=OH, OW=OW, Cout=sc, k=sk, stride=ss,
+                            act=sact, tile=tile, per_wave=True)]))
                 ops[stem_at] = Choice("stem", stem_variants)
             PH, PW = conv_out_hw(h, w, 3, 2, 1)
             y = buf("pool0", B, PH, PW, c)

@@ -739,12 +739,10 @@ def pack_stem_mfma(w: torch.Tensor, k: int, Cout: int) -> torch.Tensor:
 
 
 def stem_mfma(frames, lut_x, lut_y, wpk, bias, out, *, H, W, OH, OW, Cout, k, stride, act,
-              out_scale=None, tile=(8, 16), per_wave=False, dense=None):
+              out_scale=None, tile=(8, 16), per_wave=False):
     """stem_conv on MFMA (TY x TX output tiles); wpk from ``pack_stem_mfma``.
     ``per_wave``: one wave per 16 output channels over the whole tile (7x7 / 64 channels
-    only; tiles up to 1024 pixels). ``dense`` (per_wave only): a [B, H, W, 4] bf16 buffer
-    that first receives the letterboxed model input (each camera pixel gathered once); the
-    tiles then load it densely. Bit-identical to the gathering form."""
+    only; tiles up to 1024 pixels)."""
     B, Hc, Wc, C3 = frames.shape
     if C3 != 3 or (Cout, k) not in ((64, 7), (32, 3)):
         raise ValueError("stem_mfma: (Cout, k) must be (64, 7) or (32, 3)")
@@ -761,14 +759,9 @@ def stem_mfma(frames, lut_x, lut_y, wpk, bias, out, *, H, W, OH, OW, Cout, k, st
     _chk(wpk, torch.bfloat16, "wpk", Cout * (-(-k * k // 4)) * 16)
     _chk(bias, torch.float32, "bias", Cout)
     _chk(out, torch.int8 if out_scale else torch.bfloat16, "out", B * OH * OW * Cout)
-    if dense is not None:
-        if not per_wave:
-            raise ValueError("stem_mfma: the dense input needs per_wave")
-        _chk(dense, torch.bfloat16, "dense", B * H * W * 4)
     _hip_mod().stem_mfma(_ptr(frames), _ptr(lut_x), _ptr(lut_y), _ptr(wpk), _ptr(bias), _ptr(out), B,
                          Hc, Wc, H, W, OH, OW, Cout, k, stride, ACT[act],
-                         1.0 / out_scale if out_scale else 0.0, ty, tx, _stream(),
-                         2 if dense is not None else int(per_wave), 0 if dense is None else _ptr(dense))
+                         1.0 / out_scale if out_scale else 0.0, ty, tx, _stream(), int(per_wave))
     _dbg('stem_mfma')
     return out
 
