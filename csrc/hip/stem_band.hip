@@ -137,7 +137,8 @@ __global__ __launch_bounds__(64 * NW) void stem_band_kernel(StemBandArgs a) {
     v.c0 = px[0]; v.c1 = px[1]; v.c2 = px[2];
     return v;
   };
-  auto store_px = [&](int rel_row, int u, const Px& v) {
+  // off: the pixel's element offset in the ring (-1: ring row rel_row % 6 computed here)
+  auto store_px = [&](int rel_row, int u, const Px& v, int off = -1) {
     if (gk[u] > 1 || rel_row >= n_rows) return;
     float rgb[3] = {0.f, 0.f, 0.f};
     if (v.kind == 0) {
@@ -148,7 +149,7 @@ __global__ __launch_bounds__(64 * NW) void stem_band_kernel(StemBandArgs a) {
       rgb[0] = rgb[1] = rgb[2] = -1.f;
     }
     const bf16x4 o = {(bf16)rgb[0], (bf16)rgb[1], (bf16)rgb[2], (bf16)0.f};
-    *reinterpret_cast<bf16x4*>(IN + (size_t)(rel_row % 6) * in_row + gi[u] * 4) = o;
+    *reinterpret_cast<bf16x4*>(IN + (off >= 0 ? off : (rel_row % 6) * in_row + gi[u] * 4)) = o;
   };
   // row pair q = ring rows 2q + 1, 2q + 2 (step q's new rows; step 0 also reads row 0)
   Px xr[PD][GPX];
@@ -185,6 +186,20 @@ __global__ __launch_bounds__(64 * NW) void stem_band_kernel(StemBandArgs a) {
     tky[m] = tp < 9 ? tp / 3 : 0;
     toff[m] = (2 * sjc + (tp < 9 ? tp % 3 : 0)) * 4;
   }
+  // ring-row offsets by step phase: the loop's t0 is a multiple of U = 3, so the ring row
+  // (2t + k) % 6 of step t = t0 + ph is (2 ph + k) % 6 -- static per phase; precomputed here
+  // instead of an integer modulo per tap and step (3 stem reads + the gathered rows' stores:
+  // ~40 of the step's ~160 VALU)
+  static_assert(U == 3, "ring offsets assume the 3-step unroll (2 U == the 6-row ring)");
+  int sro[U][3];  // stem fragment reads: (2 ph + tky[m]) % 6 ring row, + toff
+  int sto[U][GPX];  // gathered-row stores of step ph (rows 2 (t + 1) + 1 + gk): ring row, + column
+#pragma unroll
+  for (int ph = 0; ph < U; ++ph) {
+#pragma unroll
+    for (int m = 0; m < 3; ++m) sro[ph][m] = ((2 * ph + tky[m]) % 6) * in_row + toff[m];
+#pragma unroll
+    for (int u = 0; u < GPX; ++u) sto[ph][u] = ((2 * ph + 3 + gk[u]) % 6) * in_row + gi[u] * 4;
+  }
   const int xl = g * 16 + r16;                // local output column (reads stem cols xl..xl+2)
   const bool xv = xl < twv;
   const int xc = xv ? xl : 0;
@@ -205,7 +220,7 @@ __global__ __launch_bounds__(64 * NW) void stem_band_kernel(StemBandArgs a) {
       {
         const int sl = (ph + 1) % PD;
 #pragma unroll
-        for (int u = 0; u < GPX; ++u) store_px(2 * (t + 1) + 1 + gk[u], u, xr[sl][u]);
+        for (int u = 0; u < GPX; ++u) store_px(2 * (t + 1) + 1 + gk[u], u, xr[sl][u], sto[ph][u]);
 #pragma unroll
         for (int u = 0; u < GPX; ++u) xr[sl][u] = fetch_px(2 * (t + 1 + PD) + 1 + gk[u], u);
       }
@@ -216,7 +231,7 @@ __global__ __launch_bounds__(64 * NW) void stem_band_kernel(StemBandArgs a) {
         s16x4 xf[3];
 #pragma unroll
         for (int m = 0; m < 3; ++m)
-          xf[m] = *reinterpret_cast<const s16x4*>(IN + (size_t)((2 * t + tky[m]) % 6) * in_row + toff[m]);
+          xf[m] = *reinterpret_cast<const s16x4*>(IN + sro[ph][m]);
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub) {
           f32x4 e4 = bst[sub];

@@ -30,12 +30,13 @@ CSRC = os.path.join(ROOT, "csrc")
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 ARCH = os.environ.get("SSA_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-# per-source extra flags: MFMA results in VGPRs instead of AGPRs (the kernels whose
-# MFMA epilogues run per fragment on the VALU paid one v_accvgpr_read per result dword)
-EXTRA_FLAGS = {
-    "fused_ir_band.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"],
-    "aspp_head.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"],
-}
+# per-source extra flags (none at present). MFMA results live in VGPRs instead of AGPRs in
+# every source (-amdgpu-mfma-vgpr-form in cflags): kernels whose MFMA epilogues run per
+# fragment on the VALU paid one v_accvgpr_read per result dword and one v_accvgpr_write per
+# accumulator initialisation (stem_band: 12 of ~134 VALU per stem row; conv_gemm: 2,536
+# reads + 4,257 writes in the ISA), and no kernel spills in the VGPR form (round 6, hipcc
+# -Rpass-analysis=kernel-resource-usage: scratch 0 everywhere, occupancy equal or higher)
+EXTRA_FLAGS: dict = {}
 
 
 def _pybind_includes():
@@ -91,7 +92,7 @@ def build_hip(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
     binding = os.path.join(CSRC, "hip", "bindings.cpp")
     out = os.path.join(HERE, "_hip" + EXT_SUFFIX)
     cflags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fno-gpu-rdc",
-              "-Wno-unused-result", "-munsafe-fp-atomics"]
+              "-Wno-unused-result", "-munsafe-fp-atomics", "-mllvm", "-amdgpu-mfma-vgpr-form"]
     if os.environ.get("SSA_PACKED_F32", "0") != "1":
         # no packed-f32 VALU (v_pk_fma/mul/add_f32): under co-residence with other kernels'
         # waves, their low halves came back wrong in lanes 48-63 (scripts/debug_pool.py,
