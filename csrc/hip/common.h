@@ -32,6 +32,12 @@ __device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }
 
 // 16-byte vector load/store of 8 bf16.
 __device__ __forceinline__ bf16x8 ld8(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+// 16 bytes at a uniform base + a 32-bit BYTE offset: the zero-extended 32-bit offset is
+// what lets the compiler pick the SGPR-base + VGPR-offset global addressing form (an
+// element offset is scaled in 64 bits and costs a 64-bit VALU add per access)
+__device__ __forceinline__ bf16x8 ld8_at(const bf16* base, unsigned byte_off) {
+  return *reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(base) + byte_off);
+}
 __device__ __forceinline__ void st8(bf16* p, bf16x8 v) { *reinterpret_cast<bf16x8*>(p) = v; }
 
 __device__ __forceinline__ bf16x8 zero8() {

@@ -172,14 +172,16 @@ __global__ __launch_bounds__(64 * NW * HS) void fused_ir_band_kernel(BandArgs a)
   // for the row just prefetched). No masking is needed: channel-padding lanes read real
   // (finite) channels that meet zero expansion weights, and out-of-image columns are
   // zeroed when E is written; out-of-image rows are never expanded.
+  // per-lane element offsets inside a row (fixed for the kernel) against a uniform row base:
+  // SGPR base + 32-bit VGPR offset per access instead of 64-bit VALU address arithmetic
+  unsigned xoff[GI];
+#pragma unroll
+  for (int k = 0; k < GI; ++k) xoff[k] = (min(max(gcol[k], 0), a.IW - 1) * a.Cin + (kin ? kq * 8 : 0)) * 2u;  // bytes
   auto load_x = [&](int iy, bf16x8* dst) {
     const int iyc = min(max(iy, 0), a.IH - 1);
+    const bf16* row = a.in + ((size_t)b * a.IH + iyc) * a.IW * a.Cin;
 #pragma unroll
-    for (int k = 0; k < GI; ++k) {
-      const int col = min(max(gcol[k], 0), a.IW - 1);
-      const int ch = kin ? kq * 8 : 0;
-      dst[k] = ld8(a.in + (((size_t)b * a.IH + iyc) * a.IW + col) * a.Cin + ch);
-    }
+    for (int k = 0; k < GI; ++k) dst[k] = ld8_at(row, xoff[k]);
   };
 
   f16x8 D[NDS][NCHH];
@@ -193,19 +195,22 @@ __global__ __launch_bounds__(64 * NW * HS) void fused_ir_band_kernel(BandArgs a)
   int pend_o = -1, pend_buf = 0;
   auto store_row = [&](int o, const f32x4 (&acc)[NS]) {
     if (!xv) return;
-    const size_t opix = ((size_t)b * a.OH + o) * a.OW + x0 + xl;
+    const size_t orow = ((size_t)b * a.OH + o) * a.OW;  // uniform
+    const int px = x0 + xl;
+    const bf16* rrow = a.in + orow * a.Cin;
+    bf16* wrow = a.out + orow * a.Cout;
 #pragma unroll
     for (int n = 0; n < NS; ++n) {
       const int ch = n * 16 + kq * 4;
       if (ch >= a.Cout) continue;
       f32x4 v = acc[n];
       if (a.residual) {  // stride 1, Cin == Cout: same pixel of the input
-        const bf16x4 r = *reinterpret_cast<const bf16x4*>(a.in + opix * a.Cin + ch);
+        const bf16x4 r = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const char*>(rrow) + (unsigned)(px * a.Cin + ch) * 2u);
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] += (float)r[q];
       }
       const bf16x4 ob = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-      *reinterpret_cast<bf16x4*>(a.out + opix * a.Cout + ch) = ob;
+      *reinterpret_cast<bf16x4*>(reinterpret_cast<char*>(wrow) + (unsigned)(px * a.Cout + ch) * 2u) = ob;
     }
   };
   auto flush_pending = [&]() {  // first half, behind a barrier after the exchange write

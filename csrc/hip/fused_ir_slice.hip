@@ -150,16 +150,21 @@ __global__ __launch_bounds__(64 * NW * NCH) void fused_ir_slice_kernel(SliceArgs
   __syncthreads();  // (the only full barrier: no global store is pending yet)
 
   const bool kin = kq * 8 < a.Cin;
+  // per-lane element offsets inside a row, fixed for the kernel: the row base is uniform
+  // (a scalar 64-bit pointer), so every load / store below is SGPR base + 32-bit VGPR
+  // offset -- no per-access 64-bit address arithmetic on the VALU (~120 of the unrolled
+  // loop's ~410 VALU were address math)
+  unsigned xoff[GI];
+#pragma unroll
+  for (int k = 0; k < GI; ++k) xoff[k] = (min(max(gcol[k], 0), a.IW - 1) * a.Cin + (kin ? kq * 8 : 0)) * 2u;  // bytes
   bf16x8 xq[PD][GI];
   auto load_x = [&](int iy, bf16x8* dst) {
     // clamped, branch-free: padding-channel lanes read real channels that meet zero
     // expansion weights; out-of-image rows are never expanded
     const int iyc = min(max(iy, 0), a.IH - 1);
+    const bf16* row = a.in + ((size_t)b * a.IH + iyc) * a.IW * a.Cin;
 #pragma unroll
-    for (int k = 0; k < GI; ++k) {
-      const int col = min(max(gcol[k], 0), a.IW - 1);
-      dst[k] = ld8(a.in + (((size_t)b * a.IH + iyc) * a.IW + col) * a.Cin + (kin ? kq * 8 : 0));
-    }
+    for (int k = 0; k < GI; ++k) dst[k] = ld8_at(row, xoff[k]);
   };
 
   f16x8 D[NDS];
@@ -181,14 +186,15 @@ __global__ __launch_bounds__(64 * NW * NCH) void fused_ir_slice_kernel(SliceArgs
     }
     const int ch = c * 16 + kq * 4;
     if (!xv || ch >= a.Cout) return;
-    const size_t opix = ((size_t)b * a.OH + o) * a.OW + x0 + xl;
+    const size_t orow = ((size_t)b * a.OH + o) * a.OW;  // uniform
+    const int px = x0 + xl;
     if (a.residual) {  // stride 1, Cin == Cout: the same pixel of the input
-      const bf16x4 r = *reinterpret_cast<const bf16x4*>(a.in + opix * a.Cin + ch);
+      const bf16x4 r = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const char*>(a.in + orow * a.Cin) + (unsigned)(px * a.Cin + ch) * 2u);
 #pragma unroll
       for (int q = 0; q < 4; ++q) acc[q] += (float)r[q];
     }
     const bf16x4 ob = {(bf16)acc[0], (bf16)acc[1], (bf16)acc[2], (bf16)acc[3]};
-    *reinterpret_cast<bf16x4*>(a.out + opix * a.Cout + ch) = ob;
+    *reinterpret_cast<bf16x4*>(reinterpret_cast<char*>(a.out + orow * a.Cout) + (unsigned)(px * a.Cout + ch) * 2u) = ob;
   };
 
   const int iy0 = y0 * S - 1;

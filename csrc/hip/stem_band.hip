@@ -133,7 +133,9 @@ __global__ __launch_bounds__(64 * NW) void stem_band_kernel(StemBandArgs a) {
     const int sx = gsx[u];
     Px v;
     v.kind = (gk[u] > 1 || rel_row >= n_rows || sy == -2 || sx == -2) ? -2 : (sy < 0 || sx < 0) ? -1 : 0;
-    const uint8_t* px = fb + ((size_t)max(sy, 0) * a.Wc + max(sx, 0)) * 3;
+    // 32-bit byte offset from the uniform frame base (a frame is < 4 GiB): SGPR base +
+    // VGPR offset addressing, no 64-bit multiply-add per pixel
+    const uint8_t* px = fb + (unsigned)((max(sy, 0) * a.Wc + max(sx, 0)) * 3);
     v.c0 = px[0]; v.c1 = px[1]; v.c2 = px[2];
     return v;
   };
@@ -263,7 +265,8 @@ __global__ __launch_bounds__(64 * NW) void stem_band_kernel(StemBandArgs a) {
           f32x4 acc = {0.f, 0.f, 0.f, 0.f};
           acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, d, acc, 0, 0, 0);
           if (xv) {
-            bf16* op = a.out + (((size_t)b * a.SH + o) * a.SW + x0 + xl) * 16 + kq * 4;
+            bf16* orow = a.out + ((size_t)b * a.SH + o) * a.SW * 16;  // uniform
+            bf16* op = reinterpret_cast<bf16*>(reinterpret_cast<char*>(orow) + (unsigned)(((x0 + xl) * 16 + kq * 4) * 2));
             const bf16x4 ob = {(bf16)(acc[0] + bpv[0]), (bf16)(acc[1] + bpv[1]), (bf16)(acc[2] + bpv[2]),
                                (bf16)(acc[3] + bpv[3])};
             *reinterpret_cast<bf16x4*>(op) = ob;
