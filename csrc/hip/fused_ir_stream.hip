@@ -54,6 +54,7 @@ __host__ __device__ constexpr int stream_waves(int mode) { return (mode & 3) == 
 constexpr int kHdr = 4;    // span table header: p0, p1, wy0, nh
 constexpr int kXQ = 5;     // halo groups per expansion wave (<= 20 groups = 320 halo px)
 constexpr int kGB = 3;     // output groups per depthwise+projection wave (<= 12 groups)
+constexpr int kSpanPx = 9 * 16;  // output pixels per span at most (4 waves x 2 groups + group 8)
 // chunk-image ring slots: 4 (DMA two chunks ahead) or, for Cout 320 (31 KiB chunk images), 3
 __host__ __device__ constexpr int stream_nsl(int NS) { return NS > 10 ? 3 : 4; }
 // epilogue passes over Cout (the fp32 output tile of a 144-pixel span at Cout 320 would
@@ -289,6 +290,13 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
   // 4 slots: 72 instead of 81 KiB for blocks 7-9, so two workgroups -- of one plan copy or of
   // two slots' concurrent steps -- can share a CU's 160 KiB of LDS
   constexpr bool G8A = (MODE & 3) == 1;
+  // MODE & 8: lattice spans (ops/fused_span.lattice_table): a dilation-2 layer run on the
+  // phase-class lattice, where its taps are dilation-1 taps (DIL = 1 here) and a span's halo
+  // is +- 1 lattice row: 1.22x instead of 1.87x of the output pixels expanded at 33^2, S = 8.
+  // The span's output pixels and their window centres come from the table's output list;
+  // p0 = 0 and p1 = the span's length, so "span pixel" px is output-list entry px.
+  constexpr bool LAT = (MODE & 8) != 0;
+  __shared__ int s_opix[LAT ? kSpanPx : 1];  // output-list pixel indices (epilogue)
   constexpr int kNW = stream_waves(MODE), kNT = 64 * kNW;
   constexpr int NPC = 2 * KS + NS + 1;          // 1 KiB pieces per chunk image
   constexpr int CHB = NPC * 1024;
@@ -332,6 +340,9 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
 
   // ---- prologue: X fragments (A waves), first LAG chunk images, E zeroed (padding taps)
   const int dummy = a.WR * WCP - 1;  // window slot never read by the depthwise
+  const int olist = a.hstride - kSpanPx;  // LAT: output list offset in the span's row
+  if (LAT)
+    for (int i = tid; i < p1 - p0; i += kNT) s_opix[i] = tb[olist + i] >> 12;  // visible after the prologue barrier
   // ONE register array for both roles: the expansion waves keep their X fragments in it,
   // the depthwise+projection waves their fp32 accumulators (the allocator does not share
   // two role-private arrays by itself: 190..256 VGPRs + spills against max(A, BC))
@@ -390,8 +401,12 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
     const int p = p0 + (expander ? 8 : og[g]) * 16 + r16;  // G8A: expansion waves own group 8
     dpos[g] = d * WCP + d;  // padding lanes: any in-window centre
     if (p < p1) {
-      const int y = p / a.W, x = p - (p / a.W) * a.W;
-      dpos[g] = (y - wy0) * WCP + x + d;
+      if (LAT) {
+        dpos[g] = tb[olist + p] & 4095;
+      } else {
+        const int y = p / a.W, x = p - (p / a.W) * a.W;
+        dpos[g] = (y - wy0) * WCP + x + d;
+      }
     }
   }
   const int dpos8[1] = {dpos[0]};
@@ -453,10 +468,11 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
       const char* Wp = ring + (c % kNSL) * CHB + WEB;
       if ((MODE & 3) == 2) {
         const char* Ek = sE + (c & 1) * 4 * PLANE + kq * PLANE;
-        dwproj_groups<1, NS, DIL, WCP, NR>(Wp, Wp + WPB, Ek, dpos8, 0, NS - 1, R, 0, lane, kq);
+        // Cout 160 (lattice blocks 14-15): the register-lean depthwise, so 12 waves fit 168 VGPRs
+        dwproj_groups<1, NS, DIL, WCP, NR, true, (NS > 6)>(Wp, Wp + WPB, Ek, dpos8, 0, NS - 1, R, 0, lane, kq);
         if (bw == 7) {
           const int dposn[1] = {dpos[1]};
-          dwproj_groups<1, NS, DIL, WCP, NR>(Wp, Wp + WPB, Ek, dposn, 0, NS - 1, R, NS, lane, kq);
+          dwproj_groups<1, NS, DIL, WCP, NR, true, (NS > 6)>(Wp, Wp + WPB, Ek, dposn, 0, NS - 1, R, NS, lane, kq);
         }
       } else if (G8A)
         dwproj_groups<2, NS, DIL, WCP, NR, (NS <= 10 && !LEAN), (LEAN && NS > 10)>(Wp, Wp + WPB, sE + (c & 1) * 4 * PLANE + kq * PLANE, dpos01, 0,
@@ -512,32 +528,33 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
     const int C8 = NSP * 2, c0 = h * NSP * 16;  // 8-channel units per pixel in the slice
     const int units = (p1 - p0) * C8;
     if (a.HS > 1) {  // fp32 partial of this hidden slice, bias / residual added by the combine
-      float* pb = a.part + ((size_t)hs * a.B * HW + (size_t)b * HW + p0) * a.Cout + c0;
+      float* pb = a.part + ((size_t)hs * a.B * HW + (size_t)b * HW) * a.Cout + c0;
       for (int u = tid; u < units; u += kNT) {
         const int px = u / C8, c = (u - px * C8) * 8;
-        float* q = pb + (size_t)px * a.Cout + c;
+        float* q = pb + (size_t)(LAT ? s_opix[px] : p0 + px) * a.Cout + c;
         *reinterpret_cast<f32x4*>(q) = *reinterpret_cast<const f32x4*>(O + px * OS + c);
         *reinterpret_cast<f32x4*>(q + 4) = *reinterpret_cast<const f32x4*>(O + px * OS + c + 4);
       }
       continue;
     }
-    bf16* outb = a.out + ((size_t)b * HW + p0) * a.Cout + c0;
-    const bf16* resb = inb + (size_t)p0 * a.Cin + c0;
+    bf16* outb = a.out + (size_t)b * HW * a.Cout + c0;
+    const bf16* resb = inb + c0;
     for (int u = tid; u < units; u += kNT) {
       const int px = u / C8, c = (u - px * C8) * 8;
+      const int gp = LAT ? s_opix[px] : p0 + px;  // the pixel's index in the image
       const f32x4 o0 = *reinterpret_cast<const f32x4*>(O + px * OS + c);
       const f32x4 o1 = *reinterpret_cast<const f32x4*>(O + px * OS + c + 4);
       const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bp + c0 + c);
       const f32x4 b1 = *reinterpret_cast<const f32x4*>(a.bp + c0 + c + 4);
       bf16x8 r = zero8();
-      if (a.residual) r = ld8(resb + (size_t)px * a.Cin + c);
+      if (a.residual) r = ld8(resb + (size_t)gp * a.Cin + c);
       bf16x8 o;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         o[q] = (bf16)(o0[q] + b0[q] + (float)r[q]);
         o[q + 4] = (bf16)(o1[q] + b1[q] + (float)r[q + 4]);
       }
-      st8(outb + (size_t)px * a.Cout + c, o);
+      st8(outb + (size_t)gp * a.Cout + c, o);
     }
   }
   if (a.HS > 1 && a.cnt) {
@@ -565,18 +582,19 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
     if (*reinterpret_cast<volatile int*>(s_flag)) {
       const int C8 = a.Cout / 8, units = (p1 - p0) * C8;
       const size_t slab = (size_t)a.B * HW * a.Cout;
-      const float* pb = a.part + ((size_t)b * HW + p0) * a.Cout;
-      bf16* outb = a.out + ((size_t)b * HW + p0) * a.Cout;
-      const bf16* resb = inb + (size_t)p0 * a.Cin;
+      const float* pb = a.part + (size_t)b * HW * a.Cout;
+      bf16* outb = a.out + (size_t)b * HW * a.Cout;
+      const bf16* resb = inb;
       for (int u = tid; u < units; u += kNT) {
         const int px = u / C8, c = (u - px * C8) * 8;
+        const int gp = LAT ? s_opix[px] : p0 + px;
         f32x4 s0 = *reinterpret_cast<const f32x4*>(a.bp + c), s1 = *reinterpret_cast<const f32x4*>(a.bp + c + 4);
-        const float* q = pb + (size_t)px * a.Cout + c;
+        const float* q = pb + (size_t)gp * a.Cout + c;
         // the slabs' loads (and the residual's) issued kCombineHS at a time before their adds:
         // one L2 round trip per group instead of one per slab (as stream_combine_kernel's HSM
         // form; slabs past HS re-read the last one and are not added; order h = 0..HS-1)
         bf16x8 r = zero8();
-        if (a.residual) r = ld8(resb + (size_t)px * a.Cin + c);
+        if (a.residual) r = ld8(resb + (size_t)gp * a.Cin + c);
         for (int h0 = 0; h0 < a.HS; h0 += kCombineHS) {
           f32x4 v0[kCombineHS], v1[kCombineHS];
 #pragma unroll
@@ -598,7 +616,7 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
           o[e] = (bf16)(s0[e] + (float)r[e]);
           o[e + 4] = (bf16)(s1[e] + (float)r[e + 4]);
         }
-        st8(outb + (size_t)px * a.Cout + c, o);
+        st8(outb + (size_t)gp * a.Cout + c, o);
       }
     }
   }
@@ -608,11 +626,13 @@ __global__ __launch_bounds__(64 * stream_waves(MODE)) void fused_ir_stream_kerne
 template <int KS, int NS, int XQ, int DIL, int WCP, int MODE>
 void launch_stream(const StreamArgs& a, hipStream_t st) {
   const size_t lds = fused_ir_stream_lds(a.Cin, a.Cout, a.WR, a.WCP, (MODE & 4) ? 3 : 0);
-  if (lds > 160 * 1024) throw std::invalid_argument("fused_ir_stream: LDS over 160 KiB");
+  // the lattice form's static output-list array (s_opix) shares the CU's 160 KiB
+  constexpr size_t kStatic = (MODE & 8) ? kSpanPx * sizeof(int) : 64;
+  if (lds > 160 * 1024 - kStatic) throw std::invalid_argument("fused_ir_stream: LDS over 160 KiB");
   static bool attr = false;
   if (!attr) {
     check(hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_ir_stream_kernel<KS, NS, XQ, DIL, WCP, MODE>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - kStatic),
           "fused_ir_stream attr");
     attr = true;
   }
@@ -635,8 +655,12 @@ void fused_ir_stream(const FusedSpanParams& p, hipStream_t st) {
   if (p.Cin % 32 || p.Cout % 16 || p.hidP % 32 || p.hidP <= 0)
     throw std::invalid_argument("fused_ir_stream: Cin % 32, Cout % 16, hidP % 32");
   if (p.residual && p.Cin != p.Cout) throw std::invalid_argument("fused_ir_stream: residual needs Cin == Cout");
-  if (p.dil < 1 || 2 * p.dil + 1 > 16 || p.WCP != p.W + 16 || p.WR < 2 * p.dil + 1 || p.WR * p.WCP > 4096)
+  const bool lat = (p.npi & 8) != 0;  // lattice spans (dilation 2 as dilation-1 taps)
+  if (lat ? (p.dil != 2 || p.WCP != (p.W + 1) / 2 + 3 || p.WR < 3 || p.WR * p.WCP > 4096)
+          : (p.dil < 1 || 2 * p.dil + 1 > 16 || p.WCP != p.W + 16 || p.WR < 2 * p.dil + 1 || p.WR * p.WCP > 4096))
     throw std::invalid_argument("fused_ir_stream: bad window geometry");
+  if (lat && (p.hstride < kHdr + kSpanPx || p.nh_max > 3 * 64))
+    throw std::invalid_argument("fused_ir_stream: lattice table needs an output list and <= 192 halo px");
   if (p.S < 1 || (p.H * p.W + p.S - 1) / p.S > kGB * 4 * 16) throw std::invalid_argument("fused_ir_stream: span too long");
   if (p.H * p.W >= (1 << 19)) throw std::invalid_argument("fused_ir_stream: map too large for the halo table");
   if (p.nh_max > kXQ * 4 * 16) throw std::invalid_argument("fused_ir_stream: halo over 320 pixels");
@@ -653,13 +677,32 @@ void fused_ir_stream(const FusedSpanParams& p, hipStream_t st) {
   // an unknown variant, or the 12-wave variant where it is not instantiated, must not
   // silently launch another kernel under the requested name
   // variants: 0 / 1 (G8A) / 2 (12 waves); + 4: the 3-slot chunk ring (blocks with NS <= 10)
-  if (!(p.npi == 0 || p.npi == 1 || p.npi == 2 || p.npi == 4 || p.npi == 6))
-    throw std::invalid_argument("fused_ir_stream: variant must be 0, 1, 2, 4 or 6");
+  // + 8: lattice spans (blocks 14-16: Cin 160, dilation 2), variants 0 / 1 / 4
+  if (!(p.npi == 0 || p.npi == 1 || p.npi == 2 || p.npi == 4 || p.npi == 6 || p.npi == 8 || p.npi == 9 ||
+        p.npi == 10 || p.npi == 12))
+    throw std::invalid_argument("fused_ir_stream: variant must be 0, 1, 2, 4, 6 (+ 8 for lattice: 8, 9, 10, 12)");
+  if (lat) {
+    // window pitch 17 + 3 at W = 33; 3 halo rounds per expansion wave (<= 192 px)
+    if (KS == 5 && NS == 10) {
+      if (p.npi == 9) launch_stream<5, 10, 3, 1, 20, 9>(a, st);
+      else if (p.npi == 10) launch_stream<5, 10, 3, 1, 20, 10>(a, st);
+      else if (p.npi == 12) launch_stream<5, 10, 3, 1, 20, 12>(a, st);
+      else launch_stream<5, 10, 3, 1, 20, 8>(a, st);
+      return;
+    }
+    if (KS == 5 && NS == 20 && p.npi == 9) {
+      launch_stream<5, 20, 3, 1, 20, 9>(a, st);
+      return;
+    }
+    throw std::invalid_argument("fused_ir_stream: lattice instantiations: 160->160 (8, 9, 10, 12), 160->320 (9)");
+  }
   if ((p.npi & 3) == 2 && (p.dil != 1 || NS > 6))
     throw std::invalid_argument("fused_ir_stream: the 12-wave variant needs dilation 1 and Cout <= 96");
   if ((p.npi & 4) && NS > 10)
     throw std::invalid_argument("fused_ir_stream: the 3-slot variant is for Cout <= 160 (wider blocks use 3 slots)");
-  // 12-wave variant: blocks 7-12 (Cout <= 96; at Cout 160 the accumulators spill at 168 VGPRs)
+  // 12-wave variant: blocks 7-12 (Cout <= 96; at Cout 160 the accumulators spill at 168 VGPRs
+  // even with the register-lean depthwise -- block 13: 8 spills; the lattice form of blocks
+  // 14-15 fits, its expansion waves hold 3 halo rounds instead of 4-5)
 #define STREAM12(K_, N_) ((N_) <= 6 ? 2 : 0)
 #define STREAM(K_, N_)                                   \
   if (KS == K_ && NS == N_) {                            \

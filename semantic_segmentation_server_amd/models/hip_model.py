@@ -706,6 +706,32 @@ class HipDeepLab:
         if blk["expand"] is not None and s.stride == 1 and (s.cin, s.cout) in FS.STREAM_SHAPES:
             # expanded tensor kept on chip: raster spans of ~h*w/S pixels per workgroup
             for S in self._span_counts(B, h, w):
+                if FS.stream_supported(s.cin, s.cout, 1, h, w, S, s.dilation, lattice=True):
+                    # dilation 2 on the phase-class lattice: halo +- 1 lattice row (ops/fused_span
+                    # .lattice_table), 3 halo rounds per expansion wave instead of 5
+                    if "span" not in blk:
+                        blk["span"] = self._pack_span(blk, s)
+                    ltab = self._span_table(h, w, S, s.dilation, lattice=True)
+                    for v in ((0, 1, 2, 4) if s.cout <= 160 else (1,)):
+                        variants.insert(0, (f"stream{S}" + {0: "", 1: "g", 2: "w", 4: "r3"}[v] + "L", [
+                            lambda *_, x=inp, out=out, tab=ltab, sp=blk["span"], v=v: FS.fused_ir_stream(
+                                x, sp, tab, out, B=B, residual=s.residual, variant=v)]))
+                    nc = -(-hid // 32)
+                    hs_opts = [hs for hs in (2, 3, 4, 6) if hs <= nc and B * S * hs <= 512] if B <= 16 else []
+                    if hs_opts:
+                        key = f"b{i}_part"
+                        if key not in bufs_part:
+                            bufs_part[key] = buf(key, max(hs_opts) * B * h * w * s.cout, dtype=torch.float32)
+                        part = bufs_part[key]
+                        cnt = buf(f"b{i}_cnt{S}", B * S, dtype=torch.int32)
+                        v = 0 if s.cout <= 160 else 1
+                        for hs in hs_opts:
+                            for inl in (False, True):
+                                variants.insert(0, (f"stream{S}Lh{hs}" + ("c" if inl else ""), [
+                                    lambda *_, x=inp, out=out, tab=ltab, sp=blk["span"], v=v, hs=hs, part=part,
+                                    cnt=(cnt if inl else None): FS.fused_ir_stream(
+                                        x, sp, tab, out, B=B, residual=s.residual, variant=v, hsplit=hs,
+                                        part=part, cnt=cnt)]))
                 if FS.stream_supported(s.cin, s.cout, 1, h, w, S, s.dilation):
                     if "span" not in blk:
                         blk["span"] = self._pack_span(blk, s)
@@ -821,10 +847,10 @@ class HipDeepLab:
             out.append(4 * s0)
         return out
 
-    def _span_table(self, h: int, w: int, S: int, dil: int):
-        key = (h, w, S, dil)
+    def _span_table(self, h: int, w: int, S: int, dil: int, lattice: bool = False):
+        key = (h, w, S, dil, lattice)
         if key not in self._span_tables:
-            self._span_tables[key] = FS.span_table(h, w, S, dil, self.device)
+            self._span_tables[key] = (FS.lattice_table if lattice else FS.span_table)(h, w, S, dil, self.device)
         return self._span_tables[key]
 
     def _pack_span(self, blk: dict, s) -> dict:

@@ -1689,6 +1689,62 @@ def test_fused_ir_stream(cin, cout, dil, H, S):
             assert int(cnt.abs().sum()) == 0, (hs, rep)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("cout,H,S", [
+    (160, 33, 8),    # blocks 14-15 at the headline span count (residual)
+    (160, 33, 16),   # batch-1 span counts
+    (320, 33, 8),    # block 16 (two epilogue passes, group 8 on the expansion waves)
+    (160, 21, 5),    # odd map height: classes of 11 / 10 rows, spans across class seams
+])
+def test_fused_ir_stream_lattice(cout, H, S):
+    """Dilation-2 blocks on lattice spans (variant bit 8): vs the fp32 torch block, vs the
+    numpy re-execution of the lattice data flow, and bit-identical to the raster-span
+    kernel (same fp16 depthwise chain per pixel, same fp32 projection order); the hidden
+    split (stream_combine and in-launch combine) writes the same bytes."""
+    from semantic_segmentation_server_amd.ops import fused_span as FS
+    from test_fused_span_cpu import _block, pack_block
+    cin, dil, W = 160, 2, 33
+    assert FS.stream_supported(cin, cout, 1, H, W, S, dil, lattice=True)
+    blk, spec = _block(cin, cout, dil, seed=cin * 3 + cout + H)
+    g = torch.Generator().manual_seed(29)
+    B = 3
+    x = torch.randn(B, cin, H, W, generator=g).to(torch.bfloat16)
+    with torch.no_grad():
+        ref = blk(x.float())
+    packed = pack_block(blk, spec, device=DEV)
+    lt = FS.lattice_table(H, W, S, dil, DEV)
+    rt = FS.span_table(H, W, S, dil, DEV)
+    xd = _nhwc(x).to(DEV)
+    emu = FS.emulate_fused_span(_nhwc(x).float().numpy(), packed, lt, residual=spec.residual)
+    raster = torch.full((B, H, W, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
+    FS.fused_ir_stream(xd, packed, rt, raster, B=B, residual=spec.residual, variant=1)
+    for variant in ((0, 1, 2, 4) if cout <= 160 else (1,)):
+        out = torch.full((B, H, W, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
+        FS.fused_ir_stream(xd, packed, lt, out, B=B, residual=spec.residual, variant=variant)
+        torch.cuda.synchronize()
+        assert torch.isfinite(out).all(), variant
+        assert _rel(_nchw(out).cpu(), ref) < 2e-2, variant
+        assert _rel(out.cpu().float(), torch.from_numpy(emu)) < 5e-3, variant
+        assert torch.equal(out.view(torch.int16), raster.view(torch.int16)), variant
+    nc = packed["hidP"] // 32
+    v = 0 if cout <= 160 else 1
+    for hs in (2, 4):
+        part = torch.full((hs * B * H * W * cout,), float("nan"), dtype=torch.float32, device=DEV)
+        out = torch.full((B, H, W, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
+        FS.fused_ir_stream(xd, packed, lt, out, B=B, residual=spec.residual, variant=v, hsplit=hs, part=part)
+        torch.cuda.synchronize()
+        assert torch.isfinite(out).all(), hs
+        assert _rel(_nchw(out).cpu(), ref) < 2e-2, hs
+        cnt = torch.zeros(B * S, dtype=torch.int32, device=DEV)
+        out3 = torch.full_like(out, float("nan"))
+        FS.fused_ir_stream(xd, packed, lt, out3, B=B, residual=spec.residual, variant=v, hsplit=hs, part=part,
+                           cnt=cnt)
+        torch.cuda.synchronize()
+        assert torch.equal(out.view(torch.int16), out3.view(torch.int16)), hs
+        assert int(cnt.abs().sum()) == 0, hs
+    assert nc >= 4
+
+
 @pytest.mark.parametrize("M,HW,ncls,ldo,img", [
     (32 * 33 * 33, 33 * 33, 21, 24, True),   # the B = 32 headline head (G = 9)
     (33 * 33, 33 * 33, 21, 24, True),        # batch 1 (G = 1)
