@@ -490,7 +490,10 @@ void maxpool3x3s2(const bf16* in, bf16* out, int B, int IH, int IW, int C, int O
 // channel blocks); each lane owns 8 channels, the 4 waves of a block split the
 // slice's pixels and reduce through LDS into part[b][slice][C]; a tiny second
 // kernel sums the slices (deterministic, no float atomics).
-constexpr int kGapSlices = 16;
+// 32 slices and four 16-byte loads in flight per lane: with 16 slices and one load per
+// iteration each wave walked 17 pixels through 17 dependent L2/HBM round trips (10 us at
+// B = 32, 8 us at B = 1 where the grid is only 16 workgroups: r8l / r8p step traces).
+constexpr int kGapSlices = 32;
 
 __global__ __launch_bounds__(256) void gap_partial_kernel(const bf16* __restrict__ in,
                                                           float* __restrict__ part, int HW, int C) {
@@ -503,7 +506,17 @@ __global__ __launch_bounds__(256) void gap_partial_kernel(const bf16* __restrict
   const int p0 = (int)((long long)HW * sl / kGapSlices), p1 = (int)((long long)HW * (sl + 1) / kGapSlices);
   if (cg < CG) {
     const bf16* base = in + (long long)b * HW * C + cg * 8;
-    for (int p = p0 + wid; p < p1; p += 4) {
+    int p = p0 + wid;
+    for (; p + 12 < p1; p += 16) {  // this wave's next 4 pixels: all loads issued first
+      bf16x8 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = ld8(base + (long long)(p + 4 * u) * C);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] += (float)v[u][q];
+    }
+    for (; p < p1; p += 4) {
       const bf16x8 v = ld8(base + (long long)p * C);
 #pragma unroll
       for (int q = 0; q < 8; ++q) acc[q] += (float)v[q];
