@@ -371,9 +371,9 @@ def test_gloo_record_gather_cost_world8():
     print(f"gloo gather world 8, 41 KB/rank: p50 {p50 * 1e3:.3f} ms p90 {p90 * 1e3:.3f} ms")
     # with a core per rank and its gloo threads (an MI355X node; the 16-CPU GPU box
     # measured p50 0.295 ms, profiles/r2_pg_ab.txt) the gather is a fifth of the step;
-    # an 8-CPU container running 8 busy ranks is contention-bound (p50 ~2 ms), so there
-    # only a sanity bound applies
-    bound = 0.7e-3 if (os.cpu_count() or 1) >= 2 * world else 10e-3
+    # an 8-CPU container running 8 busy ranks is contention-bound (p50 ~2 ms alone, 10.4 ms
+    # next to other test workers under pytest -n 4), so there only a sanity bound applies
+    bound = 0.7e-3 if (os.cpu_count() or 1) >= 2 * world else 25e-3
     assert p50 < bound, p50
 
 
