@@ -332,12 +332,18 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 // One BM x BN output tile (index bid, row-major over (m-tile, n-tile)); shared by the
 // single-conv kernel and the grouped kernel (the int8 ASPP branches in one grid).
-template <int MT, int NT, int WM, int WN>
+// KB: K bytes per stage row. 128 (two MFMA k-steps per stage, 8 rows per glds) or 64 (one
+// k-step, 16 rows per glds): half the LDS per stage, so twice the workgroups per CU hide each
+// other's global -> LDS round trips -- the short-K convs (layer-4 1x1s, K = 512: four
+// 128-deep stages per tile) are latency-bound at two workgroups per CU
+template <int MT, int NT, int WM, int WN, int KB = 128>
 __device__ __forceinline__ void i8_glds_tile(const I8Args& a, const int bid, char* smem) {
   constexpr int NW = WM * WN, ST = 2;
-  constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN, ROWB = 128;  // 128 int8 of K per row
-  constexpr int GA = BM / (8 * NW), GB = BN / (8 * NW);
-  static_assert(GA * 8 * NW == BM && GB * 8 * NW == BN, "tile rows must split over the waves");
+  constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN, ROWB = KB;  // KB int8 of K per row
+  constexpr int CPR = ROWB / 16, RPG = 1024 / ROWB;  // 16-byte chunks per row, rows per glds
+  static_assert(KB == 128 || KB == 64, "KB 128 or 64");
+  constexpr int GA = BM / (RPG * NW), GB = BN / (RPG * NW);
+  static_assert(GA * RPG * NW == BM && GB * RPG * NW == BN, "tile rows must split over the waves");
   constexpr int SB = (BM + BN) * ROWB;
   int* s_tap = reinterpret_cast<int*>(smem + ST * SB);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -352,7 +358,7 @@ __device__ __forceinline__ void i8_glds_tile(const I8Args& a, const int bid, cha
   const int tm = a.nmajor ? bid - tn * tiles_m : bid / tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int taps = a.KH * a.KW;
-  const int grow = lane >> 3, lc = (lane & 7) ^ grow;
+  const int grow = lane / CPR, lc = (lane % CPR) ^ (grow % CPR);
 
   // Operand rows come in through buffer_load ... lds on range-checked descriptors (round 5):
   // an out-of-image tap, a channel tail or a row past M gets an offset past the descriptor's
@@ -369,7 +375,7 @@ __device__ __forceinline__ void i8_glds_tile(const I8Args& a, const int bid, cha
   int tapbits = 0;
 #pragma unroll
   for (int i = 0; i < GA; ++i) {
-    const int m = m0 + wid * (BM / NW) + i * 8 + grow;
+    const int m = m0 + wid * (BM / NW) + i * RPG + grow;
     const int pm = m < M ? (a.perm ? a.perm[m] : m) : -1;
     const int mm = pm >= 0 ? pm : 0;
     const int b = mm / (a.OH * a.OW);
@@ -383,7 +389,7 @@ __device__ __forceinline__ void i8_glds_tile(const I8Args& a, const int bid, cha
   unsigned boff[GB];
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
-    const int n = n0 + wid * (BN / NW) + j * 8 + grow;
+    const int n = n0 + wid * (BN / NW) + j * RPG + grow;
     boff[j] = n < a.Cout ? (unsigned)(n * taps * a.Cin + lc * 16) : kOOB;
   }
   if (tid == 0) *s_tap = 0;
@@ -395,16 +401,16 @@ __device__ __forceinline__ void i8_glds_tile(const I8Args& a, const int bid, cha
   int ntap = 0;
   for (int t = 0; t < taps; ++t)
     if ((tapmask >> t) & 1) { tl |= (unsigned long long)t << (4 * ntap); ++ntap; }
-  const int cch = cdiv_dev(a.Cin, 128);
+  const int cch = cdiv_dev(a.Cin, KB);
   const int total = ntap * cch;
-  const int cin_left = a.Cin - lc * 16;  // this lane's 16-byte chunk exists while 128 * c < cin_left
+  const int cin_left = a.Cin - lc * 16;  // this lane's 16-byte chunk exists while KB * c < cin_left
 
   int is_tap = 0, is_c = 0;
   auto issue = [&](int stage) {
     const int t = (int)((tl >> (4 * is_tap)) & 15);
     const int ty = a.KW == 3 ? (t * 11) >> 5 : a.KW == 1 ? t : t / a.KW;
     const int dy = (ty - a.KH / 2) * a.dil, dx = (t - ty * a.KW - a.KW / 2) * a.dil;
-    const int cb = is_c * 128;
+    const int cb = is_c * KB;
     // branch-free range handling: bit 31 set = past the descriptor's end (reads zeros)
     const unsigned cbad = (unsigned)(cin_left - cb - 1) & kOOB;
     const unsigned doff = (unsigned)((dy * a.IW + dx) * a.Cin + cb);
@@ -412,14 +418,14 @@ __device__ __forceinline__ void i8_glds_tile(const I8Args& a, const int bid, cha
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
       const unsigned vo = (aoff[i] + doff) | cbad | (((unsigned)nrtap[i] << (31 - t)) & kOOB);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_ptr_t)(sA + (wid * (BM / NW) + i * 8) * ROWB), 16, vo, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_ptr_t)(sA + (wid * (BM / NW) + i * RPG) * ROWB), 16, vo, 0, 0, 0);
     }
     char* sB = sA + BM * ROWB;
     const unsigned wofs = (unsigned)(t * a.Cin + cb);
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
       const unsigned vo = (boff[j] + wofs) | cbad;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rwt, (lds_ptr_t)(sB + (wid * (BN / NW) + j * 8) * ROWB), 16, vo, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rwt, (lds_ptr_t)(sB + (wid * (BN / NW) + j * RPG) * ROWB), 16, vo, 0, 0, 0);
     }
     if (++is_c == cch) { is_c = 0; ++is_tap; }
   };
@@ -441,23 +447,24 @@ __device__ __forceinline__ void i8_glds_tile(const I8Args& a, const int bid, cha
     const char* sB = sA + BM * ROWB;
     // both K halves' fragments are requested up front: the second half's reads land
     // under the first half's MFMAs
-    i32x4v bfr[2][MT], afr[2][NT];
+    constexpr int KST = KB / 64;  // MFMA k-steps per stage
+    i32x4v bfr[KST][MT], afr[KST][NT];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < KST; ++ks) {
       const int kc = ks * 4 + kq;
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         const int r = wm * 16 * MT + i * 16 + r16;
-        bfr[ks][i] = *reinterpret_cast<const i32x4v*>(sA + r * ROWB + ((kc ^ (r & 7)) << 4));
+        bfr[ks][i] = *reinterpret_cast<const i32x4v*>(sA + r * ROWB + ((kc ^ (r % CPR)) << 4));
       }
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         const int n = wn * 16 * NT + j * 16 + r16;
-        afr[ks][j] = *reinterpret_cast<const i32x4v*>(sB + n * ROWB + ((kc ^ (n & 7)) << 4));
+        afr[ks][j] = *reinterpret_cast<const i32x4v*>(sB + n * ROWB + ((kc ^ (n % CPR)) << 4));
       }
     }
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < KST; ++ks)
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -471,13 +478,13 @@ __device__ __forceinline__ void i8_glds_tile(const I8Args& a, const int bid, cha
                       reinterpret_cast<int*>(smem) + wid * 16 * kEpPitch, lane);
 }
 
-template <int MT, int NT, int WM, int WN>
+template <int MT, int NT, int WM, int WN, int KB = 128>
 __global__ __launch_bounds__(64 * WM * WN) void conv_i8_glds_kernel(I8Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN;
   const int M = a.perm ? a.Mp : a.B * a.OH * a.OW;
   const int tiles = cdiv_dev(M, BM) * cdiv_dev(a.Cout, BN);
-  i8_glds_tile<MT, NT, WM, WN>(a, xcd_remap(blockIdx.x, tiles), smem);
+  i8_glds_tile<MT, NT, WM, WN, KB>(a, xcd_remap(blockIdx.x, tiles), smem);
 }
 
 constexpr int kMaxI8Group = 4;
@@ -514,20 +521,22 @@ void launch_i8_glds_group(const I8GroupArgs& ga, int nblocks, hipStream_t s) {
   check_launch("conv_i8_glds_group");
 }
 
-template <int MT, int NT, int WM, int WN>
+template <int MT, int NT, int WM, int WN, int KB = 128>
 void launch_i8_glds(const I8Args& a, hipStream_t s) {
   constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN;
   const int M = a.perm ? a.Mp : a.B * a.OH * a.OW;
   const int grid = cdiv(M, BM) * cdiv(a.Cout, BN);
-  const size_t lds = 2 * (size_t)(BM + BN) * 128 + 16;
+  // the epilogue stages every wave's 16 x 64 int32 tile in the ring's bytes
+  static_assert(2 * (BM + BN) * KB >= WM * WN * 16 * kEpPitch * 4, "epilogue staging exceeds the ring");
+  const size_t lds = 2 * (size_t)(BM + BN) * KB + 16;
   static bool attr = false;
   if (!attr) {
-    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_i8_glds_kernel<MT, NT, WM, WN>),
+    check(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_i8_glds_kernel<MT, NT, WM, WN, KB>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
           "conv_i8_glds attr");
     attr = true;
   }
-  hipLaunchKernelGGL((conv_i8_glds_kernel<MT, NT, WM, WN>), dim3(grid), dim3(64 * WM * WN), lds, s, a);
+  hipLaunchKernelGGL((conv_i8_glds_kernel<MT, NT, WM, WN, KB>), dim3(grid), dim3(64 * WM * WN), lds, s, a);
   check_launch("conv_i8_glds");
 }
 
@@ -981,7 +990,7 @@ void conv_i8(const ConvI8Params& p, hipStream_t s) {
     v = v == 12 ? 7 : 2;
   }
   if (v == 0) v = (glds_ok && p.Cout >= 64 && M >= 8192) ? (p.Cout >= 256 ? 3 : 2) : 1;
-  const bool glds_v = (v >= 2 && v <= 4) || v == 7 || v == 8;
+  const bool glds_v = (v >= 2 && v <= 4) || v == 7 || v == 8 || (v >= 18 && v <= 20);
   if (glds_v && !glds_ok) throw std::invalid_argument("conv_i8: LDS-DMA variants need <= 16 taps and < 2 GiB operands");
   if (p.perm && !glds_v) throw std::invalid_argument("conv_i8: a row permutation needs an LDS-DMA variant");
   if (v == 5 || v == 6 || v == 10 || v == 11) {
@@ -997,6 +1006,10 @@ void conv_i8(const ConvI8Params& p, hipStream_t s) {
     case 4: launch_i8_glds<4, 4, 4, 2>(a, s); return;
     case 7: launch_i8_glds<5, 4, 2, 2>(a, s); return;
     case 8: launch_i8_glds<3, 4, 2, 2>(a, s); return;
+    // 64-byte K rows (one k-step per stage, half the LDS): 128 x 128 / 128 x 256 / 256 x 128
+    case 18: launch_i8_glds<4, 4, 2, 2, 64>(a, s); return;
+    case 19: launch_i8_glds<4, 4, 2, 4, 64>(a, s); return;
+    case 20: launch_i8_glds<4, 4, 4, 2, 64>(a, s); return;
     default: break;
   }
   if (p.Cout <= 32) launch_i8<4, 1>(a, s);

@@ -26,7 +26,8 @@ from .deeplab import DeepLabV3, synthetic_normalized
 from .quant import calibrate, pack_int8
 
 
-_I8_VARIANTS = (1, 2, 3, 4, 7, 8)  # register-fed, LDS-DMA 128x128 / 128x256 / 256x128 / 160x128 / 96x128
+_I8_VARIANTS = (1, 2, 3, 4, 7, 8, 18, 19, 20)  # register-fed, LDS-DMA 128x128 / 128x256 / 256x128 /
+# 160x128 / 96x128, and 18-20: 128x128 / 128x256 / 256x128 with 64-byte K rows per stage
 # (12 / 13, the n-tile-major orders, timed within noise of 7 / 2 or slower: not offered)
 # + 5 / 6: streaming 1x1 (weights resident per channel block, prefetched pixel tiles; 6 with
 # a narrower channel block) where it fits

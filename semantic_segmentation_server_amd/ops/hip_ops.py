@@ -795,12 +795,14 @@ def conv_i8(x, w8, scale, bias, out, *, B, IH, IW, Cin, OH, OW, Cout, k=1, strid
             out_scale=None, variant=0, perm=None) -> torch.Tensor:
     """int8 NHWC conv. out int8 (out_scale given: v / out_scale rounded) or bf16.
     variant: 0 auto, 1 register-fed, 2/3/4/7/8 LDS-DMA 128x128 / 128x256 / 256x128 / 160x128 /
-    96x128 tiles, 12 / 13 = 7 / 2 in n-tile-major block order,
+    96x128 tiles, 12 / 13 = 7 / 2 in n-tile-major block order, 18 / 19 / 20 = 2 / 3 / 4 with
+    64-byte K rows per LDS stage (half the LDS: more workgroups per CU),
     5 / 6 / 10 / 11 streaming 1x1 (stride 1; conv_i8_1x1_ok; the widest fitting channel block,
     then narrower ones).
     ``perm`` (LDS-DMA variants only; ``tap_group_perm`` with the variant's tile height): GEMM
     rows -> output pixels, tiles of equal tap validity."""
-    if variant not in (0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 13) or (variant in (2, 3, 4, 7, 8, 12, 13) and k * k > 16):
+    if variant not in (0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 13, 18, 19, 20) or (
+            variant in (2, 3, 4, 7, 8, 12, 13, 18, 19, 20) and k * k > 16):
         raise ValueError("conv_i8: bad variant")
     Mp = 0
     if perm is not None:
@@ -835,7 +837,8 @@ def conv_i8(x, w8, scale, bias, out, *, B, IH, IW, Cin, OH, OW, Cout, k=1, strid
 
 # int8 LDS-DMA tile shapes (BM, BN) by conv_i8 variant
 I8_TILE = {2: (128, 128), 3: (128, 256), 4: (256, 128), 7: (160, 128), 8: (96, 128),
-           12: (160, 128), 13: (128, 128)}  # 12 / 13: 7 / 2 with n-tile-major block order
+           12: (160, 128), 13: (128, 128),  # 12 / 13: 7 / 2 with n-tile-major block order
+           18: (128, 128), 19: (128, 256), 20: (256, 128)}  # 2 / 3 / 4 with 64-byte K rows
 
 
 def _check_perm(perm, BM, M, who):

@@ -1296,7 +1296,7 @@ def test_pw_conv_fp16_out():
     assert _rel(out.float().cpu(), ref) < 2e-3
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 7, 8, 12, 13])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 7, 8, 12, 13, 18, 19, 20])
 @pytest.mark.parametrize("Cin,Cout,k,stride,dil,res,mode", [
     (64, 256, 1, 1, 1, True, "i8"), (256, 64, 3, 2, 1, False, "i8"), (512, 512, 3, 1, 2, False, "i8"),
     (256, 19, 1, 1, 1, False, "bf16"), (1024, 256, 1, 1, 1, False, "i8"), (208, 136, 3, 1, 3, True, "i8")])
@@ -1334,6 +1334,28 @@ def test_conv_i8(Cin, Cout, k, stride, dil, res, mode, variant):
                   Cout=Cout, k=k, stride=stride, dil=dil, act="relu", variant=variant)
         torch.cuda.synchronize()
         assert _rel(_nchw(out).cpu(), ref) < 5e-3
+
+
+def test_conv_i8_k64_rows_bit_identical():
+    """64-byte K rows per LDS stage (variants 18-20) compute the same exact int32 sums and
+    the same epilogue as the 128-byte form of the same tile (2 / 3 / 4): byte-identical."""
+    K = _hip()
+    g = torch.Generator().manual_seed(37)
+    B, H = 2, 21
+    for Cin, Cout, k, dil in ((64, 256, 1, 1), (208, 512, 1, 1), (512, 256, 3, 2)):
+        x = torch.randint(-127, 128, (B, H, H, Cin), generator=g, dtype=torch.int32).to(torch.int8).to(DEV)
+        w = torch.randint(-127, 128, (Cout, k, k, Cin), generator=g, dtype=torch.int32).to(torch.int8).to(DEV)
+        sc = (torch.rand(Cout, generator=g) * 1e-4).to(DEV)
+        bi = torch.randn(Cout, generator=g).to(DEV)
+        outs = {}
+        for v in (2, 3, 4, 18, 19, 20):
+            o = torch.full((B, H, H, Cout), 99, dtype=torch.int8, device=DEV)
+            K.conv_i8(x, w, sc, bi, o, B=B, IH=H, IW=H, Cin=Cin, OH=H, OW=H, Cout=Cout, k=k, dil=dil,
+                      act="relu", out_scale=0.05, variant=v)
+            outs[v] = o
+        torch.cuda.synchronize()
+        for v, base in ((18, 2), (19, 3), (20, 4)):
+            assert torch.equal(outs[v].cpu(), outs[base].cpu()), (Cin, k, v)
 
 
 @pytest.mark.parametrize("variant", [7, 2, 8])
