@@ -511,7 +511,9 @@ __global__ __launch_bounds__(256) void stem_block0_kernel(SB0Args a) {
     toff[m] = tp < 9 ? ((tp / 3) * IWT + tp % 3) * 4 : -1;
   }
   __syncthreads();
-  const f16x4 z4 = {0, 0, 0, 0}, s4 = {6, 6, 6, 6};
+  // ReLU6 as a [0, 1] clamp (ops/hip_ops.pack_stem_block0 packs the stem / 6, the depthwise
+  // bias / 6 and the projection x 6): the clamps fold into the conversion / the last fma
+  const f16x4 z4 = {0, 0, 0, 0}, s4 = {1, 1, 1, 1};
   const s16x4 zs = {0, 0, 0, 0};
   for (int gi = wid; gi < s_groups; gi += 4) {
     const int sp = gi * 16 + r16;
@@ -541,7 +543,7 @@ __global__ __launch_bounds__(256) void stem_block0_kernel(SB0Args a) {
   const f16x8 bdv = *reinterpret_cast<const f16x8*>(a.bd + kq * 8);
   const f16x8 af = *reinterpret_cast<const f16x8*>(a.wp + (size_t)r16 * 32 + kq * 8);
   __syncthreads();
-  const f16x8 h0 = {0, 0, 0, 0, 0, 0, 0, 0}, h6 = {6, 6, 6, 6, 6, 6, 6, 6};
+  const f16x8 h0 = {0, 0, 0, 0, 0, 0, 0, 0}, h6 = {1, 1, 1, 1, 1, 1, 1, 1};  // [0, 1]: see s4
 #pragma unroll
   for (int g = 0; g < GPW; ++g) {
     const int p = (wid * GPW + g) * 16 + r16;

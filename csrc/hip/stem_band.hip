@@ -205,8 +205,11 @@ __global__ __launch_bounds__(64 * NW) void stem_band_kernel(StemBandArgs a) {
   const int xl = g * 16 + r16;                // local output column (reads stem cols xl..xl+2)
   const bool xv = xl < twv;
   const int xc = xv ? xl : 0;
-  const f16x4 z4 = {0, 0, 0, 0}, s4 = {6, 6, 6, 6};
-  const f16x8 h0 = {0, 0, 0, 0, 0, 0, 0, 0}, h6 = {6, 6, 6, 6, 6, 6, 6, 6};
+  // ReLU6 as a [0, 1] clamp (stem / 6, depthwise bias / 6, projection x 6 in the packing,
+  // ops/hip_ops.pack_stem_block0): the stem's and the depthwise's clamps fold into the
+  // f32 -> f16 conversion and the last fma (48 of the unrolled loop's ~360 VALU were min / max)
+  const f16x4 z4 = {0, 0, 0, 0}, s4 = {1, 1, 1, 1};
+  const f16x8 h0 = {0, 0, 0, 0, 0, 0, 0, 0}, h6 = {1, 1, 1, 1, 1, 1, 1, 1};
   f16x8 D[3];
 #pragma unroll
   for (int s_ = 0; s_ < 3; ++s_) D[s_] = bdv;

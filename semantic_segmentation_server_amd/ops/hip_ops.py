@@ -638,15 +638,18 @@ def pack_stem_block0(stem, wd, bd, wp, bp, device) -> dict:
     """Weights of the fused stem + block-0 kernel. stem: ConvBNAct (3x3 s2, 3 -> 32);
     wd [32, 3, 3], bd [32], wp [16, 32], bp [16] (BN folded)."""
     w, b = stem.fold()                                   # [32, 3, 3, 3] (RGB in)
+    # both ReLU6 as [0, 1] clamps (relu6(v) = 6 clamp(v / 6, 0, 1)): the stem and the
+    # depthwise bias are packed / 6 and the projection x 6, so the kernels' clamps fold into
+    # the f32 -> f16 conversion and the depthwise's last fma (no min / max instructions)
     ws = torch.zeros(32, 12, 4, dtype=torch.float32)     # K = tap*4 + c: 3 x 16x16x16 MFMA
-    ws[:, :9, :3] = w.permute(0, 2, 3, 1).reshape(32, 9, 3)
+    ws[:, :9, :3] = w.float().permute(0, 2, 3, 1).reshape(32, 9, 3) / 6.0
     ws = ws.reshape(32, 48)
     f32 = dict(dtype=torch.float32, device=device)
     return dict(
-        ws=ws.to(device=device, dtype=torch.bfloat16).contiguous(), bs=b.to(**f32).contiguous(),
+        ws=ws.to(device=device, dtype=torch.bfloat16).contiguous(), bs=(b.float() / 6.0).to(**f32).contiguous(),
         wd_h=wd.reshape(32, 9).t().contiguous().to(device=device, dtype=torch.float16),
-        bd_h=bd.to(device=device, dtype=torch.float16).contiguous(),
-        wp_h=wp.to(device=device, dtype=torch.float16).contiguous(),
+        bd_h=(bd.float() / 6.0).to(device=device, dtype=torch.float16).contiguous(),
+        wp_h=(wp.float() * 6.0).to(device=device, dtype=torch.float16).contiguous(),
         bp=bp.to(**f32).contiguous(), Cout=int(wp.shape[0]))
 
 
