@@ -391,7 +391,17 @@ __global__ __launch_bounds__(256) void stem_mfma_ws_kernel(SMArgs a) {
     for (int m = 0; m < KG; ++m) acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wf[m], xf[m], acc, 0, 0, 0);
     if (!valid) continue;
     const size_t pix = ((size_t)b * a.OH + oy) * a.OW + ox;
-    if (a.out_inv_scale > 0.f) {
+    if (a.out_inv_scale > 0.f && a.act == ACT_RELU) {
+      // relu + int8: the codes are rint(clamp(acc * s, 0, 127)) -- one med3 and one rounding
+      // pack per value (v_cvt_pk_u8_f32, nearest even like rintf; clamping to integer bounds
+      // before or after the rounding gives the same code), non-negative so the unsigned
+      // bytes are the signed ones. The float chain below took ~7 VALU per value.
+      unsigned w = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        w = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(acc[q] * a.out_inv_scale, 0.f, 127.f), q, w);
+      *reinterpret_cast<unsigned*>(static_cast<int8_t*>(a.out) + pix * Cout + n) = w;
+    } else if (a.out_inv_scale > 0.f) {
       char4 o;
       o.x = (signed char)fminf(fmaxf(rintf(apply_act(acc[0], a.act) * a.out_inv_scale), -127.f), 127.f);
       o.y = (signed char)fminf(fmaxf(rintf(apply_act(acc[1], a.act) * a.out_inv_scale), -127.f), 127.f);

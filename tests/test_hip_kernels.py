@@ -352,6 +352,19 @@ def test_stem_fused_preprocess(cam, k, cout):
                     out_scale=0.05, tile=tile, per_wave=pw)
         torch.cuda.synchronize()
         assert (_nchw(o8).cpu().float() - exp).abs().float().mean() < 0.5, tile
+    if (k, cout) == (7, 64):
+        # relu + int8 (the config-4 stem): the per-wave kernel's med3 + v_cvt_pk_u8 epilogue
+        # gives the same codes as the all-blocks kernel's float chain (same MFMA sums)
+        outs = []
+        for tile, pw in (((8, 16), False), ((32, 32), True)):
+            o8 = torch.full((2, OH, OW, cout), 99, dtype=torch.int8, device=DEV)
+            K.stem_mfma(frames.to(DEV), torch.tensor(lx, device=DEV), torch.tensor(ly, device=DEV), wpk,
+                        b.to(DEV), o8, H=H, W=W, OH=OH, OW=OW, Cout=cout, k=k, stride=2, act="relu",
+                        out_scale=0.05, tile=tile, per_wave=pw)
+            outs.append(o8)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0].cpu(), outs[1].cpu())
+        assert int(outs[1].min()) >= 0
 
 
 def test_maxpool_gap_matvec():
